@@ -1,0 +1,232 @@
+#!/usr/bin/env python3
+"""YOLOv2-tiny 416x416 images/s on 1..8 MI355X through the fused HIP plan.
+
+Workload (BASELINE.json configs[2]/[3]): a step is one forward of YOLOv2-tiny (9 convs as
+im2col + fp32-MFMA GEMM with fused bias/BN/leaky, 6 max pools) over this GPU's batch of 64
+synthetic 416x416x3 fp32 frames already resident in HBM, followed by the gather of all
+ranks' [64,13,13,125] outputs to rank 0 over RCCL.  Weights (random-init, tiny-yolo-voc
+channel plan, synth.py) are broadcast from rank 0 once before timing.  Weak scaling:
+64 frames per GPU at every N.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--batch 64]
+N>1 is launched by the driver through torch.distributed.run (one process per GPU); when
+started by hand with --gpus N>1 it relaunches itself that way.
+
+Rank 0 prints one JSON line: images/s for the whole job, plus
+  roofline      the dominant kernel (conv7's GEMM, M=64*169, N=1024, K=9216): algorithmic
+                2*M*N*K flops / its mean HIP-event duration inside the timed region, vs
+                the 157.3 TFLOP/s fp32 MFMA peak (MI355X_MICROARCH.md); traffic from the
+                committed PMC summary (profiles/pmc_summary.json) when present;
+  conv_mfma     all 9 conv GEMMs together: flops / summed GEMM time as % of fp32 peak;
+  cpu_baseline  the numpy/OpenBLAS restatement of the reference's OpenBLAS engine
+                (oracle/ref_numpy.py: im2col + sgemm, batch 1 per image) timed on this
+                host's cores on a bounded sample (N=1, rank 0 only).
+"""
+import argparse
+import json
+import os
+import socket
+import subprocess
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(REPO, "dnn-inference-engine_amd")
+ORACLE = os.path.join(REPO, "oracle")
+sys.path.insert(0, PKG)
+
+FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md, dense fp32 matrix (= vector) peak
+HBM_PEAK_GBS = 8000.0
+DOMINANT = "conv7.gemm"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=64, help="frames per GPU")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="bound on the CPU-baseline sample")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--kernels", action="store_true", help="add the per-kernel table to the JSON")
+    return ap.parse_args()
+
+
+def relaunch(args):
+    """--gpus N>1 without torch.distributed.run's environment: start it as a child
+    (nothing has touched the GPU yet in this process)."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    sys.exit(subprocess.call(cmd))
+
+
+def pmc_traffic(kernel):
+    p = os.path.join(REPO, "profiles", "pmc_summary.json")
+    try:
+        with open(p) as f:
+            d = json.load(f)
+        return d.get("kernels", {}).get(kernel, {}).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def cpu_baseline(seconds):
+    """numpy/OpenBLAS restatement of proj3's OpenBLAS engine: per image im2col + fp32 sgemm
+    (numpy's bundled OpenBLAS), bias/bn/leaky/pool in numpy — the same work per image as
+    dnn_openblas.c:160-194 plus its element-wise passes.  Bounded sample."""
+    sys.path.insert(0, ORACLE)
+    import numpy as np
+    import ref_numpy as R
+    import synth
+    try:
+        from threadpoolctl import threadpool_info
+        cores = max([i.get("num_threads", 1) for i in threadpool_info() if i.get("internal_api") == "openblas"]
+                    or [1])
+    except Exception:
+        cores = os.cpu_count() or 1
+    ws = synth.yolo_weights()
+    x = synth.frame(0)
+    R.yolo_forward(ws, x, acc=np.float32)  # warm
+    n, t0 = 0, time.perf_counter()
+    times = []
+    while True:
+        t = time.perf_counter()
+        R.yolo_forward(ws, x, acc=np.float32)
+        times.append(time.perf_counter() - t)
+        n += 1
+        if (time.perf_counter() - t0 > seconds and n >= 3) or n >= 200:
+            break
+    med = sorted(times)[len(times) // 2]
+    return {"value": round(1.0 / med, 3), "unit": "images/s", "cores": int(cores), "kind": "port",
+            "sample": f"{n} single-frame YOLOv2-tiny forwards (median {med * 1e3:.0f} ms), "
+                      "oracle/ref_numpy.py im2col + numpy/OpenBLAS sgemm, batch 1 like dnn_openblas.c"}
+
+
+def main():
+    args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        relaunch(args)
+
+    import torch
+    import torch.distributed as tdist
+
+    import dist as D
+    import dnn_hip
+    import synth
+    import yolo_graph
+
+    rank, local_rank, world = D.env_rank()
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        D.init("nccl", device=dev)
+
+    B = args.batch
+    # rank 0 holds the weights; the other ranks only lay the plan out and receive the
+    # packed buffer by broadcast
+    ws = synth.yolo_weights() if rank == 0 else yolo_graph.zero_weights_like(synth.yolo_weights())
+    g, _ = yolo_graph.build_graph(dnn_hip.DnnGraphBuilder, ws, in_shape=(B, 416, 416, 3))
+    entries = dnn_hip.lower_graph(g)
+    wbytes, sbytes = dnn_hip.Plan.memory(B, (416, 416, 3), entries)
+    wbuf = torch.empty(wbytes, dtype=torch.uint8, device=dev)
+    sbuf = torch.empty(max(sbytes, 1), dtype=torch.uint8, device=dev)
+    plan = dnn_hip.Plan(B, (416, 416, 3), entries, device=local_rank, weights_ptr=wbuf.data_ptr(),
+                        workspace_ptr=sbuf.data_ptr(), upload=(rank == 0))
+    torch.cuda.synchronize()
+    D.broadcast_weights(wbuf, src=0)
+    torch.cuda.synchronize()
+
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(1234 + rank)
+    frames = torch.rand((B, 416, 416, 3), generator=gen, device=dev, dtype=torch.float32)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+
+    def compute(inp, out, n):
+        plan.run_device(n, inp.data_ptr(), out.data_ptr(), stream)
+
+    runner = D.ShardedRunner(compute, B * world, (416, 416, 3), (13, 13, 125), dev)
+
+    for _ in range(args.warmup):
+        runner.step(frames)
+    torch.cuda.synchronize()
+    if world > 1:
+        tdist.barrier()
+
+    plan.timing_begin(args.steps)
+    torch.cuda.synchronize()
+    if world > 1:
+        tdist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        full = runner.step(frames)
+    torch.cuda.synchronize()
+    if world > 1:
+        tdist.barrier()
+    elapsed = time.perf_counter() - t0
+    ms, cnt = plan.timing_end()
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    if rank == 0:
+        assert full is not None and full.shape[0] == B * world
+        kinfo = plan.kernels()
+        by_name = {k["name"]: (k, ms[i], cnt[i]) for i, k in enumerate(kinfo)}
+        k, kms, kc = by_name[DOMINANT]
+        avg_s = kms / max(kc, 1) / 1e3
+        achieved = k["flops"] / avg_s / 1e12
+        traffic = pmc_traffic(DOMINANT)
+        gemm_fl = sum(v[0]["flops"] for n, v in by_name.items() if n.endswith(".gemm"))
+        gemm_s = sum(v[1] / max(v[2], 1) for n, v in by_name.items() if n.endswith(".gemm")) / 1e3
+        conv67 = [by_name["conv6.gemm"], by_name["conv7.gemm"]]
+        c67_fl = sum(v[0]["flops"] for v in conv67)
+        c67_s = sum(v[1] / max(v[2], 1) for v in conv67) / 1e3
+        total_kernel_ms = sum(m / max(c, 1) for m, c in zip(ms, cnt))
+        value = B * world * args.steps / elapsed
+        res = {
+            "metric": "YOLOv2-tiny 416×416 images/sec at 1/2/4/8 GPU; conv MFMA % of fp32 peak",
+            "value": round(value, 2),
+            "unit": "images/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32",
+            "data": "synthetic (uniform [0,1) frames, random-init weights, tiny-yolo-voc channel plan)",
+            "config": {"workload": "YOLOv2-tiny forward, 416x416x3 NHWC fp32, 64 frames per GPU in HBM, "
+                                   "outputs gathered to rank 0",
+                       "model": "yolov2-tiny (9 conv, 6 maxpool)", "global_batch": B * world,
+                       "per_gpu_batch": B, "seq_len": None, "parallelism": f"dp{world}"},
+            "roofline": {"kernel": DOMINANT, "bound": "mfma", "achieved": round(achieved, 2),
+                         "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
+                         "flops_per_launch": k["flops"], "avg_launch_ms": round(avg_s * 1e3, 4)},
+            "conv_mfma": {"all_gemms_pct_fp32_peak": round(100 * gemm_fl / gemm_s / 1e12 / FP32_MFMA_PEAK_TFLOPS, 2),
+                          "conv6_conv7_pct_fp32_peak": round(100 * c67_fl / c67_s / 1e12 / FP32_MFMA_PEAK_TFLOPS, 2),
+                          "net_pct_fp32_peak": round(100 * 6.971e9 * value / world / 1e12 / FP32_MFMA_PEAK_TFLOPS,
+                                                     2)},
+            "kernel_ms_per_step": round(total_kernel_ms, 4),
+        }
+        if args.kernels:
+            res["kernels"] = {n: {"ms": round(v[1] / max(v[2], 1), 4),
+                                  "tflops": round(v[0]["flops"] / (v[1] / max(v[2], 1) / 1e3) / 1e12, 2)
+                                  if v[0]["flops"] else None,
+                                  "gbs": round(v[0]["bytes"] / (v[1] / max(v[2], 1) / 1e3) / 1e9, 1)}
+                              for n, v in by_name.items()}
+        res["cpu_baseline"] = None if (world > 1 or args.no_cpu) else cpu_baseline(args.cpu_seconds)
+        print(json.dumps(res), flush=True)
+
+    plan.close()
+    if world > 1:
+        tdist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

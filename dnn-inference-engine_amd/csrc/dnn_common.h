@@ -1,0 +1,103 @@
+// Shared declarations for the MI355X (gfx950) Conv2D hot path.
+// Layout conventions: activations NHWC fp32 contiguous; conv weights
+// HWIO; the GEMM sees A = im2col rows [M = B*OH*OW][Kpad] with K order (kh, kw, ic) and
+// B = packed weights Bt[Npad][Kpad] (K contiguous), C = NHWC output [M][ldc].
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstddef>
+#include <cstdint>
+
+namespace dnnhip {
+
+// ---------------------------------------------------------------- errors
+void set_error(const char* fmt, ...);
+const char* last_error();
+
+#define DNN_HIP_TRY(x)                                                             \
+  do {                                                                             \
+    hipError_t e_ = (x);                                                           \
+    if (e_ != hipSuccess) {                                                        \
+      ::dnnhip::set_error("%s:%d %s -> %s", __FILE__, __LINE__, #x,               \
+                          hipGetErrorString(e_));                                  \
+      return -1;                                                                   \
+    }                                                                              \
+  } while (0)
+
+#define DNN_REQUIRE(cond, ...)                                                     \
+  do {                                                                             \
+    if (!(cond)) {                                                                 \
+      ::dnnhip::set_error(__VA_ARGS__);                                            \
+      return -2;                                                                   \
+    }                                                                              \
+  } while (0)
+
+// ---------------------------------------------------------------- geometry
+// TF SAME/VALID output size and front pad (proj3/dnn_openblas.py:127-142).
+void out_pads(int in, int k, int s, int same, int* out, int* pad_front);
+
+struct ConvGeom {
+  int B, H, W, C;        // input (unpadded) NHWC
+  int OH, OW;            // output spatial
+  int kh, kw, sh, sw;    // window / stride
+  int pt, pl;            // front pads (zero fill)
+  int K, Kpad;           // K = kh*kw*C, Kpad = multiple of the GEMM's BK
+};
+
+struct PoolGeom {
+  int B, H, W, C, OH, OW, kh, kw, sh, sw, pt, pl;  // pads filled with -FLT_MAX
+  // Channels c < gt_below use `m > x ? m : x` (_mm256_max_ps, dnn_avx.c:392-405); the rest
+  // use the C macro `m >= x ? m : x` (dnn_openblas.c:8,220).  They differ only on +-0/NaN.
+  int gt_below;
+};
+
+// Per-output-channel epilogue of a conv: conv -> bias_add -> batch_norm -> leaky_relu,
+// evaluated in exactly the reference's operation order (proj3/dnn_openblas.c:9-65,236-254).
+enum EpiFlags : int {
+  EPI_BIAS = 1,
+  EPI_BN = 2,          // ((v - mean) / sq) * gamma, sq = sqrtf(var + eps)
+  EPI_LEAKY_F64 = 4,   // v < 0 ? (float)(0.1 * (double)v) : v   (dnn_openblas.c:250)
+  EPI_LEAKY_F32 = 8,   // max(v, 0.1f * v)                       (dnn_avx.c:540-542)
+  EPI_BN_AB = 16,      // v * alpha - beta                       (dnn_avx.c:505-507)
+};
+
+struct EpiParams {
+  const float* bias;   // [Npad]
+  const float* mean;   // [Npad] (alpha for EPI_BN_AB)
+  const float* sq;     // [Npad] (beta for EPI_BN_AB)
+  const float* gamma;  // [Npad]
+  int flags;
+};
+
+// GEMM tile configurations (see kernels.hip). Each has its own BM/BN/BK.
+enum GemmCfg : int {
+  GEMM_256x16_K32 = 0,   // N <= 16 (conv0), MFMA 16x16x4
+  GEMM_256x32_K16 = 1,   // N <= 32 (conv1), MFMA 16x16x4
+  GEMM_128x64_K32 = 2,   // N <= 64, MFMA 32x32x2
+  GEMM_128x128_K32 = 3,  // wide layers, MFMA 32x32x2
+  GEMM_64x128_K32 = 4,   // wide layers with few M tiles, MFMA 32x32x2
+  GEMM_NUM_CFGS = 5,
+};
+int gemm_cfg_bm(int cfg);
+int gemm_cfg_bn(int cfg);
+int gemm_cfg_bk(int cfg);
+int choose_gemm_cfg(long long M, int N, int K);
+
+// ---------------------------------------------------------------- launchers
+// All launchers are asynchronous on `stream` and return 0 / negative on launch error.
+int launch_im2col(const float* in, float* col, const ConvGeom& g, hipStream_t stream);
+int launch_gemm(int cfg, const float* A, int lda, const float* Bt, int ldb, float* C, int ldc,
+                long long M, int N, int Kpad, const EpiParams& epi, hipStream_t stream);
+int launch_maxpool(const float* in, float* out, const PoolGeom& g, hipStream_t stream);
+// order 0: rows of w are (kh, kw, ic)  [HWIO flattened];  order 1: rows are (ic, kh, kw)
+// [proj3 kernel_r layout, dnn_openblas.py:166-167].  Output bt[Npad][Kpad] zero padded.
+int launch_pack_weights(const float* w, float* bt, int K, int N, int Kpad, int Npad, int order,
+                        int kh, int kw, int C, hipStream_t stream);
+// element-wise ops of the per-op ABI
+int launch_bias_add(const float* in, const float* b, float* out, long long n, int C, hipStream_t s);
+int launch_bn_mvg(const float* in, const float* mean, const float* sq, const float* gamma, float* out,
+                  long long n, int C, hipStream_t s);
+int launch_bn_ab(const float* in, const float* alpha, const float* beta, float* out, long long n,
+                 int C, hipStream_t s);
+int launch_leaky(const float* in, float* out, long long n, int f32_variant, hipStream_t s);
+
+}  // namespace dnnhip

@@ -1,0 +1,531 @@
+// Hand-written gfx950 kernels for YOLOv2-tiny's Conv2D hot path.
+//
+//   im2col      NHWC -> col[M][Kpad], K order (kh, kw, ic) so HWIO weights are already
+//               [K][N]; SAME padding by predication (no host np.pad). Reference semantics:
+//               proj3/dnn_openblas.c:135-158 (there K order is (ic, kh, kw) on a pre-padded
+//               input; the order is a private layout choice because weights are packed to match).
+//   gemm        C[M][N] = A[M][K] * B[K][N] on fp32 MFMA (v_mfma_f32_32x32x2_f32 or
+//               v_mfma_f32_16x16x4_f32), LDS double buffer, fused per-channel epilogue
+//               bias -> batch-norm -> leaky in the reference's order. Replaces
+//               cblas_sgemm(RowMajor,N,N,M,N,K,1,col,K,kernel_r,od,0,out,od)
+//               (proj3/dnn_openblas.c:184-192) and the bias/bn/leaky passes.
+//   maxpool     NHWC window max over a -FLT_MAX padded view (proj3/dnn_openblas.c:196-234,
+//               padding from proj3/dnn_openblas.py:232-235).
+//   element-wise bias_add / batch_norm / leaky_relu of the per-op ABI (dnn_openblas.c:9-65,
+//               236-254; dnn_avx.c:483-553).
+#include <hip/hip_runtime.h>
+#include <cfloat>
+#include "dnn_common.h"
+
+namespace dnnhip {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+static inline int ceil_div_i(long long a, long long b) { return (int)((a + b - 1) / b); }
+
+static int check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    set_error("launch %s: %s", what, hipGetErrorString(e));
+    return -1;
+  }
+  return 0;
+}
+
+// ============================================================================ im2col
+// One block = IM2COL_ROWS consecutive output pixels (rows of col). Per-row window origins
+// and per-K-column tap offsets are tabulated in LDS once per block, so the streaming loop
+// does no integer division by layer constants. Writes are fully coalesced (a block writes
+// IM2COL_ROWS*Kpad contiguous floats); reads are contiguous runs of ic floats per tap.
+constexpr int IM2COL_ROWS = 32;
+constexpr int IM2COL_THREADS = 256;
+constexpr int IM2COL_MAX_KQ = 2560;  // Kpad/VEC entries of the tap table (Kpad <= 10240)
+
+template <int VEC>
+__global__ void __launch_bounds__(IM2COL_THREADS)
+im2col_nhwc_kernel(const float* __restrict__ in, float* __restrict__ col, ConvGeom g, long long M) {
+  __shared__ int s_off[IM2COL_MAX_KQ];   // (dy*W + dx)*C + c relative to the window origin
+  __shared__ int s_dydx[IM2COL_MAX_KQ];  // (dy << 16) | dx, or -1 for K padding columns
+  __shared__ long long s_base[IM2COL_ROWS];
+  __shared__ int s_iy[IM2COL_ROWS];
+  __shared__ int s_ix[IM2COL_ROWS];
+
+  const int kq = g.Kpad / VEC;
+  for (int k4 = threadIdx.x; k4 < kq; k4 += IM2COL_THREADS) {
+    int k = k4 * VEC;
+    if (k < g.K) {
+      int tap = k / g.C, c = k - tap * g.C;
+      int dy = tap / g.kw, dx = tap - dy * g.kw;
+      s_off[k4] = (dy * g.W + dx) * g.C + c;
+      s_dydx[k4] = (dy << 16) | dx;
+    } else {
+      s_off[k4] = 0;
+      s_dydx[k4] = -1;
+    }
+  }
+  const long long m0 = (long long)blockIdx.x * IM2COL_ROWS;
+  if (threadIdx.x < IM2COL_ROWS) {
+    long long m = m0 + threadIdx.x;
+    if (m >= M) m = M - 1;
+    int ox = (int)(m % g.OW);
+    long long t = m / g.OW;
+    int oy = (int)(t % g.OH);
+    int b = (int)(t / g.OH);
+    int iy0 = oy * g.sh - g.pt, ix0 = ox * g.sw - g.pl;
+    s_iy[threadIdx.x] = iy0;
+    s_ix[threadIdx.x] = ix0;
+    s_base[threadIdx.x] = (((long long)b * g.H + iy0) * g.W + ix0) * g.C;
+  }
+  __syncthreads();
+
+  const int rows = (int)((M - m0) < IM2COL_ROWS ? (M - m0) : IM2COL_ROWS);
+  const int total = rows * kq;
+  float* dst = col + m0 * g.Kpad;
+  for (int idx = threadIdx.x; idx < total; idx += IM2COL_THREADS) {
+    int r = idx / kq;
+    int k4 = idx - r * kq;
+    int dd = s_dydx[k4];
+    int iy = s_iy[r] + (dd >> 16);
+    int ix = s_ix[r] + (dd & 0xffff);
+    bool ok = dd >= 0 && (unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W;
+    const float* src = in + s_base[r] + s_off[k4];
+    if constexpr (VEC == 4) {
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (ok) v = *reinterpret_cast<const float4*>(src);
+      reinterpret_cast<float4*>(dst)[idx] = v;
+    } else {
+      dst[idx] = ok ? *src : 0.f;
+    }
+  }
+}
+
+int launch_im2col(const float* in, float* col, const ConvGeom& g, hipStream_t stream) {
+  long long M = (long long)g.B * g.OH * g.OW;
+  if (M == 0) return 0;
+  const bool vec = (g.C % 4) == 0 && (g.Kpad % 4) == 0;
+  const int kq = vec ? g.Kpad / 4 : g.Kpad;
+  if (kq > IM2COL_MAX_KQ) {
+    set_error("im2col: Kpad=%d exceeds the tap table (%d)", g.Kpad, IM2COL_MAX_KQ * (vec ? 4 : 1));
+    return -2;
+  }
+  dim3 grid(ceil_div_i(M, IM2COL_ROWS));
+  if (vec)
+    hipLaunchKernelGGL(im2col_nhwc_kernel<4>, grid, dim3(IM2COL_THREADS), 0, stream, in, col, g, M);
+  else
+    hipLaunchKernelGGL(im2col_nhwc_kernel<1>, grid, dim3(IM2COL_THREADS), 0, stream, in, col, g, M);
+  return check_launch("im2col");
+}
+
+// ============================================================================ GEMM
+__device__ __forceinline__ float apply_epilogue(float v, float bias, float mean, float sq, float gamma,
+                                                int flags) {
+  if (flags & EPI_BIAS) v = v + bias;
+  if (flags & EPI_BN) v = ((v - mean) / sq) * gamma;
+  if (flags & EPI_BN_AB) v = v * mean - sq;
+  if (flags & EPI_LEAKY_F64) v = v < 0.f ? (float)(0.1 * (double)v) : v;
+  if (flags & EPI_LEAKY_F32) {
+    float t = v * 0.1f;
+    v = v > t ? v : t;
+  }
+  return v;
+}
+
+template <int MF>
+struct Mfma;
+
+// v_mfma_f32_32x32x2_f32: lane l supplies A[l&31][k=l>>5], B[k=l>>5][l&31];
+// D[row][col]: col = l&31, row = (reg&3) + 8*(reg>>2) + 4*(l>>5).
+template <>
+struct Mfma<32> {
+  typedef f32x16 acc_t;
+  static constexpr int KG = 8;  // k covered by one 16-byte fragment read (2 lane halves x 4 steps)
+  static constexpr int REGS = 16;
+  __device__ static __forceinline__ acc_t op(float a, float b, acc_t c) {
+    return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+  }
+  __device__ static __forceinline__ int frag_row(int lane) { return lane & 31; }
+  __device__ static __forceinline__ int frag_kofs(int lane) { return 4 * (lane >> 5); }
+  __device__ static __forceinline__ int out_row(int lane, int reg) { return (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5); }
+  __device__ static __forceinline__ int out_col(int lane) { return lane & 31; }
+};
+
+// v_mfma_f32_16x16x4_f32: lane l supplies A[l&15][k=l>>4], B[k=l>>4][l&15];
+// D[row][col]: col = l&15, row = 4*(l>>4) + reg.
+template <>
+struct Mfma<16> {
+  typedef f32x4 acc_t;
+  static constexpr int KG = 16;  // 4 lane quarters x 4 steps
+  static constexpr int REGS = 4;
+  __device__ static __forceinline__ acc_t op(float a, float b, acc_t c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+  }
+  __device__ static __forceinline__ int frag_row(int lane) { return lane & 15; }
+  __device__ static __forceinline__ int frag_kofs(int lane) { return 4 * (lane >> 4); }
+  __device__ static __forceinline__ int out_row(int lane, int reg) { return 4 * (lane >> 4) + reg; }
+  __device__ static __forceinline__ int out_col(int lane) { return lane & 15; }
+};
+
+// K permutation: inside a KG-wide group, lane part p reads k = KG*g + 4p + (0..3) with one
+// ds_read_b128 and feeds them to 4 consecutive MFMAs. A and B use the same mapping, so the
+// reduction still covers every k exactly once.
+template <int BM, int BN, int BK, int WM, int WN, int MF>
+__global__ void __launch_bounds__(WM* WN * 64)
+gemm_f32_mfma_kernel(const float* __restrict__ A, int lda, const float* __restrict__ Bt, int ldb,
+                     float* __restrict__ C, int ldc, int M, int N, int K, EpiParams epi, int tilesN) {
+  typedef Mfma<MF> MM;
+  typedef typename MM::acc_t acc_t;
+  constexpr int T = WM * WN * 64;
+  constexpr int LS = BK + 4;  // LDS row stride (floats): breaks the power-of-two bank aliasing
+  constexpr int WTM = BM / WM, WTN = BN / WN;
+  constexpr int TM = WTM / MF, TN = WTN / MF;
+  constexpr int KQ = BK / 4;
+  constexpr int A_V4 = BM * KQ, B_V4 = BN * KQ;
+  constexpr int A_LD = (A_V4 + T - 1) / T, B_LD = (B_V4 + T - 1) / T;
+  static_assert(BK % MM::KG == 0, "BK must be a multiple of the fragment group");
+  static_assert(WTM % MF == 0 && WTN % MF == 0, "wave tile must be a multiple of the MFMA tile");
+
+  __shared__ __attribute__((aligned(16))) float smem[2 * (BM + BN) * LS];
+
+  // XCD-aware bijective remap: the 8 XCDs each get a contiguous range of tiles, so the
+  // N tiles of one A row-panel run under one L2 (cdna_hip_programming.md T1).
+  const int nb = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, q = nb >> 3, rr = nb & 7;
+  const int tile = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (bid >> 3);
+  const int tm_ = tile / tilesN, tn_ = tile - tm_ * tilesN;
+  const int m0 = tm_ * BM, n0 = tn_ * BN;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid - (wid / WN) * WN;
+
+  f32x4 ra[A_LD], rb[B_LD];
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < A_LD; ++i) {
+      int idx = tid + i * T;
+      if (A_V4 % T == 0 || idx < A_V4) {
+        int row = idx / KQ, c4 = idx - (idx / KQ) * KQ;
+        int gm = m0 + row;
+        gm = gm < M ? gm : M - 1;
+        ra[i] = *reinterpret_cast<const f32x4*>(A + (size_t)gm * lda + k0 + c4 * 4);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < B_LD; ++i) {
+      int idx = tid + i * T;
+      if (B_V4 % T == 0 || idx < B_V4) {
+        int row = idx / KQ, c4 = idx - (idx / KQ) * KQ;
+        rb[i] = *reinterpret_cast<const f32x4*>(Bt + (size_t)(n0 + row) * ldb + k0 + c4 * 4);
+      }
+    }
+  };
+  auto sstore = [&](float* As, float* Bs) {
+#pragma unroll
+    for (int i = 0; i < A_LD; ++i) {
+      int idx = tid + i * T;
+      if (A_V4 % T == 0 || idx < A_V4) {
+        int row = idx / KQ, c4 = idx - (idx / KQ) * KQ;
+        *reinterpret_cast<f32x4*>(As + row * LS + c4 * 4) = ra[i];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < B_LD; ++i) {
+      int idx = tid + i * T;
+      if (B_V4 % T == 0 || idx < B_V4) {
+        int row = idx / KQ, c4 = idx - (idx / KQ) * KQ;
+        *reinterpret_cast<f32x4*>(Bs + row * LS + c4 * 4) = rb[i];
+      }
+    }
+  };
+
+  acc_t acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < MM::REGS; ++r) acc[i][j][r] = 0.f;
+
+  const int fr = MM::frag_row(lane), fk = MM::frag_kofs(lane);
+  const int a_base = (wm * WTM + fr) * LS + fk;
+  const int b_base = (wn * WTN + fr) * LS + fk;
+
+  const int nk = K / BK;
+  gload(0);
+  sstore(smem, smem + BM * LS);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    float* As = smem + (kt & 1) * (BM + BN) * LS;
+    float* Bs = As + BM * LS;
+    if (kt + 1 < nk) gload((kt + 1) * BK);
+#pragma unroll
+    for (int g = 0; g < BK / MM::KG; ++g) {
+      f32x4 af[TM], bf[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        af[i] = *reinterpret_cast<const f32x4*>(As + a_base + i * MF * LS + g * MM::KG);
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        bf[j] = *reinterpret_cast<const f32x4*>(Bs + b_base + j * MF * LS + g * MM::KG);
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] = MM::op(af[i][s], bf[j][s], acc[i][j]);
+    }
+    if (kt + 1 < nk) {
+      float* Asn = smem + ((kt + 1) & 1) * (BM + BN) * LS;
+      sstore(Asn, Asn + BM * LS);
+    }
+    __syncthreads();
+  }
+
+  // fused epilogue + store (NHWC: row = output pixel, col = output channel)
+  const int oc = MM::out_col(lane);
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int n = n0 + wn * WTN + j * MF + oc;
+    const float pb = (epi.flags & EPI_BIAS) ? epi.bias[n] : 0.f;
+    const float pm = (epi.flags & (EPI_BN | EPI_BN_AB)) ? epi.mean[n] : 0.f;
+    const float ps = (epi.flags & (EPI_BN | EPI_BN_AB)) ? epi.sq[n] : 1.f;
+    const float pg = (epi.flags & EPI_BN) ? epi.gamma[n] : 1.f;
+    if (n < N) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+#pragma unroll
+        for (int r = 0; r < MM::REGS; ++r) {
+          const int m = m0 + wm * WTM + i * MF + MM::out_row(lane, r);
+          if (m < M) C[(size_t)m * ldc + n] = apply_epilogue(acc[i][j][r], pb, pm, ps, pg, epi.flags);
+        }
+      }
+    }
+  }
+}
+
+struct CfgInfo {
+  int bm, bn, bk;
+};
+static const CfgInfo kCfgs[GEMM_NUM_CFGS] = {
+    {256, 16, 32}, {256, 32, 16}, {128, 64, 32}, {128, 128, 32}, {64, 128, 32}};
+
+int gemm_cfg_bm(int cfg) { return kCfgs[cfg].bm; }
+int gemm_cfg_bn(int cfg) { return kCfgs[cfg].bn; }
+int gemm_cfg_bk(int cfg) { return kCfgs[cfg].bk; }
+
+int choose_gemm_cfg(long long M, int N, int K) {
+  (void)K;
+  if (N <= 16) return GEMM_256x16_K32;
+  if (N <= 32) return GEMM_256x32_K16;
+  if (N <= 64) return GEMM_128x64_K32;
+  long long t128 = ((M + 127) / 128) * ((N + 127) / 128);
+  if (t128 >= 512) return GEMM_128x128_K32;
+  return GEMM_64x128_K32;
+}
+
+int launch_gemm(int cfg, const float* A, int lda, const float* Bt, int ldb, float* C, int ldc,
+                long long M, int N, int Kpad, const EpiParams& epi, hipStream_t stream) {
+  if (M == 0 || N == 0) return 0;
+  if (cfg < 0 || cfg >= GEMM_NUM_CFGS) {
+    set_error("gemm: bad cfg %d", cfg);
+    return -2;
+  }
+  const CfgInfo ci = kCfgs[cfg];
+  if (Kpad % ci.bk != 0 || lda % 4 != 0 || ldb % 4 != 0 || M > 0x7fffffffLL) {
+    set_error("gemm: unsupported shape M=%lld Kpad=%d lda=%d ldb=%d for cfg %d", M, Kpad, lda, ldb, cfg);
+    return -2;
+  }
+  const int tilesM = ceil_div_i(M, ci.bm), tilesN = ceil_div_i(N, ci.bn);
+  dim3 grid(tilesM * tilesN);
+  const int m = (int)M;
+  switch (cfg) {
+    case GEMM_256x16_K32:
+      hipLaunchKernelGGL((gemm_f32_mfma_kernel<256, 16, 32, 4, 1, 16>), grid, dim3(256), 0, stream, A, lda,
+                         Bt, ldb, C, ldc, m, N, Kpad, epi, tilesN);
+      break;
+    case GEMM_256x32_K16:
+      hipLaunchKernelGGL((gemm_f32_mfma_kernel<256, 32, 16, 4, 1, 16>), grid, dim3(256), 0, stream, A, lda,
+                         Bt, ldb, C, ldc, m, N, Kpad, epi, tilesN);
+      break;
+    case GEMM_128x64_K32:
+      hipLaunchKernelGGL((gemm_f32_mfma_kernel<128, 64, 32, 2, 2, 32>), grid, dim3(256), 0, stream, A, lda,
+                         Bt, ldb, C, ldc, m, N, Kpad, epi, tilesN);
+      break;
+    case GEMM_128x128_K32:
+      hipLaunchKernelGGL((gemm_f32_mfma_kernel<128, 128, 32, 2, 2, 32>), grid, dim3(256), 0, stream, A, lda,
+                         Bt, ldb, C, ldc, m, N, Kpad, epi, tilesN);
+      break;
+    case GEMM_64x128_K32:
+      hipLaunchKernelGGL((gemm_f32_mfma_kernel<64, 128, 32, 2, 2, 32>), grid, dim3(256), 0, stream, A, lda,
+                         Bt, ldb, C, ldc, m, N, Kpad, epi, tilesN);
+      break;
+  }
+  return check_launch("gemm");
+}
+
+// ============================================================================ maxpool
+// Window max with the reference's comparison: imax = first element; imax = imax >= x ? imax : x
+// over every (di, dj), pad cells read as -FLT_MAX (np.finfo(float32).min).  The AVX ABI's
+// vector channels compare with `>` instead (PoolGeom::gt_below).
+template <int VEC>
+__global__ void __launch_bounds__(256)
+maxpool_nhwc_kernel(const float* __restrict__ in, float* __restrict__ out, PoolGeom g, long long total) {
+  const int cq = g.C / VEC;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    int c = (int)(i % cq) * VEC;
+    long long p = i / cq;
+    int ox = (int)(p % g.OW);
+    long long t = p / g.OW;
+    int oy = (int)(t % g.OH);
+    int b = (int)(t / g.OH);
+    int iy0 = oy * g.sh - g.pt, ix0 = ox * g.sw - g.pl;
+    const float* base = in + (long long)b * g.H * g.W * g.C + c;
+    auto fetch = [&](int iy, int ix) {
+      f32x4 v;
+      if ((unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W) {
+        const float* s = base + ((long long)iy * g.W + ix) * g.C;
+        if constexpr (VEC == 4) {
+          v = *reinterpret_cast<const f32x4*>(s);
+        } else {
+          v[0] = *s;
+        }
+      } else {
+        v = f32x4{-FLT_MAX, -FLT_MAX, -FLT_MAX, -FLT_MAX};
+      }
+      return v;
+    };
+    f32x4 m = fetch(iy0, ix0);
+    for (int di = 0; di < g.kh; ++di)
+      for (int dj = 0; dj < g.kw; ++dj) {
+        f32x4 x = fetch(iy0 + di, ix0 + dj);
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) {
+          if (c + e < g.gt_below)
+            m[e] = m[e] > x[e] ? m[e] : x[e];
+          else
+            m[e] = m[e] >= x[e] ? m[e] : x[e];
+        }
+      }
+    float* d = out + p * g.C + c;
+    if constexpr (VEC == 4) {
+      *reinterpret_cast<f32x4*>(d) = m;
+    } else {
+      *d = m[0];
+    }
+  }
+}
+
+static dim3 stream_grid(long long total, int threads = 256) {
+  long long b = (total + threads - 1) / threads;
+  const long long cap = 256LL * 16;  // 256 CUs x 16 blocks, grid-stride for the rest
+  return dim3((unsigned)(b < cap ? (b > 0 ? b : 1) : cap));
+}
+
+int launch_maxpool(const float* in, float* out, const PoolGeom& g, hipStream_t stream) {
+  long long outs = (long long)g.B * g.OH * g.OW;
+  if (outs == 0 || g.C == 0) return 0;
+  if (g.C % 4 == 0) {
+    long long total = outs * (g.C / 4);
+    hipLaunchKernelGGL(maxpool_nhwc_kernel<4>, stream_grid(total), dim3(256), 0, stream, in, out, g, total);
+  } else {
+    long long total = outs * g.C;
+    hipLaunchKernelGGL(maxpool_nhwc_kernel<1>, stream_grid(total), dim3(256), 0, stream, in, out, g, total);
+  }
+  return check_launch("maxpool");
+}
+
+// ============================================================================ weight packing
+__global__ void pack_weights_kernel(const float* __restrict__ w, float* __restrict__ bt, int K, int N, int Kpad,
+                                    int Npad, int order, int kh, int kw, int C) {
+  long long total = (long long)Npad * Kpad;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    int n = (int)(i / Kpad), k = (int)(i % Kpad);
+    float v = 0.f;
+    if (n < N && k < K) {
+      int src = k;
+      if (order == 1) {
+        int tap = k / C, c = k - tap * C;
+        int dy = tap / kw, dx = tap - dy * kw;
+        src = (c * kh + dy) * kw + dx;
+      }
+      v = w[(long long)src * N + n];
+    }
+    bt[i] = v;
+  }
+}
+
+int launch_pack_weights(const float* w, float* bt, int K, int N, int Kpad, int Npad, int order, int kh, int kw,
+                        int C, hipStream_t stream) {
+  long long total = (long long)Npad * Kpad;
+  if (total == 0) return 0;
+  hipLaunchKernelGGL(pack_weights_kernel, stream_grid(total), dim3(256), 0, stream, w, bt, K, N, Kpad, Npad,
+                     order, kh, kw, C);
+  return check_launch("pack_weights");
+}
+
+// ============================================================================ element-wise
+__global__ void bias_add_kernel(const float* __restrict__ in, const float* __restrict__ b, float* __restrict__ out,
+                                long long n, int C) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    out[i] = in[i] + b[i % C];
+}
+
+__global__ void bn_mvg_kernel(const float* __restrict__ in, const float* __restrict__ mean,
+                              const float* __restrict__ sq, const float* __restrict__ gamma,
+                              float* __restrict__ out, long long n, int C) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    int d = (int)(i % C);
+    out[i] = ((in[i] - mean[d]) / sq[d]) * gamma[d];
+  }
+}
+
+__global__ void bn_ab_kernel(const float* __restrict__ in, const float* __restrict__ alpha,
+                             const float* __restrict__ beta, float* __restrict__ out, long long n, int C) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    int d = (int)(i % C);
+    float r = in[i] * alpha[d];
+    out[i] = r - beta[d];
+  }
+}
+
+__global__ void leaky_kernel(const float* __restrict__ in, float* __restrict__ out, long long n, int f32v) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    float t = in[i];
+    if (f32v) {
+      float s = t * 0.1f;
+      out[i] = t > s ? t : s;
+    } else {
+      out[i] = t < 0.f ? (float)(0.1 * (double)t) : t;
+    }
+  }
+}
+
+int launch_bias_add(const float* in, const float* b, float* out, long long n, int C, hipStream_t s) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(bias_add_kernel, stream_grid(n), dim3(256), 0, s, in, b, out, n, C);
+  return check_launch("bias_add");
+}
+int launch_bn_mvg(const float* in, const float* mean, const float* sq, const float* gamma, float* out, long long n,
+                  int C, hipStream_t s) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(bn_mvg_kernel, stream_grid(n), dim3(256), 0, s, in, mean, sq, gamma, out, n, C);
+  return check_launch("batch_norm");
+}
+int launch_bn_ab(const float* in, const float* alpha, const float* beta, float* out, long long n, int C,
+                 hipStream_t s) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(bn_ab_kernel, stream_grid(n), dim3(256), 0, s, in, alpha, beta, out, n, C);
+  return check_launch("batch_norm_ab");
+}
+int launch_leaky(const float* in, float* out, long long n, int f32_variant, hipStream_t s) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(leaky_kernel, stream_grid(n), dim3(256), 0, s, in, out, n, f32_variant);
+  return check_launch("leaky_relu");
+}
+
+}  // namespace dnnhip

@@ -1,0 +1,465 @@
+// Device-resident execution plan (include/dnn_hip_plan.h).
+//
+// The reference walks its graph node by node and round-trips every intermediate through
+// host numpy arrays (proj3/dnn_openblas.py:29-57; each CUDA/cuBLAS call even mallocs and
+// copies per image, dnn_cuda.cu:193-210).  Here the same node chain is lowered once to a
+// list of device steps:
+//   conv entry  = im2col (skipped for 1x1/stride-1/unpadded layers, where col == input)
+//                 + one fp32-MFMA GEMM whose epilogue applies BiasAdd, BatchNorm, LeakyReLU
+//   pool entry  = one maxpool kernel
+// Weights are packed once into a device arena as Bt[Npad][Kpad] (K order kh,kw,ic) plus
+// four Npad-long epilogue vectors (bias, mean, sqrt(var+eps), gamma).  Activations ping-pong
+// between two workspace buffers; the im2col buffer is shared by all layers.
+#include <hip/hip_runtime.h>
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+#include "dnn_common.h"
+#include "../../include/dnn_hip_plan.h"
+
+namespace dnnhip {
+
+static thread_local std::string g_last_error;
+
+void set_error(const char* fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_last_error = buf;
+}
+const char* last_error() { return g_last_error.c_str(); }
+
+void out_pads(int in, int k, int s, int same, int* out, int* pad_front) {
+  // proj3/dnn_openblas.py:127-142 (TensorFlow SAME / VALID)
+  if (same) {
+    int o = (in + s - 1) / s;
+    int pad = (o - 1) * s + k - in;
+    if (pad < 0) pad = 0;
+    *out = o;
+    *pad_front = pad / 2;
+  } else {
+    int span = in - k + 1;
+    *out = span > 0 ? (span + s - 1) / s : 0;
+    *pad_front = 0;
+  }
+}
+
+static size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+}  // namespace dnnhip
+
+using namespace dnnhip;
+
+struct PlanLayer {
+  int type = 0;  // 0 conv, 1 pool
+  // shapes (per image)
+  int H = 0, W = 0, C = 0, OH = 0, OW = 0, OC = 0;
+  int kh = 0, kw = 0, sh = 1, sw = 1, pt = 0, pl = 0;
+  // conv
+  int K = 0, Kpad = 0, Npad = 0, cfg = 0, epi_flags = 0;
+  bool direct = false;  // A operand is the input itself (1x1, stride 1, no pad, C % BK == 0)
+  size_t w_off = 0, epi_off = 0;  // float offsets in the weight arena
+  bool have_host = false;
+  std::vector<float> w, bias, mean, sq, gamma;
+  int kernel_idx = 0;  // index of this layer's first kernel in the kernel list
+};
+
+struct KernelDesc {
+  std::string name;
+  int layer;
+  int kind;  // 0 im2col, 1 gemm, 2 pool
+  double flops, bytes;  // algorithmic, full planned batch
+};
+
+struct dnn_plan {
+  int batch = 0, in_h = 0, in_w = 0, in_c = 0;
+  int cur_h = 0, cur_w = 0, cur_c = 0;
+  std::vector<PlanLayer> layers;
+  std::vector<KernelDesc> kernels;
+  int device = -1;
+  bool finalized = false;
+  float* weights = nullptr;
+  size_t weight_floats = 0;
+  bool own_weights = false;
+  float* ws = nullptr;
+  size_t ws_floats = 0;
+  bool own_ws = false;
+  size_t act_floats = 0, col_floats = 0;
+  // staging for dnn_plan_run_host
+  float* h_in_dev = nullptr;
+  size_t h_in_floats = 0;
+  // timing
+  bool timing = false;
+  int ev_cap = 0, ev_used = 0;
+  std::vector<hipEvent_t> ev;
+  std::vector<int> ev_kernel;
+};
+
+static void layout(dnn_plan* p) {
+  // weight arena and workspace sizes
+  size_t off = 0, act = (size_t)p->in_h * p->in_w * p->in_c, col = 0;
+  int nconv = 0, npool = 0;  // kernel names use conv / pool ordinals: "conv7.gemm" is YOLO's conv7
+  p->kernels.clear();
+  for (size_t i = 0; i < p->layers.size(); ++i) {
+    PlanLayer& L = p->layers[i];
+    act = std::max(act, (size_t)L.OH * L.OW * L.OC);
+    const double B = p->batch;
+    const double M = B * L.OH * L.OW;
+    L.kernel_idx = (int)p->kernels.size();
+    char nm[64];
+    if (L.type == 0) {
+      L.w_off = off;
+      off = align_up(off + (size_t)L.Npad * L.Kpad, 64);
+      L.epi_off = off;
+      off = align_up(off + 4 * (size_t)L.Npad, 64);
+      if (!L.direct) {
+        col = std::max(col, (size_t)L.OH * L.OW * L.Kpad);
+        snprintf(nm, sizeof(nm), "conv%d.im2col", nconv);
+        // algorithmic bytes: col written once + input read once
+        p->kernels.push_back({nm, (int)i, 0, 0.0, 4.0 * (M * L.K + B * L.H * L.W * L.C)});
+      }
+      snprintf(nm, sizeof(nm), "conv%d.gemm", nconv++);
+      p->kernels.push_back({nm, (int)i, 1, 2.0 * M * L.OC * L.K,
+                            4.0 * (M * L.K + (double)L.K * L.OC + M * L.OC)});
+    } else {
+      snprintf(nm, sizeof(nm), "pool%d", npool++);
+      p->kernels.push_back({nm, (int)i, 2, 0.0, 4.0 * (B * L.H * L.W * L.C + M * L.OC)});
+    }
+  }
+  p->weight_floats = align_up(off, 64);
+  p->act_floats = align_up(act * (size_t)p->batch, 64);
+  p->col_floats = align_up(col * (size_t)p->batch, 64);
+  p->ws_floats = 2 * p->act_floats + p->col_floats;
+}
+
+extern "C" {
+
+const char* dnn_last_error(void) { return last_error(); }
+
+int dnn_plan_create(int batch, int in_h, int in_w, int in_c, dnn_plan** out) {
+  DNN_REQUIRE(out != nullptr, "dnn_plan_create: out is NULL");
+  DNN_REQUIRE(batch >= 0 && in_h > 0 && in_w > 0 && in_c > 0, "dnn_plan_create: bad shape %d,%d,%d,%d", batch,
+              in_h, in_w, in_c);
+  dnn_plan* p = new dnn_plan();
+  p->batch = batch;
+  p->in_h = p->cur_h = in_h;
+  p->in_w = p->cur_w = in_w;
+  p->in_c = p->cur_c = in_c;
+  *out = p;
+  return 0;
+}
+
+void dnn_plan_destroy(dnn_plan* p) {
+  if (!p) return;
+  if (p->device >= 0) (void)hipSetDevice(p->device);
+  for (auto e : p->ev) (void)hipEventDestroy(e);
+  if (p->own_weights && p->weights) (void)hipFree(p->weights);
+  if (p->own_ws && p->ws) (void)hipFree(p->ws);
+  if (p->h_in_dev) (void)hipFree(p->h_in_dev);
+  delete p;
+}
+
+int dnn_plan_add_conv(dnn_plan* p, int kh, int kw, int od, int stride_h, int stride_w, int padding,
+                      const float* kernel, const float* biases, const float* mean, const float* var,
+                      const float* gamma, float eps, int leaky) {
+  DNN_REQUIRE(p && !p->finalized, "dnn_plan_add_conv: plan is NULL or finalized");
+  DNN_REQUIRE(kh > 0 && kw > 0 && od > 0 && stride_h > 0 && stride_w > 0, "dnn_plan_add_conv: bad args");
+  DNN_REQUIRE((mean == nullptr) == (var == nullptr) && (var == nullptr) == (gamma == nullptr),
+              "dnn_plan_add_conv: mean/var/gamma must be all set or all NULL");
+  DNN_REQUIRE(leaky >= 0 && leaky <= 2, "dnn_plan_add_conv: leaky must be 0, 1 or 2");
+  PlanLayer L;
+  L.type = 0;
+  L.H = p->cur_h;
+  L.W = p->cur_w;
+  L.C = p->cur_c;
+  L.kh = kh;
+  L.kw = kw;
+  L.sh = stride_h;
+  L.sw = stride_w;
+  out_pads(L.H, kh, stride_h, padding, &L.OH, &L.pt);
+  out_pads(L.W, kw, stride_w, padding, &L.OW, &L.pl);
+  DNN_REQUIRE(L.OH > 0 && L.OW > 0, "dnn_plan_add_conv: empty output (%dx%d input, %dx%d kernel)", L.H, L.W, kh,
+              kw);
+  L.OC = od;
+  L.K = kh * kw * L.C;
+  L.cfg = choose_gemm_cfg((long long)p->batch * L.OH * L.OW, od, L.K);
+  const int bk = gemm_cfg_bk(L.cfg), bn = gemm_cfg_bn(L.cfg);
+  L.Kpad = (int)align_up(L.K, bk);
+  L.Npad = (int)align_up(od, bn);
+  L.direct = kh == 1 && kw == 1 && stride_h == 1 && stride_w == 1 && L.pt == 0 && L.pl == 0 &&
+             L.OH == L.H && L.OW == L.W && L.C % bk == 0;
+  L.epi_flags = (biases ? EPI_BIAS : 0) | (mean ? EPI_BN : 0) |
+                (leaky == 1 ? EPI_LEAKY_F64 : leaky == 2 ? EPI_LEAKY_F32 : 0);
+  if (kernel) {
+    L.have_host = true;
+    L.w.assign(kernel, kernel + (size_t)L.K * od);
+    L.bias.assign(L.Npad, 0.f);
+    L.mean.assign(L.Npad, 0.f);
+    L.sq.assign(L.Npad, 1.f);
+    L.gamma.assign(L.Npad, 1.f);
+    for (int d = 0; d < od; ++d) {
+      if (biases) L.bias[d] = biases[d];
+      if (mean) {
+        L.mean[d] = mean[d];
+        // sqrt(variance + epsilon) in fp32 as the reference (dnn_openblas.c:48-50; dnn.py:325-327)
+        volatile float s = var[d] + eps;
+        L.sq[d] = sqrtf(s);
+        L.gamma[d] = gamma[d];
+      }
+    }
+  }
+  p->layers.push_back(std::move(L));
+  p->cur_h = p->layers.back().OH;
+  p->cur_w = p->layers.back().OW;
+  p->cur_c = od;
+  return 0;
+}
+
+int dnn_plan_add_max_pool(dnn_plan* p, int kh, int kw, int stride_h, int stride_w, int padding) {
+  DNN_REQUIRE(p && !p->finalized, "dnn_plan_add_max_pool: plan is NULL or finalized");
+  DNN_REQUIRE(kh > 0 && kw > 0 && stride_h > 0 && stride_w > 0, "dnn_plan_add_max_pool: bad args");
+  PlanLayer L;
+  L.type = 1;
+  L.H = p->cur_h;
+  L.W = p->cur_w;
+  L.C = L.OC = p->cur_c;
+  L.kh = kh;
+  L.kw = kw;
+  L.sh = stride_h;
+  L.sw = stride_w;
+  out_pads(L.H, kh, stride_h, padding, &L.OH, &L.pt);
+  out_pads(L.W, kw, stride_w, padding, &L.OW, &L.pl);
+  DNN_REQUIRE(L.OH > 0 && L.OW > 0, "dnn_plan_add_max_pool: empty output");
+  p->layers.push_back(std::move(L));
+  p->cur_h = p->layers.back().OH;
+  p->cur_w = p->layers.back().OW;
+  return 0;
+}
+
+int dnn_plan_output_shape(const dnn_plan* p, int* batch, int* h, int* w, int* c) {
+  DNN_REQUIRE(p, "dnn_plan_output_shape: plan is NULL");
+  if (batch) *batch = p->batch;
+  if (h) *h = p->cur_h;
+  if (w) *w = p->cur_w;
+  if (c) *c = p->cur_c;
+  return 0;
+}
+
+int dnn_plan_memory(const dnn_plan* pc, size_t* weight_bytes, size_t* workspace_bytes) {
+  DNN_REQUIRE(pc, "dnn_plan_memory: plan is NULL");
+  dnn_plan* p = const_cast<dnn_plan*>(pc);
+  layout(p);
+  if (weight_bytes) *weight_bytes = p->weight_floats * sizeof(float);
+  if (workspace_bytes) *workspace_bytes = p->ws_floats * sizeof(float);
+  return 0;
+}
+
+int dnn_plan_finalize(dnn_plan* p, int device, void* weights, void* workspace) {
+  DNN_REQUIRE(p && !p->finalized, "dnn_plan_finalize: plan is NULL or already finalized");
+  DNN_REQUIRE(!p->layers.empty(), "dnn_plan_finalize: plan has no layers");
+  layout(p);
+  DNN_HIP_TRY(hipSetDevice(device));
+  p->device = device;
+  if (weights) {
+    p->weights = static_cast<float*>(weights);
+  } else {
+    DNN_HIP_TRY(hipMalloc(&p->weights, p->weight_floats * sizeof(float)));
+    p->own_weights = true;
+  }
+  if (workspace) {
+    p->ws = static_cast<float*>(workspace);
+  } else if (p->ws_floats) {
+    DNN_HIP_TRY(hipMalloc(&p->ws, p->ws_floats * sizeof(float)));
+    p->own_ws = true;
+  }
+  bool all_host = true;
+  for (auto& L : p->layers)
+    if (L.type == 0 && !L.have_host) all_host = false;
+  if (all_host) {
+    // upload raw HWIO weights through a temporary buffer, pack on the device
+    size_t maxw = 0;
+    for (auto& L : p->layers)
+      if (L.type == 0) maxw = std::max(maxw, L.w.size());
+    float* tmp = nullptr;
+    DNN_HIP_TRY(hipMalloc(&tmp, std::max<size_t>(maxw, 1) * sizeof(float)));
+    int rc = 0;
+    for (auto& L : p->layers) {
+      if (L.type != 0) continue;
+      if (hipMemcpy(tmp, L.w.data(), L.w.size() * sizeof(float), hipMemcpyHostToDevice) != hipSuccess) {
+        set_error("dnn_plan_finalize: weight upload failed");
+        rc = -1;
+        break;
+      }
+      rc = launch_pack_weights(tmp, p->weights + L.w_off, L.K, L.OC, L.Kpad, L.Npad, 0, L.kh, L.kw, L.C, 0);
+      if (rc) break;
+      float* e = p->weights + L.epi_off;
+      const size_t nb = (size_t)L.Npad * sizeof(float);
+      if (hipMemcpy(e, L.bias.data(), nb, hipMemcpyHostToDevice) != hipSuccess ||
+          hipMemcpy(e + L.Npad, L.mean.data(), nb, hipMemcpyHostToDevice) != hipSuccess ||
+          hipMemcpy(e + 2 * L.Npad, L.sq.data(), nb, hipMemcpyHostToDevice) != hipSuccess ||
+          hipMemcpy(e + 3 * L.Npad, L.gamma.data(), nb, hipMemcpyHostToDevice) != hipSuccess) {
+        set_error("dnn_plan_finalize: epilogue upload failed");
+        rc = -1;
+        break;
+      }
+      if (hipDeviceSynchronize() != hipSuccess) {
+        set_error("dnn_plan_finalize: pack failed");
+        rc = -1;
+        break;
+      }
+    }
+    (void)hipFree(tmp);
+    if (rc) return rc;
+    for (auto& L : p->layers) {  // host copies no longer needed
+      std::vector<float>().swap(L.w);
+    }
+  }
+  p->finalized = true;
+  return 0;
+}
+
+int dnn_plan_weight_buffer(const dnn_plan* p, void** ptr, size_t* bytes) {
+  DNN_REQUIRE(p && p->finalized, "dnn_plan_weight_buffer: plan not finalized");
+  if (ptr) *ptr = p->weights;
+  if (bytes) *bytes = p->weight_floats * sizeof(float);
+  return 0;
+}
+
+static int record(dnn_plan* p, int kernel, hipStream_t s) {
+  if (!p->timing) return 0;
+  if (p->ev_used + 1 >= p->ev_cap) return 0;  // capacity exhausted: stop recording silently
+  DNN_HIP_TRY(hipEventRecord(p->ev[p->ev_used], s));
+  p->ev_kernel[p->ev_used] = kernel;
+  p->ev_used++;
+  return 0;
+}
+
+int dnn_plan_run(dnn_plan* p, int n, const float* d_in, float* d_out, void* stream) {
+  DNN_REQUIRE(p && p->finalized, "dnn_plan_run: plan not finalized");
+  DNN_REQUIRE(n >= 0 && n <= p->batch, "dnn_plan_run: n=%d outside [0, %d]", n, p->batch);
+  if (n == 0) return 0;
+  DNN_REQUIRE(d_in && d_out, "dnn_plan_run: NULL tensor");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  float* act[2] = {p->ws, p->ws + p->act_floats};
+  float* col = p->ws + 2 * p->act_floats;
+  const float* cur = d_in;
+  const int nl = (int)p->layers.size();
+  for (int i = 0; i < nl; ++i) {
+    PlanLayer& L = p->layers[i];
+    float* dst = (i == nl - 1) ? d_out : act[i & 1];
+    int k = L.kernel_idx;
+    int rc = 0;
+    if (L.type == 0) {
+      const float* A = cur;
+      int lda = L.C;
+      if (!L.direct) {
+        ConvGeom g{n, L.H, L.W, L.C, L.OH, L.OW, L.kh, L.kw, L.sh, L.sw, L.pt, L.pl, L.K, L.Kpad};
+        if ((rc = record(p, k, s))) return rc;
+        if ((rc = launch_im2col(cur, col, g, s))) return rc;
+        A = col;
+        lda = L.Kpad;
+        ++k;
+      }
+      const float* e = p->weights + L.epi_off;
+      EpiParams epi{e, e + L.Npad, e + 2 * L.Npad, e + 3 * L.Npad, L.epi_flags};
+      if ((rc = record(p, k, s))) return rc;
+      if ((rc = launch_gemm(L.cfg, A, lda, p->weights + L.w_off, L.Kpad, dst, L.OC, (long long)n * L.OH * L.OW,
+                            L.OC, L.Kpad, epi, s)))
+        return rc;
+    } else {
+      PoolGeom g{n, L.H, L.W, L.C, L.OH, L.OW, L.kh, L.kw, L.sh, L.sw, L.pt, L.pl, 0};
+      if ((rc = record(p, k, s))) return rc;
+      if ((rc = launch_maxpool(cur, dst, g, s))) return rc;
+    }
+    cur = dst;
+  }
+  return record(p, -1, s);
+}
+
+int dnn_plan_run_host(dnn_plan* p, int n, const float* h_in, float* h_out) {
+  DNN_REQUIRE(p && p->finalized, "dnn_plan_run_host: plan not finalized");
+  DNN_REQUIRE(n >= 0 && n <= p->batch, "dnn_plan_run_host: n=%d outside [0, %d]", n, p->batch);
+  if (n == 0) return 0;
+  DNN_HIP_TRY(hipSetDevice(p->device));
+  const size_t in_f = (size_t)n * p->in_h * p->in_w * p->in_c;
+  const size_t out_f = (size_t)n * p->cur_h * p->cur_w * p->cur_c;
+  if (p->h_in_floats < in_f + out_f) {
+    if (p->h_in_dev) DNN_HIP_TRY(hipFree(p->h_in_dev));
+    p->h_in_dev = nullptr;
+    DNN_HIP_TRY(hipMalloc(&p->h_in_dev, (in_f + out_f) * sizeof(float)));
+    p->h_in_floats = in_f + out_f;
+  }
+  float* d_in = p->h_in_dev;
+  float* d_out = p->h_in_dev + in_f;
+  DNN_HIP_TRY(hipMemcpy(d_in, h_in, in_f * sizeof(float), hipMemcpyHostToDevice));
+  int rc = dnn_plan_run(p, n, d_in, d_out, nullptr);
+  if (rc) return rc;
+  DNN_HIP_TRY(hipMemcpy(h_out, d_out, out_f * sizeof(float), hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int dnn_plan_num_kernels(const dnn_plan* pc) {
+  if (!pc) return -2;
+  dnn_plan* p = const_cast<dnn_plan*>(pc);
+  if (!p->finalized) layout(p);
+  return (int)p->kernels.size();
+}
+
+int dnn_plan_kernel_info(const dnn_plan* pc, int idx, char* name, int name_len, double* flops, double* bytes) {
+  DNN_REQUIRE(pc, "dnn_plan_kernel_info: plan is NULL");
+  dnn_plan* p = const_cast<dnn_plan*>(pc);
+  if (!p->finalized) layout(p);
+  DNN_REQUIRE(idx >= 0 && idx < (int)p->kernels.size(), "dnn_plan_kernel_info: bad index %d", idx);
+  const KernelDesc& k = p->kernels[idx];
+  if (name && name_len > 0) snprintf(name, name_len, "%s", k.name.c_str());
+  if (flops) *flops = k.flops;
+  if (bytes) *bytes = k.bytes;
+  return 0;
+}
+
+int dnn_plan_timing_begin(dnn_plan* p, int max_runs) {
+  DNN_REQUIRE(p && p->finalized, "dnn_plan_timing_begin: plan not finalized");
+  DNN_REQUIRE(max_runs > 0, "dnn_plan_timing_begin: max_runs must be > 0");
+  DNN_HIP_TRY(hipSetDevice(p->device));
+  int need = max_runs * ((int)p->kernels.size() + 1) + 1;
+  while ((int)p->ev.size() < need) {
+    hipEvent_t e;
+    DNN_HIP_TRY(hipEventCreate(&e));
+    p->ev.push_back(e);
+  }
+  p->ev_kernel.assign(p->ev.size(), -1);
+  p->ev_cap = (int)p->ev.size();
+  p->ev_used = 0;
+  p->timing = true;
+  return 0;
+}
+
+int dnn_plan_timing_end(dnn_plan* p, double* ms_sum, long long* launches) {
+  DNN_REQUIRE(p && p->timing, "dnn_plan_timing_end: timing not active");
+  p->timing = false;
+  const int nk = (int)p->kernels.size();
+  for (int i = 0; i < nk; ++i) {
+    if (ms_sum) ms_sum[i] = 0.0;
+    if (launches) launches[i] = 0;
+  }
+  if (p->ev_used > 0) DNN_HIP_TRY(hipEventSynchronize(p->ev[p->ev_used - 1]));
+  // event i opens kernel ev_kernel[i]; it is closed by event i+1 (same stream, in order)
+  for (int i = 0; i + 1 < p->ev_used; ++i) {
+    int k = p->ev_kernel[i];
+    if (k < 0) continue;
+    float ms = 0.f;
+    DNN_HIP_TRY(hipEventElapsedTime(&ms, p->ev[i], p->ev[i + 1]));
+    if (ms_sum) ms_sum[k] += ms;
+    if (launches) launches[k] += 1;
+  }
+  p->ev_used = 0;
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,87 @@
+/* dnn_hip_plan.h — device-resident, fused execution plan for the YOLOv2-tiny Conv2D path.
+ *
+ * The reference has no plan object: `DnnInferenceEngine.run` (proj3/dnn_openblas.py:29-57)
+ * walks the networkx graph and calls one host-pointer C function per node
+ * (conv2d_mul / bias_add / batch_norm / leaky_relu / max_pool2d, dnn_openblas.c).  The
+ * plan is the device-resident lowering of that same node chain: each
+ * Conv2D -> BiasAdd -> BatchNorm -> LeakyReLU run becomes ONE conv entry (im2col + fp32
+ * MFMA GEMM with the three element-wise ops as its epilogue, evaluated in the reference's
+ * operation order), each MaxPool2D one pool entry, and activations never leave HBM.
+ * It is what `dnn_hip.DnnInferenceEngine.run` (the Python mirror of dnn_openblas.py)
+ * lowers the graph to.
+ *
+ * Conventions: plain C ABI, cdecl, no torch types.  All tensors NHWC fp32 contiguous,
+ * conv kernels HWIO (the pickle layout of proj3/yolov2tiny.py:30-77).  Functions return
+ * 0 on success and a negative code on error; dnn_last_error() describes the last error
+ * of the calling thread.  Padding: 0 = VALID, 1 = SAME with TF semantics
+ * (get_out_pads, proj3/dnn_openblas.py:127-142).
+ */
+#ifndef DNN_HIP_PLAN_H
+#define DNN_HIP_PLAN_H
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+#pragma GCC visibility push(default)
+
+typedef struct dnn_plan dnn_plan;
+
+/* Last error message of the calling thread ("" if none). */
+const char* dnn_last_error(void);
+
+/* Create an empty plan for inputs [batch, in_h, in_w, in_c]. */
+int dnn_plan_create(int batch, int in_h, int in_w, int in_c, dnn_plan** out);
+void dnn_plan_destroy(dnn_plan* plan);
+
+/* Append a Conv2D (proj3/dnn_openblas.py:144-188) with its trailing BiasAdd / BatchNorm /
+ * LeakyReLU fused.  kernel: [kh][kw][in_c][od] HWIO.  biases may be NULL (no BiasAdd);
+ * mean/var/gamma all NULL means no BatchNorm (else all three, eps as in
+ * proj3/dnn_openblas.py:263-270); leaky: 0 none, 1 = dnn_openblas.c leaky_relu
+ * (t<0 ? 0.1*t in double : t), 2 = dnn_avx.c leaky_relu (max(t, 0.1f*t)).
+ * Host weight pointers are copied; pass kernel == NULL to declare the layer's shape only
+ * (weights then arrive through dnn_plan_weight_buffer, e.g. an RCCL broadcast). */
+int dnn_plan_add_conv(dnn_plan* plan, int kh, int kw, int od, int stride_h, int stride_w, int padding,
+                      const float* kernel, const float* biases, const float* mean, const float* var,
+                      const float* gamma, float eps, int leaky);
+
+/* Append a MaxPool2D (proj3/dnn_openblas.py:213-242). */
+int dnn_plan_add_max_pool(dnn_plan* plan, int kh, int kw, int stride_h, int stride_w, int padding);
+
+/* Output shape of the plan so far (per image, plus the planned batch). */
+int dnn_plan_output_shape(const dnn_plan* plan, int* batch, int* h, int* w, int* c);
+
+/* Device bytes the plan needs: packed weights + epilogue params, and workspace
+ * (two activation buffers + the im2col buffer) for the planned batch. */
+int dnn_plan_memory(const dnn_plan* plan, size_t* weight_bytes, size_t* workspace_bytes);
+
+/* Bind device memory and upload weights.  weights / workspace may be NULL, in which case
+ * the plan hipMallocs its own.  If every conv was added with host weights they are packed
+ * into the weight buffer here (hipMemcpy + pack kernel, synchronous). */
+int dnn_plan_finalize(dnn_plan* plan, int device, void* weights, void* workspace);
+
+/* Device pointer and size of the packed weight buffer (for a broadcast from rank 0). */
+int dnn_plan_weight_buffer(const dnn_plan* plan, void** ptr, size_t* bytes);
+
+/* Run n <= batch images: d_in [n,in_h,in_w,in_c] -> d_out [n,oh,ow,oc], both device
+ * pointers, asynchronously on `stream` (a hipStream_t; NULL = default stream). */
+int dnn_plan_run(dnn_plan* plan, int n, const float* d_in, float* d_out, void* stream);
+
+/* Host-pointer convenience: H2D copy, run, D2H copy, synchronise. */
+int dnn_plan_run_host(dnn_plan* plan, int n, const float* h_in, float* h_out);
+
+/* Per-kernel timing with HIP events recorded on the run stream.
+ * begin: allocate events for up to max_runs runs and start recording;
+ * end: synchronise, write per-kernel summed milliseconds and launch counts (arrays of
+ * dnn_plan_num_kernels() entries), stop recording. */
+int dnn_plan_num_kernels(const dnn_plan* plan);
+int dnn_plan_kernel_info(const dnn_plan* plan, int idx, char* name, int name_len, double* flops,
+                         double* bytes);
+int dnn_plan_timing_begin(dnn_plan* plan, int max_runs);
+int dnn_plan_timing_end(dnn_plan* plan, double* ms_sum, long long* launches);
+
+#pragma GCC visibility pop
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,103 @@
+"""TEST INFRASTRUCTURE ONLY — ctypes binding of oracle/liboracle_dnn.so (dnn_oracle.c).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg use this.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = os.path.join(_HERE, "liboracle_dnn.so")
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def load():
+    if not os.path.exists(_LIB):
+        build()
+    lib = ctypes.CDLL(_LIB)
+    P = ctypes.c_void_p
+    i, f = ctypes.c_int, ctypes.c_float
+    lib.oracle_im2col.argtypes = [P, P] + [i] * 9
+    lib.oracle_conv2d_mul.argtypes = [P, P, P] + [i] * 11
+    lib.oracle_conv2d_direct.argtypes = [P, P, P, i, P, i]
+    lib.oracle_bias_add.argtypes = [P, P, P, i, i, i, i]
+    lib.oracle_batch_norm.argtypes = [P, P, P, P, f, P, i, i, i, i]
+    lib.oracle_batch_norm_ab.argtypes = [P, P, P, P, i, i, i, i]
+    lib.oracle_leaky_relu.argtypes = [P, P, i, i, i, i, i]
+    lib.oracle_max_pool2d.argtypes = [P, P] + [i] * 13
+    for fn in ("oracle_im2col", "oracle_conv2d_mul", "oracle_conv2d_direct", "oracle_bias_add",
+               "oracle_batch_norm", "oracle_batch_norm_ab", "oracle_leaky_relu", "oracle_max_pool2d"):
+        getattr(lib, fn).restype = None
+    return lib
+
+
+def _p(a):
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+def _f32(a):
+    return np.ascontiguousarray(a, dtype=np.float32)
+
+
+class OracleC(object):
+    """numpy-friendly wrappers around the C restatement."""
+
+    def __init__(self):
+        self.lib = load()
+
+    def conv2d_mul(self, xp, kernel_r, oh, ow, kh, kw, sh, sw):
+        xp, kernel_r = _f32(xp), _f32(kernel_r)
+        B, ih, iw, ic = xp.shape
+        od = kernel_r.shape[1]
+        out = np.empty((B, oh, ow, od), np.float32)
+        self.lib.oracle_conv2d_mul(_p(xp), _p(kernel_r), _p(out), B, oh, ow, od, ih, iw, ic, kh, kw, sh, sw)
+        return out
+
+    def conv2d_direct(self, xp, kernel_hwio, oh, ow, sh, sw, nthreads=4):
+        xp, k = _f32(xp), _f32(kernel_hwio)
+        B, ih, iw, ic = xp.shape
+        kh, kw, _, od = k.shape
+        args = np.array([oh, ow, od, ih, iw, ic, kh, kw, sh, sw], np.int32)
+        out = np.empty((B, oh, ow, od), np.float32)
+        self.lib.oracle_conv2d_direct(_p(xp), _p(k), _p(out), B, _p(args), nthreads)
+        return out
+
+    def bias_add(self, x, b):
+        x, b = _f32(x), _f32(b)
+        out = np.empty_like(x)
+        self.lib.oracle_bias_add(_p(x), _p(b), _p(out), *x.shape)
+        return out
+
+    def batch_norm(self, x, mean, var, gamma, eps):
+        x, mean, var, gamma = _f32(x), _f32(mean), _f32(var), _f32(gamma)
+        out = np.empty_like(x)
+        self.lib.oracle_batch_norm(_p(x), _p(mean), _p(var), _p(gamma), float(eps), _p(out), *x.shape)
+        return out
+
+    def batch_norm_ab(self, x, alpha, beta):
+        x, alpha, beta = _f32(x), _f32(alpha), _f32(beta)
+        out = np.empty_like(x)
+        self.lib.oracle_batch_norm_ab(_p(x), _p(alpha), _p(beta), _p(out), *x.shape)
+        return out
+
+    def leaky_relu(self, x, f32_variant=0):
+        x = _f32(x)
+        out = np.empty_like(x)
+        self.lib.oracle_leaky_relu(_p(x), _p(out), *x.shape, int(f32_variant))
+        return out
+
+    def max_pool2d(self, x, ksize, strides, padding, gt_below=0):
+        from ref_numpy import get_out_pads  # noqa: E402  (same directory)
+        x = _f32(x)
+        B, h, w, c = x.shape
+        kh, kw, sh, sw = ksize[1], ksize[2], strides[1], strides[2]
+        oh, pt, _ = get_out_pads(h, kh, sh, padding)
+        ow, pl, _ = get_out_pads(w, kw, sw, padding)
+        out = np.empty((B, oh, ow, c), np.float32)
+        self.lib.oracle_max_pool2d(_p(x), _p(out), B, h, w, c, oh, ow, kh, kw, sh, sw, pt, pl, int(gt_below))
+        return out

@@ -1,0 +1,160 @@
+"""CPU-only checks of the drop-in boundary and the host logic (no GPU compute):
+  * both C-ABI libraries load and export every function include/*.h declares;
+  * the Python mirror keeps the reference's API and ValueError checks;
+  * graph lowering fuses conv->bias->bn->leaky and keeps pools;
+  * the plan's shape inference / memory / algorithmic-FLOP bookkeeping (pure host code)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import PKG, REPO
+
+import dnn_hip
+import synth
+import yolo_graph
+import ref_numpy as R
+
+HEADERS = {
+    "libdnn_hip.so": ["dnn_hip_plan.h", "dnn_hip.h"],
+    "libdnn_hip_avx.so": ["dnn_hip_plan.h", "dnn_hip_avx.h"],
+}
+
+
+def declared_functions(header):
+    text = open(os.path.join(REPO, "include", header)).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    names = re.findall(r"^\s*(?:const\s+)?(?:void|int|char|size_t)\s*\**\s*(\w+)\s*\(", text, flags=re.M)
+    return set(names)
+
+
+@pytest.mark.parametrize("lib", sorted(HEADERS))
+def test_library_exports_every_declared_symbol(lib):
+    so = ctypes.CDLL(os.path.join(PKG, lib))
+    names = set()
+    for h in HEADERS[lib]:
+        names |= declared_functions(h)
+    assert len(names) >= 15
+    missing = [n for n in sorted(names) if not hasattr(so, n)]
+    assert not missing, missing
+
+
+def test_reference_symbol_sets_present():
+    """The exact symbol names the reference wrappers bind."""
+    ob = declared_functions("dnn_hip.h")
+    assert {"conv2d_mul", "conv2d_cublas", "bias_add", "batch_norm", "max_pool2d", "leaky_relu", "im2col"} <= ob
+    av = declared_functions("dnn_hip_avx.h")
+    assert {"conv2d_pthread", "conv2d_cuda_pthread", "bias_add_pthread", "max_pool2d_pthread", "max_pool2d_avx",
+            "batch_norm", "batch_norm_cuda", "leaky_relu"} <= av
+
+
+def test_get_out_pads_matches_reference_rule():
+    for n in range(1, 40):
+        for k in (1, 2, 3):
+            for s in (1, 2, 3):
+                for p in ("SAME", "VALID"):
+                    if p == "VALID" and n < k:
+                        continue
+                    assert dnn_hip.get_out_pads(n, k, s, p) == R.get_out_pads(n, k, s, p)
+
+
+def test_node_value_errors():
+    g = dnn_hip.DnnGraphBuilder()
+    x = g.create_input([1, 5, 5, 3])
+    with pytest.raises(ValueError):
+        g.create_conv2d(x, np.zeros((3, 3, 4, 8), np.float32), [1, 1, 1, 1], "SAME")
+    with pytest.raises(ValueError):
+        g.create_conv2d(x, np.zeros((3, 3, 3, 8), np.float32), [1, 1, 1, 1], "FULL")
+    with pytest.raises(ValueError):
+        g.create_bias_add(x, np.zeros(4, np.float32))
+    with pytest.raises(ValueError):
+        g.create_batch_norm(x, np.zeros(3), np.zeros(4), np.zeros(3), 1e-5)
+    with pytest.raises(ValueError):
+        g.create_max_pool2d(x, [1, 2, 2, 1], [1, 2, 2, 1], "full")
+    c = g.create_conv2d(x, np.zeros((3, 3, 3, 8), np.float32), [1, 2, 2, 1], "SAME")
+    assert c.result.shape == (1, 3, 3, 8)
+    assert c.kernel_r.shape == (27, 8)
+    names = [c.name, g.create_bias_add(c, np.zeros(8, np.float32)).name]
+    # as in the reference, get_name() advances the counter before a constructor raises
+    # (proj3/dnn_openblas.py:81-89): two failed convs and one failed bias_add came first
+    assert names == ["conv2d_2", "bias_add_1"]
+
+
+def test_yolo_graph_lowering():
+    ws = synth.yolo_weights()
+    g, nodes = yolo_graph.build_graph(dnn_hip.DnnGraphBuilder, ws)
+    assert len(nodes) == 40
+    entries = dnn_hip.lower_graph(g)
+    kinds = ["C" if isinstance(e, dnn_hip.ConvEntry) else "P" for e in entries]
+    assert "".join(kinds) == "CPCPCPCPCPCPCCC"
+    convs = [e for e in entries if isinstance(e, dnn_hip.ConvEntry)]
+    assert all(e.bias is not None for e in convs)
+    assert all(e.bn is not None and e.leaky for e in convs[:-1])
+    assert convs[-1].bn is None and not convs[-1].leaky
+    assert sum(len(e.nodes) for e in entries) == 40
+    assert yolo_graph.conv_flops_per_image(ws) == pytest.approx(6.971e9, rel=1e-3)
+
+
+def test_lowering_rejects_unfusable_graph():
+    g = dnn_hip.DnnGraphBuilder()
+    x = g.create_input([1, 4, 4, 8])
+    y = g.create_leaky_relu(x)  # element-wise op with no producing conv
+    g.set_out_node(y)
+    assert dnn_hip.lower_graph(g) is None
+
+
+def test_plan_shape_memory_and_flops_host_only():
+    ws = synth.yolo_weights()
+    g, _ = yolo_graph.build_graph(dnn_hip.DnnGraphBuilder, ws, in_shape=(64, 416, 416, 3))
+    entries = dnn_hip.lower_graph(g)
+    wb, sb = dnn_hip.Plan.memory(64, (416, 416, 3), entries)
+    nparams = sum(w["kernel"].size for w in ws)
+    assert wb >= 4 * nparams and wb < 4 * nparams * 1.2
+    # workspace: two activation buffers (conv0 output, 64x416x416x16) + the largest col
+    act = 64 * 416 * 416 * 16 * 4
+    assert sb >= 2 * act
+    lib = dnn_hip.mylib
+    h = ctypes.c_void_p()
+    assert lib.dnn_plan_create(64, 416, 416, 3, ctypes.byref(h)) == 0
+    try:
+        for e in entries:
+            if isinstance(e, dnn_hip.ConvEntry):
+                kh, kw, _, od = e.conv.kernel.shape
+                assert lib.dnn_plan_add_conv(h, kh, kw, od, 1, 1, 1, None, None, None, None, None, 0.0, 1) == 0
+            else:
+                assert lib.dnn_plan_add_max_pool(h, 2, 2, e.pool.strides[1], e.pool.strides[2], 1) == 0
+        b, oh, ow, oc = (ctypes.c_int() for _ in range(4))
+        lib.dnn_plan_output_shape(h, ctypes.byref(b), ctypes.byref(oh), ctypes.byref(ow), ctypes.byref(oc))
+        assert (b.value, oh.value, ow.value, oc.value) == (64, 13, 13, 125)
+        nk = lib.dnn_plan_num_kernels(h)
+        names, flops = [], 0.0
+        for i in range(nk):
+            nm = ctypes.create_string_buffer(64)
+            fl, by = ctypes.c_double(), ctypes.c_double()
+            assert lib.dnn_plan_kernel_info(h, i, nm, 64, ctypes.byref(fl), ctypes.byref(by)) == 0
+            names.append(nm.value.decode())
+            flops += fl.value
+        assert flops == pytest.approx(64 * 6.971e9, rel=1e-3)
+        # the 1x1 conv8 reads its input directly (no im2col), every 3x3 conv has one
+        assert "conv8.im2col" not in names and "conv8.gemm" in names and "conv7.gemm" in names
+        assert sum(n.endswith(".im2col") for n in names) == 8
+        assert sum(n.startswith("pool") for n in names) == 6
+    finally:
+        lib.dnn_plan_destroy(h)
+
+
+def test_plan_errors_are_reported():
+    lib = dnn_hip.mylib
+    h = ctypes.c_void_p()
+    assert lib.dnn_plan_create(1, 4, 4, 3, ctypes.byref(h)) == 0
+    try:
+        rc = lib.dnn_plan_add_conv(h, 5, 5, 8, 1, 1, 0, None, None, None, None, None, 0.0, 0)  # VALID 5x5 on 4x4
+        assert rc != 0 and "empty output" in dnn_hip.last_error()
+        rc = lib.dnn_plan_add_conv(h, 3, 3, 8, 1, 1, 1, None, None, ctypes.c_void_p(1), None, None, 0.0, 0)
+        assert rc != 0 and "mean/var/gamma" in dnn_hip.last_error()
+        assert lib.dnn_plan_run(h, 1, None, None, None) != 0  # not finalized
+    finally:
+        lib.dnn_plan_destroy(h)
+    assert lib.dnn_plan_create(-1, 4, 4, 3, ctypes.byref(h)) != 0

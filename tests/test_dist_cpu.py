@@ -1,0 +1,86 @@
+"""The N>1 path on CPU: world_size-2 gloo processes drive dist.py exactly as bench.py does on
+RCCL — weights broadcast once from rank 0, each rank computes its contiguous shard, outputs
+gathered to rank 0 — with the numpy oracle standing in for the HIP plan."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from conftest import ORACLE, PKG, REPO
+
+import dist as D
+
+
+def test_shard_range_partitions():
+    for total in (0, 1, 7, 64, 512, 513):
+        for world in (1, 2, 3, 4, 8):
+            seen = []
+            for r in range(world):
+                s, c = D.shard_range(total, world, r)
+                seen.extend(range(s, s + c))
+            assert seen == list(range(total))
+            counts = [D.shard_range(total, world, r)[1] for r in range(world)]
+            assert max(counts) - min(counts) <= 1
+    with pytest.raises(ValueError):
+        D.shard_range(8, 2, 2)
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, total, q):
+    for p in (REPO, PKG, ORACLE):
+        sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import dist as Dw
+    import ref_numpy as R
+    Dw.init("gloo")
+    try:
+        rng = np.random.default_rng(5)
+        k_true = rng.standard_normal((3, 3, 4, 6)).astype(np.float32)
+        frames = rng.standard_normal((total, 9, 7, 4)).astype(np.float32)
+        # only rank 0 holds the real weights; the others start from garbage
+        w = torch.from_numpy(k_true.copy()) if rank == 0 else torch.full(k_true.shape, float(rank))
+        Dw.broadcast_weights(w)
+        kern = w.numpy()
+
+        def compute(inp, out, n):
+            if n:
+                out[:n] = torch.from_numpy(R.conv2d(inp[:n].numpy(), kern, padding="SAME"))
+
+        runner = Dw.ShardedRunner(compute, total, (9, 7, 4), (9, 7, 6), device="cpu")
+        local = torch.from_numpy(runner.local_slice(frames))
+        full = runner.step(local)
+        if rank == 0:
+            expect = R.conv2d(frames, k_true, padding="SAME")
+            q.put(("ok", float(np.abs(full.numpy() - expect).max()), tuple(full.shape)))
+        else:
+            q.put(("ok", None, None))
+    except Exception as e:  # pragma: no cover
+        q.put(("err", repr(e), None))
+    finally:
+        torch.distributed.destroy_process_group()
+
+
+@pytest.mark.parametrize("total", [6, 5])
+def test_sharded_broadcast_gather_gloo_world2(total):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, total, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=60)
+    assert all(r[0] == "ok" for r in res), res
+    root = [r for r in res if r[1] is not None][0]
+    assert root[2] == (total, 9, 7, 6)
+    assert root[1] == 0.0

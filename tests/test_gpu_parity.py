@@ -1,0 +1,319 @@
+"""GPU parity: the HIP path through its C-ABI vs the oracle (ref_numpy / dnn_oracle.c) and the
+golden vectors of the reference's own engine.  Bars: bit-exact for bias_add / batch_norm /
+leaky_relu / max_pool2d / im2col (pure fp32 element-wise or copy work); for convolutions
+(fp32 MFMA, a different summation order than OpenBLAS) max|d| <= 1e-4 * max|ref| per tensor
+(normwise), checked here at a tighter 2e-6 against the float64 oracle per
+layer and 1e-4 on the 9-layer net."""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+
+import dnn_hip
+import ref_numpy as R
+import synth
+import yolo_graph
+from oracle_c import OracleC
+
+pytestmark = pytest.mark.gpu
+
+NET_TOL = 1e-4
+LAYER_TOL = 2e-6
+
+
+class _Fake(object):
+    def __init__(self, arr):
+        self.result = arr
+
+
+@pytest.fixture(scope="module")
+def oc():
+    return OracleC()
+
+
+@pytest.fixture(scope="module")
+def avx():
+    return dnn_hip.load_library("libdnn_hip_avx.so")
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+
+
+# ------------------------------------------------------------------ per-op ABI (libdnn_hip.so)
+@pytest.mark.parametrize("name", ["c3_same", "c3_same_c3", "c3_valid", "c1_same", "c2_same", "c3_wide"])
+def test_conv2d_mul_vs_golden(golden_ops, name):
+    x, k = golden_ops[f"conv_{name}_x"], golden_ops[f"conv_{name}_k"]
+    pad = str(golden_ops[f"conv_{name}_pad"])
+    node = dnn_hip.Conv2D("c", _Fake(x), k, [1, 1, 1, 1], pad)
+    node.run()
+    assert R.normwise_err(node.result, golden_ops[f"conv_{name}_y"]) < 1e-5
+    assert R.normwise_err(node.result, R.conv2d(x, k, padding=pad)) < LAYER_TOL
+
+
+@pytest.mark.parametrize("name", ["a", "b", "c"])
+def test_elementwise_abi_bit_exact(golden_ops, name):
+    g = golden_ops
+    n = dnn_hip.BiasAdd("b", _Fake(g[f"bias_{name}_x"]), g[f"bias_{name}_b"]); n.run()
+    assert np.array_equal(n.result, g[f"bias_{name}_y"])
+    n = dnn_hip.BatchNorm("bn", _Fake(g[f"bn_{name}_x"]), g[f"bn_{name}_mean"], g[f"bn_{name}_var"],
+                          g[f"bn_{name}_gamma"], 1e-5)
+    var_before = n.variance.copy()
+    n.run()
+    assert np.array_equal(n.result, g[f"bn_{name}_y"])
+    assert np.array_equal(n.variance, var_before)  # never mutated (dnn_openblas.c:48-50 does)
+    n.run()
+    assert np.array_equal(n.result, g[f"bn_{name}_y"])  # stable across runs
+    n = dnn_hip.LeakyReLU("l", _Fake(g[f"leaky_{name}_x"])); n.run()
+    assert np.array_equal(n.result, g[f"leaky_{name}_y"])
+
+
+@pytest.mark.parametrize("name", ["k2s2_even", "k2s2_odd", "k2s1_same", "k3s2_valid", "k3s2_same"])
+def test_max_pool_abi_bit_exact(golden_ops, name):
+    g = golden_ops
+    k, s = g[f"pool_{name}_k"], g[f"pool_{name}_s"]
+    n = dnn_hip.MaxPool2D("p", _Fake(g[f"pool_{name}_x"]), [1, int(k[0]), int(k[1]), 1],
+                          [1, int(s[0]), int(s[1]), 1], str(g[f"pool_{name}_pad"]))
+    n.run()
+    assert np.array_equal(n.result, g[f"pool_{name}_y"])
+
+
+def test_conv2d_mul_batched_and_strided(oc):
+    """Batch > 1 is strided by ih*iw*ic (the reference strides by oh*ow*od, dnn_openblas.c:170)."""
+    rng = np.random.default_rng(11)
+    for (B, H, W, C, od, s) in [(3, 11, 9, 7, 12, 1), (2, 12, 10, 8, 20, 2)]:
+        x = rng.standard_normal((B, H, W, C)).astype(np.float32)
+        k = rng.standard_normal((3, 3, C, od)).astype(np.float32)
+        node = dnn_hip.Conv2D("c", _Fake(x), k, [1, s, s, 1], "SAME")
+        node.run()
+        ref = R.conv2d(x, k, strides=[1, s, s, 1], padding="SAME")
+        assert R.normwise_err(node.result, ref) < LAYER_TOL
+        xp, oh, ow = R.pad_nhwc(x, 3, 3, s, s, "SAME")
+        kr = np.ascontiguousarray(k.transpose(2, 0, 1, 3).reshape(-1, od))
+        assert R.normwise_err(node.result, oc.conv2d_mul(xp, kr, oh, ow, 3, 3, s, s)) < LAYER_TOL
+
+
+def test_im2col_abi_bit_exact(oc):
+    lib = dnn_hip.mylib
+    rng = np.random.default_rng(4)
+    xp = rng.standard_normal((1, 9, 8, 6)).astype(np.float32)
+    oh, ow, kh, kw, sh, sw = 4, 3, 3, 3, 2, 2
+    col = np.zeros((oh * ow, 6 * 9), np.float32)
+    lib.im2col(_p(xp), _p(col), oh, ow, 9, 8, 6, kh, kw, sh, sw)
+    assert dnn_hip.last_error() == ""
+    ref = np.empty_like(col)
+    oc.lib.oracle_im2col(xp.ctypes.data, ref.ctypes.data, oh, ow, 9, 8, 6, kh, kw, sh, sw)
+    assert np.array_equal(col, ref)
+
+
+def test_legacy_error_is_raised():
+    x = np.zeros((1, 4, 4, 3), np.float32)
+    node = dnn_hip.Conv2D("c", _Fake(x), np.zeros((3, 3, 3, 4), np.float32), [1, 1, 1, 1], "VALID")
+    node.result = np.zeros((1, 5, 5, 4), np.float32)  # inconsistent with the padded input
+    with pytest.raises(dnn_hip.DnnHipError):
+        node.run()
+
+
+# ------------------------------------------------------------------ AVX / CUDA ABI (libdnn_hip_avx.so)
+def test_avx_abi(avx, oc):
+    rng = np.random.default_rng(21)
+    B, H, W, C, od = 2, 9, 8, 12, 20
+    x = rng.standard_normal((B, H, W, C)).astype(np.float32)
+    k = rng.standard_normal((3, 3, C, od)).astype(np.float32)
+    xp, oh, ow = R.pad_nhwc(x, 3, 3, 1, 1, "SAME")
+    xp = np.ascontiguousarray(xp)
+    args = np.array([oh, ow, od, xp.shape[1], xp.shape[2], C, 3, 3, 1, 1], np.int32)
+    out = np.zeros((B, oh, ow, od), np.float32)
+    avx.conv2d_pthread(_p(xp), _p(k), _p(out), B, args.ctypes.data_as(ctypes.POINTER(ctypes.c_int)))
+    assert dnn_hip.last_error(avx) == ""
+    ref = R.conv2d(x, k, padding="SAME")
+    assert R.normwise_err(out, ref) < LAYER_TOL
+    kr = np.ascontiguousarray(k.transpose(2, 0, 1, 3).reshape(-1, od))
+    out2 = np.zeros_like(out)
+    avx.conv2d_cuda_pthread(_p(xp), _p(out2), _p(kr), _p(out2), B, args.ctypes.data_as(ctypes.POINTER(ctypes.c_int)))
+    assert R.normwise_err(out2, ref) < LAYER_TOL
+
+    y = ref
+    b = rng.standard_normal(od).astype(np.float32)
+    r = np.zeros_like(y)
+    avx.bias_add_pthread(_p(y), _p(b), _p(r), *y.shape)
+    assert np.array_equal(r, oc.bias_add(y, b))
+    alpha = rng.uniform(0.5, 1.5, od).astype(np.float32)
+    beta = rng.uniform(-0.1, 0.1, od).astype(np.float32)
+    for fn in (avx.batch_norm, avx.batch_norm_cuda):
+        r = np.zeros_like(y)
+        fn(_p(y), _p(alpha), _p(beta), _p(r), *y.shape)
+        assert np.array_equal(r, oc.batch_norm_ab(y, alpha, beta))
+    r = np.zeros_like(y)
+    avx.leaky_relu(_p(y), _p(r), *y.shape)
+    assert np.array_equal(r, R.leaky_relu_avx(y))
+
+    # max pool, with signed zeros so `>` (vector channels) and `>=` (tail) differ
+    z = rng.choice(np.array([0.0, -0.0, 1.0, -1.0], np.float32), size=(B, 8, 8, od)).astype(np.float32)
+    zp = np.ascontiguousarray(z)
+    pargs = np.array([4, 4, od, 8, 8, od, 2, 2, 2, 2], np.int32)
+    r = np.zeros((B, 4, 4, od), np.float32)
+    avx.max_pool2d_pthread(_p(zp), _p(r), B, pargs.ctypes.data_as(ctypes.POINTER(ctypes.c_int)))
+    gt = od - od % 8
+    ref = oc.max_pool2d(z, [1, 2, 2, 1], [1, 2, 2, 1], "VALID", gt_below=gt)
+    assert np.array_equal(r.view(np.int32), ref.view(np.int32))
+    r2 = np.zeros_like(r)
+    avx.max_pool2d_avx(_p(zp), _p(r2), B, 4, 4, od, 8, 8, od, 2, 2, 2, 2)
+    assert np.array_equal(r2.view(np.int32), ref.view(np.int32))
+    r3 = np.zeros_like(r)
+    dnn_hip.mylib.max_pool2d(_p(zp), _p(r3), B, 4, 4, od, 8, 8, od, 2, 2, 2, 2)
+    assert np.array_equal(r3.view(np.int32), oc.max_pool2d(z, [1, 2, 2, 1], [1, 2, 2, 1], "VALID").view(np.int32))
+
+
+# ------------------------------------------------------------------ fused plan, single layers
+def _chain(x_shape, k, strides=(1, 1, 1, 1), pad="SAME", bias=None, bn=None, leaky=False, pool=None):
+    g = dnn_hip.DnnGraphBuilder()
+    y = g.create_input(list(x_shape))
+    y = g.create_conv2d(y, k, list(strides), pad)
+    if bias is not None:
+        y = g.create_bias_add(y, bias)
+    if bn is not None:
+        y = g.create_batch_norm(y, *bn, 1e-5)
+    if leaky:
+        y = g.create_leaky_relu(y)
+    if pool is not None:
+        y = g.create_max_pool2d(y, [1, pool[0], pool[0], 1], [1, pool[1], pool[1], 1], pool[2])
+    g.set_out_node(y)
+    return g
+
+
+def _oracle_chain(x, k, strides=(1, 1, 1, 1), pad="SAME", bias=None, bn=None, leaky=False, pool=None):
+    y = R.conv2d(x, k, strides=strides, padding=pad)
+    if bias is not None:
+        y = R.bias_add(y, bias)
+    if bn is not None:
+        y = R.batch_norm(y, *bn, 1e-5)
+    if leaky:
+        y = R.leaky_relu(y)
+    if pool is not None:
+        y = R.max_pool2d(y, [1, pool[0], pool[0], 1], [1, pool[1], pool[1], 1], pool[2])
+    return y
+
+
+FUSED_CASES = [
+    # B, H, W, C, kh, od, stride, pad, pool  -> exercises every GEMM config and edge
+    (2, 40, 38, 3, 3, 16, 1, "SAME", (2, 2, "SAME")),     # cfg 256x16 (K=27 -> 32), conv0-like
+    (1, 30, 26, 16, 3, 32, 1, "SAME", (2, 2, "SAME")),    # cfg 256x32 (K=144)
+    (2, 17, 15, 32, 3, 64, 1, "SAME", None),              # cfg 128x64
+    (8, 20, 20, 64, 3, 128, 1, "SAME", (2, 1, "SAME")),   # M=3200, 25 128-tiles -> cfg 64x128
+    (64, 13, 13, 96, 3, 1024, 1, "SAME", None),           # M=10816, N=1024 -> cfg 128x128 (conv7-like)
+    (3, 13, 13, 64, 1, 125, 1, "SAME", None),             # 1x1 direct path, ragged N=125
+    (2, 9, 11, 5, 3, 48, 2, "SAME", None),                # stride 2, K=45 not a multiple of BK
+    (1, 10, 9, 8, 3, 24, 1, "VALID", None),               # VALID
+]
+
+
+@pytest.mark.parametrize("case", FUSED_CASES)
+def test_fused_conv_bn_leaky_pool(case):
+    B, H, W, C, kh, od, s, pad, pool = case
+    rng = np.random.default_rng(B * 1000 + C * 10 + od)
+    x = rng.standard_normal((B, H, W, C)).astype(np.float32)
+    k = (rng.standard_normal((kh, kh, C, od)) * np.sqrt(2.0 / (kh * kh * C))).astype(np.float32)
+    bias = rng.standard_normal(od).astype(np.float32) * 0.1
+    bn = (rng.standard_normal(od).astype(np.float32) * 0.1, rng.uniform(0.5, 1.5, od).astype(np.float32),
+          rng.uniform(0.5, 1.5, od).astype(np.float32))
+    kw = dict(strides=(1, s, s, 1), pad=pad, bias=bias, bn=bn, leaky=True, pool=pool)
+    g = _chain(x.shape, k, **kw)
+    assert dnn_hip.lower_graph(g) is not None
+    y = dnn_hip.DnnInferenceEngine(g, False).run(x)
+    ref = _oracle_chain(x, k, **kw)
+    assert y.shape == ref.shape
+    assert R.normwise_err(y, ref) < LAYER_TOL
+    # conv-only variant (no epilogue ops)
+    g2 = _chain(x.shape, k, strides=(1, s, s, 1), pad=pad)
+    y2 = dnn_hip.DnnInferenceEngine(g2, False).run(x)
+    assert R.normwise_err(y2, R.conv2d(x, k, strides=(1, s, s, 1), padding=pad)) < LAYER_TOL
+
+
+def test_fused_epilogue_is_reference_order():
+    """With an exactly representable conv (integer data, small K) the fused epilogue must equal
+    bias_add -> batch_norm -> leaky_relu applied separately, bit for bit."""
+    rng = np.random.default_rng(8)
+    x = rng.integers(-3, 4, size=(2, 12, 12, 8)).astype(np.float32)
+    k = rng.integers(-2, 3, size=(3, 3, 8, 40)).astype(np.float32)
+    bias = rng.standard_normal(40).astype(np.float32)
+    bn = (rng.standard_normal(40).astype(np.float32), rng.uniform(0.5, 1.5, 40).astype(np.float32),
+          rng.uniform(0.5, 1.5, 40).astype(np.float32))
+    g = _chain(x.shape, k, bias=bias, bn=bn, leaky=True)
+    y = dnn_hip.DnnInferenceEngine(g, False).run(x)
+    assert np.array_equal(y, _oracle_chain(x, k, bias=bias, bn=bn, leaky=True))
+
+
+# ------------------------------------------------------------------ whole YOLOv2-tiny net
+@pytest.fixture(scope="module")
+def yolo_b1(yolo_weights):
+    g, _ = yolo_graph.build_graph(dnn_hip.DnnGraphBuilder, yolo_weights, in_shape=(1, 416, 416, 3))
+    return dnn_hip.DnnInferenceEngine(g, False)
+
+
+@pytest.mark.parametrize("frame", [0, 1, 2, 3])
+def test_yolo_batch1_vs_reference_golden(yolo_b1, golden_frames, frame):
+    y = yolo_b1.run(synth.frame(frame))
+    assert y.shape == (1, 13, 13, 125)
+    err = R.normwise_err(y, golden_frames[frame])
+    assert err < NET_TOL, err
+
+
+def test_yolo_repeat_runs_identical(yolo_b1):
+    a = yolo_b1.run(synth.frame(0)).copy()
+    b = yolo_b1.run(synth.frame(0))
+    assert np.array_equal(a, b)  # no cross-run state (the reference drifts)
+
+
+def test_yolo_node_by_node_debug_path(yolo_weights, golden_frames, tmp_path, monkeypatch):
+    """debug=True runs the reference's per-node traversal through the per-op ABI and dumps
+    every layer like proj3/dnn_openblas.py:47-50."""
+    import os
+    monkeypatch.chdir(tmp_path)
+    g, nodes = yolo_graph.build_graph(dnn_hip.DnnGraphBuilder, yolo_weights, in_shape=(1, 416, 416, 3))
+    y = dnn_hip.DnnInferenceEngine(g, True).run(synth.frame(0))
+    assert R.normwise_err(y, golden_frames[0]) < NET_TOL
+    files = sorted(os.listdir(tmp_path / "intermediate"))
+    assert len(files) == 40 and "layer_1.npy" in files and "layer_40.npy" in files
+    from conftest import GOLDEN
+    st = np.load(os.path.join(GOLDEN, "nodes_frame0.npz"))
+    for k, n in enumerate(nodes):
+        r = np.asarray(n.result)
+        idx = np.linspace(0, r.size - 1, 64).astype(np.int64)
+        assert R.normwise_err(r.reshape(-1)[idx], st[f"sample_{k}"]) < NET_TOL, k
+
+
+def test_yolo_batch64_golden_indices_and_batch_invariance(yolo_weights, golden_frames, yolo_b1):
+    """Batch 64 with the 4 golden frames at 0/17/42/63: each row must match
+    its golden, and every row must equal the batch-1 run of the same frame bit for bit
+    (images are independent and the k-order of the MFMA reduction does not depend on M)."""
+    slots = {0: 0, 17: 1, 42: 2, 63: 3}
+    idx = [slots.get(i, 100 + i) for i in range(64)]
+    x = synth.frames(idx)
+    g, _ = yolo_graph.build_graph(dnn_hip.DnnGraphBuilder, yolo_weights, in_shape=(64, 416, 416, 3))
+    eng = dnn_hip.DnnInferenceEngine(g, False)
+    y = eng.run(x)
+    assert y.shape == (64, 13, 13, 125)
+    for pos, f in slots.items():
+        assert R.normwise_err(y[pos], golden_frames[f][0]) < NET_TOL
+    for pos in (0, 5, 17, 42, 63):
+        assert np.array_equal(y[pos:pos + 1], yolo_b1.run(x[pos:pos + 1]))
+    # ragged n < batch and n == 0 through the same plan
+    plan = eng.plan()
+    y5 = plan.run_host(x[:5])
+    assert np.array_equal(y5, y[:5])
+    assert plan.run_host(x[:0]).shape == (0, 13, 13, 125)
+
+
+def test_plan_timing_api(yolo_b1):
+    plan = yolo_b1.plan()
+    x = synth.frame(1)
+    plan.timing_begin(3)
+    for _ in range(3):
+        plan.run_host(x)
+    ms, cnt = plan.timing_end()
+    ks = plan.kernels()
+    assert len(ms) == len(ks) == 23
+    assert all(c == 3 for c in cnt)
+    assert all(m > 0 for m in ms)
