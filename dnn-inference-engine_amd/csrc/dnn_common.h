@@ -73,8 +73,8 @@ enum GemmCfg : int {
   GEMM_256x16_K32 = 0,   // N <= 16 (conv0), MFMA 16x16x4
   GEMM_256x32_K16 = 1,   // N <= 32 (conv1), MFMA 16x16x4
   GEMM_128x64_K32 = 2,   // N <= 64, MFMA 32x32x2
-  GEMM_128x128_K32 = 3,  // wide layers, MFMA 32x32x2
-  GEMM_64x128_K32 = 4,   // wide layers with few M tiles, MFMA 32x32x2
+  GEMM_128x128_K32 = 3,  // long-K wide layers (conv6/7): LDS-DMA 2-stage ring, MFMA 32x32x2
+  GEMM_64x128_K32 = 4,   // other N >= 128 layers: LDS-DMA 3-stage ring, MFMA 32x32x2
   GEMM_NUM_CFGS = 5,
 };
 int gemm_cfg_bm(int cfg);

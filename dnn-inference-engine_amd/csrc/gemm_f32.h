@@ -1,0 +1,364 @@
+// fp32 MFMA GEMM kernels for the conv hot path (gfx950), device code only.
+//
+// C[M][N] = A[M][K] * Bt[N][K]^T with a fused per-output-channel epilogue.
+//   A  : im2col rows (or the NHWC input itself for 1x1 convs), row-major, lda >= K
+//   Bt : packed weights, row n = output channel, K contiguous (HWIO -> [N][K])
+//   C  : NHWC output, row = output pixel, ldc = number of channels
+// This replaces cblas_sgemm(RowMajor, N, N, M=oh*ow, N=od, K=ic*kh*kw, 1, col, K,
+// kernel_r, od, 0, out, od) of proj3/dnn_openblas.c:184-192 and the bias/bn/leaky passes
+// that follow it (proj3/dnn_openblas.c:9-65, 236-254).
+//
+// Two main loops:
+//   gemm_f32_mfma_kernel   register-staged global->LDS double buffer (any BK, any tile)
+//   gemm_f32_glds_kernel   LDS-DMA (global_load_lds_dwordx4) ring of NS stages with a
+//                          counted vmcnt across raw s_barriers (cdna_hip_programming.md
+//                          §5 "Pipelining across barriers"); LDS image XOR-swizzled on the
+//                          SOURCE address so the fragment reads are conflict-free.
+#pragma once
+#include <hip/hip_runtime.h>
+#include "dnn_common.h"
+
+namespace dnnhip {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ float apply_epilogue(float v, float bias, float mean, float sq, float gamma,
+                                                int flags) {
+  if (flags & EPI_BIAS) v = v + bias;
+  if (flags & EPI_BN) v = ((v - mean) / sq) * gamma;
+  if (flags & EPI_BN_AB) v = v * mean - sq;
+  if (flags & EPI_LEAKY_F64) v = v < 0.f ? (float)(0.1 * (double)v) : v;
+  if (flags & EPI_LEAKY_F32) {
+    float t = v * 0.1f;
+    v = v > t ? v : t;
+  }
+  return v;
+}
+
+template <int MF>
+struct Mfma;
+
+// v_mfma_f32_32x32x2_f32: lane l supplies A[l&31][k=l>>5], B[k=l>>5][l&31];
+// D[row][col]: col = l&31, row = (reg&3) + 8*(reg>>2) + 4*(l>>5).
+template <>
+struct Mfma<32> {
+  typedef f32x16 acc_t;
+  static constexpr int KG = 8;  // k covered by one 16-byte fragment read (2 lane halves x 4 steps)
+  static constexpr int PARTS = 2;
+  static constexpr int REGS = 16;
+  __device__ static __forceinline__ acc_t op(float a, float b, acc_t c) {
+    return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+  }
+  __device__ static __forceinline__ int frag_row(int lane) { return lane & 31; }
+  __device__ static __forceinline__ int frag_part(int lane) { return lane >> 5; }
+  __device__ static __forceinline__ int out_row(int lane, int reg) { return (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5); }
+  __device__ static __forceinline__ int out_col(int lane) { return lane & 31; }
+};
+
+// v_mfma_f32_16x16x4_f32: lane l supplies A[l&15][k=l>>4], B[k=l>>4][l&15];
+// D[row][col]: col = l&15, row = 4*(l>>4) + reg.
+template <>
+struct Mfma<16> {
+  typedef f32x4 acc_t;
+  static constexpr int KG = 16;  // 4 lane quarters x 4 steps
+  static constexpr int PARTS = 4;
+  static constexpr int REGS = 4;
+  __device__ static __forceinline__ acc_t op(float a, float b, acc_t c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+  }
+  __device__ static __forceinline__ int frag_row(int lane) { return lane & 15; }
+  __device__ static __forceinline__ int frag_part(int lane) { return lane >> 4; }
+  __device__ static __forceinline__ int out_row(int lane, int reg) { return 4 * (lane >> 4) + reg; }
+  __device__ static __forceinline__ int out_col(int lane) { return lane & 15; }
+};
+
+// XCD-aware bijective block remap: the 8 XCDs each get a contiguous range of tiles, so the
+// N tiles of one A row-panel run under one L2 (cdna_hip_programming.md T1).
+__device__ __forceinline__ int xcd_tile(int bid, int nb) {
+  const int xcd = bid & 7, q = nb >> 3, rr = nb & 7;
+  return (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (bid >> 3);
+}
+
+// Fused epilogue + store of one wave's accumulators (NHWC: row = pixel, col = channel).
+template <int MF, int TM, int TN, int WTM, int WTN>
+__device__ __forceinline__ void store_tile(const typename Mfma<MF>::acc_t (&acc)[TM][TN], float* __restrict__ C,
+                                           int ldc, int M, int N, int m0, int n0, int wm, int wn, int lane,
+                                           const EpiParams& epi) {
+  typedef Mfma<MF> MM;
+  const int oc = MM::out_col(lane);
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int n = n0 + wn * WTN + j * MF + oc;
+    const float pb = (epi.flags & EPI_BIAS) ? epi.bias[n] : 0.f;
+    const float pm = (epi.flags & (EPI_BN | EPI_BN_AB)) ? epi.mean[n] : 0.f;
+    const float ps = (epi.flags & (EPI_BN | EPI_BN_AB)) ? epi.sq[n] : 1.f;
+    const float pg = (epi.flags & EPI_BN) ? epi.gamma[n] : 1.f;
+    if (n < N) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+#pragma unroll
+        for (int r = 0; r < MM::REGS; ++r) {
+          const int m = m0 + wm * WTM + i * MF + MM::out_row(lane, r);
+          if (m < M) C[(size_t)m * ldc + n] = apply_epilogue(acc[i][j][r], pb, pm, ps, pg, epi.flags);
+        }
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Register-staged double buffer.  K permutation: inside a KG-wide group, lane part p reads
+// k = KG*g + 4p + (0..3) with one ds_read_b128 and feeds them to 4 consecutive MFMAs. A and
+// B use the same mapping, so the reduction still covers every k exactly once.
+template <int BM, int BN, int BK, int WM, int WN, int MF>
+__global__ void __launch_bounds__(WM* WN * 64)
+gemm_f32_mfma_kernel(const float* __restrict__ A, int lda, const float* __restrict__ Bt, int ldb,
+                     float* __restrict__ C, int ldc, int M, int N, int K, EpiParams epi, int tilesN) {
+  typedef Mfma<MF> MM;
+  typedef typename MM::acc_t acc_t;
+  constexpr int T = WM * WN * 64;
+  constexpr int LS = BK + 4;  // LDS row stride (floats): breaks the power-of-two bank aliasing
+  constexpr int WTM = BM / WM, WTN = BN / WN;
+  constexpr int TM = WTM / MF, TN = WTN / MF;
+  constexpr int KQ = BK / 4;
+  constexpr int A_V4 = BM * KQ, B_V4 = BN * KQ;
+  constexpr int A_LD = (A_V4 + T - 1) / T, B_LD = (B_V4 + T - 1) / T;
+  static_assert(BK % MM::KG == 0, "BK must be a multiple of the fragment group");
+  static_assert(WTM % MF == 0 && WTN % MF == 0, "wave tile must be a multiple of the MFMA tile");
+
+  __shared__ __attribute__((aligned(16))) float smem[2 * (BM + BN) * LS];
+
+  const int tile = xcd_tile(blockIdx.x, gridDim.x);
+  const int tm_ = tile / tilesN, tn_ = tile - tm_ * tilesN;
+  const int m0 = tm_ * BM, n0 = tn_ * BN;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid - (wid / WN) * WN;
+
+  f32x4 ra[A_LD], rb[B_LD];
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < A_LD; ++i) {
+      int idx = tid + i * T;
+      if (A_V4 % T == 0 || idx < A_V4) {
+        int row = idx / KQ, c4 = idx - (idx / KQ) * KQ;
+        int gm = m0 + row;
+        gm = gm < M ? gm : M - 1;
+        ra[i] = *reinterpret_cast<const f32x4*>(A + (size_t)gm * lda + k0 + c4 * 4);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < B_LD; ++i) {
+      int idx = tid + i * T;
+      if (B_V4 % T == 0 || idx < B_V4) {
+        int row = idx / KQ, c4 = idx - (idx / KQ) * KQ;
+        rb[i] = *reinterpret_cast<const f32x4*>(Bt + (size_t)(n0 + row) * ldb + k0 + c4 * 4);
+      }
+    }
+  };
+  auto sstore = [&](float* As, float* Bs) {
+#pragma unroll
+    for (int i = 0; i < A_LD; ++i) {
+      int idx = tid + i * T;
+      if (A_V4 % T == 0 || idx < A_V4) {
+        int row = idx / KQ, c4 = idx - (idx / KQ) * KQ;
+        *reinterpret_cast<f32x4*>(As + row * LS + c4 * 4) = ra[i];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < B_LD; ++i) {
+      int idx = tid + i * T;
+      if (B_V4 % T == 0 || idx < B_V4) {
+        int row = idx / KQ, c4 = idx - (idx / KQ) * KQ;
+        *reinterpret_cast<f32x4*>(Bs + row * LS + c4 * 4) = rb[i];
+      }
+    }
+  };
+
+  acc_t acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < MM::REGS; ++r) acc[i][j][r] = 0.f;
+
+  const int fr = MM::frag_row(lane), fk = 4 * MM::frag_part(lane);
+  const int a_base = (wm * WTM + fr) * LS + fk;
+  const int b_base = (wn * WTN + fr) * LS + fk;
+
+  const int nk = K / BK;
+  gload(0);
+  sstore(smem, smem + BM * LS);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    float* As = smem + (kt & 1) * (BM + BN) * LS;
+    float* Bs = As + BM * LS;
+    if (kt + 1 < nk) gload((kt + 1) * BK);
+#pragma unroll
+    for (int g = 0; g < BK / MM::KG; ++g) {
+      f32x4 af[TM], bf[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        af[i] = *reinterpret_cast<const f32x4*>(As + a_base + i * MF * LS + g * MM::KG);
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        bf[j] = *reinterpret_cast<const f32x4*>(Bs + b_base + j * MF * LS + g * MM::KG);
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] = MM::op(af[i][s], bf[j][s], acc[i][j]);
+    }
+    if (kt + 1 < nk) {
+      float* Asn = smem + ((kt + 1) & 1) * (BM + BN) * LS;
+      sstore(Asn, Asn + BM * LS);
+    }
+    __syncthreads();
+  }
+  store_tile<MF, TM, TN, WTM, WTN>(acc, C, ldc, M, N, m0, n0, wm, wn, lane, epi);
+}
+
+// ---------------------------------------------------------------------------------------
+// LDS-DMA ring.  BK = 32: one tile row is 128 B = 8 slots of 16 B, one wave instruction of
+// global_load_lds_dwordx4 fills one 1-KiB chunk = 8 rows (lane l -> row l/8, slot l%8).
+// Slot swizzle: physical slot = logical slot ^ ((row >> 1) & 7).  It is applied to the
+// per-lane SOURCE address (the DMA destination is lane-linear) and to the fragment read
+// address; every 16-lane group of a ds_read_b128 then hits 16 distinct 16-B bank slots for
+// both the 32x32x2 (rows l&31, parts l>>5) and 16x16x4 (rows l&15, parts l>>4) fragments.
+//
+// Pipeline per K-step kt (NS stages in the ring, counted waits, raw barriers):
+//   s_waitcnt vmcnt(#chunks of the stages issued after kt)   -> stage kt landed (own DMAs)
+//   s_barrier                                                 -> everyone's DMAs landed, and
+//                                                                everyone finished reading kt-1
+//   issue stage kt+NS-1 into the slot of kt-1
+//   ds_read + MFMA on stage kt
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+__device__ __forceinline__ void wait_lgkm0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ void raw_barrier() { __builtin_amdgcn_s_barrier(); }
+__device__ __forceinline__ int wave_uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
+// one global_load_lds_dwordx4: 16 B per lane from `src` (per lane) into `dst` + 16*lane
+// (`dst` wave-uniform)
+__device__ __forceinline__ void lds_dma16(const float* src, float* dst) {
+  __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+}
+
+template <int BM, int BN, int WM, int WN, int MF, int NS>
+__global__ void __launch_bounds__(WM* WN * 64)
+gemm_f32_glds_kernel(const float* __restrict__ A, int lda, const float* __restrict__ Bt, int ldb,
+                     float* __restrict__ C, int ldc, int M, int N, int K, EpiParams epi, int tilesN) {
+  typedef Mfma<MF> MM;
+  typedef typename MM::acc_t acc_t;
+  constexpr int BK = 32;
+  constexpr int NW = WM * WN;
+  constexpr int WTM = BM / WM, WTN = BN / WN;
+  constexpr int TM = WTM / MF, TN = WTN / MF;
+  constexpr int A_CH = BM / 8, B_CH = BN / 8, CH = A_CH + B_CH;
+  constexpr int LPS = CH / NW;              // DMA instructions per wave per stage
+  constexpr int STAGE = (BM + BN) * BK;     // floats per stage
+  static_assert(CH % NW == 0, "chunks must split evenly over the waves");
+  static_assert(NS >= 2 && NS <= 4, "ring depth");
+  static_assert(WTM % MF == 0 && WTN % MF == 0, "wave tile must be a multiple of the MFMA tile");
+
+  __shared__ __attribute__((aligned(1024))) float smem[NS * STAGE];
+
+  const int tile = xcd_tile(blockIdx.x, gridDim.x);
+  const int tm_ = tile / tilesN, tn_ = tile - tm_ * tilesN;
+  const int m0 = tm_ * BM, n0 = tn_ * BN;
+  const int lane = threadIdx.x & 63;
+  const int wid = wave_uniform(threadIdx.x >> 6);
+  const int wm = wid / WN, wn = wid - (wid / WN) * WN;
+
+  // per-lane DMA sources (at k = 0) and wave-uniform chunk destinations
+  const float* src[LPS];
+  int dst[LPS];
+#pragma unroll
+  for (int i = 0; i < LPS; ++i) {
+    const int c = wid + i * NW;
+    const bool isA = c < A_CH;
+    const int r = 8 * (isA ? c : c - A_CH) + (lane >> 3);
+    const int slot = (lane & 7) ^ ((r >> 1) & 7);
+    if (isA) {
+      int gm = m0 + r;
+      gm = gm < M ? gm : M - 1;
+      src[i] = A + (size_t)gm * lda + slot * 4;
+    } else {
+      src[i] = Bt + (size_t)(n0 + r) * ldb + slot * 4;
+    }
+    dst[i] = c * 256;  // 1 KiB chunk, floats
+  }
+  auto issue = [&](int stage, int k0) {
+    float* base = smem + stage * STAGE;
+#pragma unroll
+    for (int i = 0; i < LPS; ++i)
+      lds_dma16(src[i] + k0, base + dst[i]);
+  };
+
+  acc_t acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < MM::REGS; ++r) acc[i][j][r] = 0.f;
+
+  // fragment read offsets: row base + swizzled slot for each K group
+  const int fr = MM::frag_row(lane), fp = MM::frag_part(lane);
+  const int sw = (fr >> 1) & 7;
+  constexpr int NG = BK / MM::KG;
+  int kofs[NG];
+#pragma unroll
+  for (int g = 0; g < NG; ++g) kofs[g] = 4 * ((g * MM::PARTS + fp) ^ sw);
+  const int a_row = (wm * WTM + fr) * BK;
+  const int b_row = BM * BK + (wn * WTN + fr) * BK;
+
+  const int nk = K / BK;
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s)
+    if (s < nk) issue(s, s * BK);
+
+  int stage = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    // own DMAs of stage kt have landed once only the younger stages' remain outstanding
+    const int ahead = nk - 1 - kt < NS - 2 ? nk - 1 - kt : NS - 2;
+    if (ahead >= 2)
+      wait_vmcnt<2 * LPS>();
+    else if (ahead == 1)
+      wait_vmcnt<LPS>();
+    else
+      wait_vmcnt<0>();
+    raw_barrier();
+    if (kt + NS - 1 < nk) {
+      int ns = stage + NS - 1;
+      ns = ns >= NS ? ns - NS : ns;
+      issue(ns, (kt + NS - 1) * BK);
+    }
+    const float* S = smem + stage * STAGE;
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      f32x4 af[TM], bf[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const f32x4*>(S + a_row + i * MF * BK + kofs[g]);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bf[j] = *reinterpret_cast<const f32x4*>(S + b_row + j * MF * BK + kofs[g]);
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] = MM::op(af[i][s], bf[j][s], acc[i][j]);
+    }
+    // this wave's reads of `stage` are complete before it can pass the next barrier
+    wait_lgkm0();
+    stage = stage + 1 == NS ? 0 : stage + 1;
+  }
+  store_tile<MF, TM, TN, WTM, WTN>(acc, C, ldc, M, N, m0, n0, wm, wn, lane, epi);
+}
+
+}  // namespace dnnhip

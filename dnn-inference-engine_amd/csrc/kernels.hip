@@ -16,11 +16,9 @@
 #include <hip/hip_runtime.h>
 #include <cfloat>
 #include "dnn_common.h"
+#include "gemm_f32.h"
 
 namespace dnnhip {
-
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 static inline int ceil_div_i(long long a, long long b) { return (int)((a + b - 1) / b); }
 
@@ -117,192 +115,6 @@ int launch_im2col(const float* in, float* col, const ConvGeom& g, hipStream_t st
   return check_launch("im2col");
 }
 
-// ============================================================================ GEMM
-__device__ __forceinline__ float apply_epilogue(float v, float bias, float mean, float sq, float gamma,
-                                                int flags) {
-  if (flags & EPI_BIAS) v = v + bias;
-  if (flags & EPI_BN) v = ((v - mean) / sq) * gamma;
-  if (flags & EPI_BN_AB) v = v * mean - sq;
-  if (flags & EPI_LEAKY_F64) v = v < 0.f ? (float)(0.1 * (double)v) : v;
-  if (flags & EPI_LEAKY_F32) {
-    float t = v * 0.1f;
-    v = v > t ? v : t;
-  }
-  return v;
-}
-
-template <int MF>
-struct Mfma;
-
-// v_mfma_f32_32x32x2_f32: lane l supplies A[l&31][k=l>>5], B[k=l>>5][l&31];
-// D[row][col]: col = l&31, row = (reg&3) + 8*(reg>>2) + 4*(l>>5).
-template <>
-struct Mfma<32> {
-  typedef f32x16 acc_t;
-  static constexpr int KG = 8;  // k covered by one 16-byte fragment read (2 lane halves x 4 steps)
-  static constexpr int REGS = 16;
-  __device__ static __forceinline__ acc_t op(float a, float b, acc_t c) {
-    return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
-  }
-  __device__ static __forceinline__ int frag_row(int lane) { return lane & 31; }
-  __device__ static __forceinline__ int frag_kofs(int lane) { return 4 * (lane >> 5); }
-  __device__ static __forceinline__ int out_row(int lane, int reg) { return (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5); }
-  __device__ static __forceinline__ int out_col(int lane) { return lane & 31; }
-};
-
-// v_mfma_f32_16x16x4_f32: lane l supplies A[l&15][k=l>>4], B[k=l>>4][l&15];
-// D[row][col]: col = l&15, row = 4*(l>>4) + reg.
-template <>
-struct Mfma<16> {
-  typedef f32x4 acc_t;
-  static constexpr int KG = 16;  // 4 lane quarters x 4 steps
-  static constexpr int REGS = 4;
-  __device__ static __forceinline__ acc_t op(float a, float b, acc_t c) {
-    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
-  }
-  __device__ static __forceinline__ int frag_row(int lane) { return lane & 15; }
-  __device__ static __forceinline__ int frag_kofs(int lane) { return 4 * (lane >> 4); }
-  __device__ static __forceinline__ int out_row(int lane, int reg) { return 4 * (lane >> 4) + reg; }
-  __device__ static __forceinline__ int out_col(int lane) { return lane & 15; }
-};
-
-// K permutation: inside a KG-wide group, lane part p reads k = KG*g + 4p + (0..3) with one
-// ds_read_b128 and feeds them to 4 consecutive MFMAs. A and B use the same mapping, so the
-// reduction still covers every k exactly once.
-template <int BM, int BN, int BK, int WM, int WN, int MF>
-__global__ void __launch_bounds__(WM* WN * 64)
-gemm_f32_mfma_kernel(const float* __restrict__ A, int lda, const float* __restrict__ Bt, int ldb,
-                     float* __restrict__ C, int ldc, int M, int N, int K, EpiParams epi, int tilesN) {
-  typedef Mfma<MF> MM;
-  typedef typename MM::acc_t acc_t;
-  constexpr int T = WM * WN * 64;
-  constexpr int LS = BK + 4;  // LDS row stride (floats): breaks the power-of-two bank aliasing
-  constexpr int WTM = BM / WM, WTN = BN / WN;
-  constexpr int TM = WTM / MF, TN = WTN / MF;
-  constexpr int KQ = BK / 4;
-  constexpr int A_V4 = BM * KQ, B_V4 = BN * KQ;
-  constexpr int A_LD = (A_V4 + T - 1) / T, B_LD = (B_V4 + T - 1) / T;
-  static_assert(BK % MM::KG == 0, "BK must be a multiple of the fragment group");
-  static_assert(WTM % MF == 0 && WTN % MF == 0, "wave tile must be a multiple of the MFMA tile");
-
-  __shared__ __attribute__((aligned(16))) float smem[2 * (BM + BN) * LS];
-
-  // XCD-aware bijective remap: the 8 XCDs each get a contiguous range of tiles, so the
-  // N tiles of one A row-panel run under one L2 (cdna_hip_programming.md T1).
-  const int nb = gridDim.x, bid = blockIdx.x;
-  const int xcd = bid & 7, q = nb >> 3, rr = nb & 7;
-  const int tile = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (bid >> 3);
-  const int tm_ = tile / tilesN, tn_ = tile - tm_ * tilesN;
-  const int m0 = tm_ * BM, n0 = tn_ * BN;
-
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid / WN, wn = wid - (wid / WN) * WN;
-
-  f32x4 ra[A_LD], rb[B_LD];
-  auto gload = [&](int k0) {
-#pragma unroll
-    for (int i = 0; i < A_LD; ++i) {
-      int idx = tid + i * T;
-      if (A_V4 % T == 0 || idx < A_V4) {
-        int row = idx / KQ, c4 = idx - (idx / KQ) * KQ;
-        int gm = m0 + row;
-        gm = gm < M ? gm : M - 1;
-        ra[i] = *reinterpret_cast<const f32x4*>(A + (size_t)gm * lda + k0 + c4 * 4);
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < B_LD; ++i) {
-      int idx = tid + i * T;
-      if (B_V4 % T == 0 || idx < B_V4) {
-        int row = idx / KQ, c4 = idx - (idx / KQ) * KQ;
-        rb[i] = *reinterpret_cast<const f32x4*>(Bt + (size_t)(n0 + row) * ldb + k0 + c4 * 4);
-      }
-    }
-  };
-  auto sstore = [&](float* As, float* Bs) {
-#pragma unroll
-    for (int i = 0; i < A_LD; ++i) {
-      int idx = tid + i * T;
-      if (A_V4 % T == 0 || idx < A_V4) {
-        int row = idx / KQ, c4 = idx - (idx / KQ) * KQ;
-        *reinterpret_cast<f32x4*>(As + row * LS + c4 * 4) = ra[i];
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < B_LD; ++i) {
-      int idx = tid + i * T;
-      if (B_V4 % T == 0 || idx < B_V4) {
-        int row = idx / KQ, c4 = idx - (idx / KQ) * KQ;
-        *reinterpret_cast<f32x4*>(Bs + row * LS + c4 * 4) = rb[i];
-      }
-    }
-  };
-
-  acc_t acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int r = 0; r < MM::REGS; ++r) acc[i][j][r] = 0.f;
-
-  const int fr = MM::frag_row(lane), fk = MM::frag_kofs(lane);
-  const int a_base = (wm * WTM + fr) * LS + fk;
-  const int b_base = (wn * WTN + fr) * LS + fk;
-
-  const int nk = K / BK;
-  gload(0);
-  sstore(smem, smem + BM * LS);
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    float* As = smem + (kt & 1) * (BM + BN) * LS;
-    float* Bs = As + BM * LS;
-    if (kt + 1 < nk) gload((kt + 1) * BK);
-#pragma unroll
-    for (int g = 0; g < BK / MM::KG; ++g) {
-      f32x4 af[TM], bf[TN];
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-        af[i] = *reinterpret_cast<const f32x4*>(As + a_base + i * MF * LS + g * MM::KG);
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-        bf[j] = *reinterpret_cast<const f32x4*>(Bs + b_base + j * MF * LS + g * MM::KG);
-#pragma unroll
-      for (int s = 0; s < 4; ++s)
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j) acc[i][j] = MM::op(af[i][s], bf[j][s], acc[i][j]);
-    }
-    if (kt + 1 < nk) {
-      float* Asn = smem + ((kt + 1) & 1) * (BM + BN) * LS;
-      sstore(Asn, Asn + BM * LS);
-    }
-    __syncthreads();
-  }
-
-  // fused epilogue + store (NHWC: row = output pixel, col = output channel)
-  const int oc = MM::out_col(lane);
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int n = n0 + wn * WTN + j * MF + oc;
-    const float pb = (epi.flags & EPI_BIAS) ? epi.bias[n] : 0.f;
-    const float pm = (epi.flags & (EPI_BN | EPI_BN_AB)) ? epi.mean[n] : 0.f;
-    const float ps = (epi.flags & (EPI_BN | EPI_BN_AB)) ? epi.sq[n] : 1.f;
-    const float pg = (epi.flags & EPI_BN) ? epi.gamma[n] : 1.f;
-    if (n < N) {
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-#pragma unroll
-        for (int r = 0; r < MM::REGS; ++r) {
-          const int m = m0 + wm * WTM + i * MF + MM::out_row(lane, r);
-          if (m < M) C[(size_t)m * ldc + n] = apply_epilogue(acc[i][j][r], pb, pm, ps, pg, epi.flags);
-        }
-      }
-    }
-  }
-}
-
 struct CfgInfo {
   int bm, bn, bk;
 };
@@ -313,13 +125,17 @@ int gemm_cfg_bm(int cfg) { return kCfgs[cfg].bm; }
 int gemm_cfg_bn(int cfg) { return kCfgs[cfg].bn; }
 int gemm_cfg_bk(int cfg) { return kCfgs[cfg].bk; }
 
+// Measured on MI355X at the batch-64 shapes (tools/gemm_bench.hip, profiles/r01_gemm_bench.txt):
+// the LDS-DMA 128x128 two-stage ring wins the long-K layers (conv6/7: 118 TF), the 64x128
+// three-stage ring everything else with N >= 128 (conv3-5: 103-104 TF).  Every N >= 128 config
+// uses 32x32x2 MFMAs with the same K permutation, so an output element's summation order does
+// not depend on M: results are bit-identical across batch sizes.
 int choose_gemm_cfg(long long M, int N, int K) {
-  (void)K;
   if (N <= 16) return GEMM_256x16_K32;
   if (N <= 32) return GEMM_256x32_K16;
   if (N <= 64) return GEMM_128x64_K32;
   long long t128 = ((M + 127) / 128) * ((N + 127) / 128);
-  if (t128 >= 512) return GEMM_128x128_K32;
+  if (K >= 4096 && t128 >= 512) return GEMM_128x128_K32;
   return GEMM_64x128_K32;
 }
 
@@ -352,12 +168,12 @@ int launch_gemm(int cfg, const float* A, int lda, const float* Bt, int ldb, floa
                          Bt, ldb, C, ldc, m, N, Kpad, epi, tilesN);
       break;
     case GEMM_128x128_K32:
-      hipLaunchKernelGGL((gemm_f32_mfma_kernel<128, 128, 32, 2, 2, 32>), grid, dim3(256), 0, stream, A, lda,
-                         Bt, ldb, C, ldc, m, N, Kpad, epi, tilesN);
+      hipLaunchKernelGGL((gemm_f32_glds_kernel<128, 128, 2, 2, 32, 2>), grid, dim3(256), 0, stream, A, lda, Bt,
+                         ldb, C, ldc, m, N, Kpad, epi, tilesN);
       break;
     case GEMM_64x128_K32:
-      hipLaunchKernelGGL((gemm_f32_mfma_kernel<64, 128, 32, 2, 2, 32>), grid, dim3(256), 0, stream, A, lda,
-                         Bt, ldb, C, ldc, m, N, Kpad, epi, tilesN);
+      hipLaunchKernelGGL((gemm_f32_glds_kernel<64, 128, 2, 2, 32, 3>), grid, dim3(256), 0, stream, A, lda, Bt,
+                         ldb, C, ldc, m, N, Kpad, epi, tilesN);
       break;
   }
   return check_launch("gemm");

@@ -1,0 +1,113 @@
+"""Summarise rocprofv3 CSV output of `bench.py` per PLAN kernel (conv0.im2col ... conv8.gemm).
+
+rocprofv3 --stats aggregates by kernel template, and one template serves several layers, so
+this maps every dispatch to its plan kernel by position inside each forward (a forward
+starts at the conv0 im2col dispatch and has a fixed kernel order).
+
+  python tools/prof_summary.py --trace DIR/trace_kernel_trace.csv \
+      [--fetch DIR/fetch_counter_collection.csv --write DIR/write_counter_collection.csv] \
+      [--out profiles/pmc_summary.json]
+
+HBM traffic per launch follows MI355X_MICROARCH.md §HBM: FETCH_SIZE (KiB) reads exactly
+half the bytes of a wide (16 B/lane) coalesced streaming read on gfx950, so it is doubled;
+WRITE_SIZE is exact for 16 B/lane stores.  bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024.
+"""
+import argparse
+import csv
+import json
+from collections import defaultdict
+
+ORDER = []
+for i in range(9):
+    if i < 8:
+        ORDER.append(f"conv{i}.im2col")
+    ORDER.append(f"conv{i}.gemm")
+    if i < 6:
+        ORDER.append(f"pool{i}")
+
+OURS = ("dnnhip::im2col", "dnnhip::gemm", "dnnhip::maxpool", "dnnhip::conv0_", "dnnhip::conv_")
+
+
+def _ours(name):
+    return any(t in name for t in OURS) and "pack_weights" not in name
+
+
+def dispatch_sequence(rows, key_start="Start_Timestamp", key_end="End_Timestamp"):
+    """[(plan_kernel, row)] for every dispatch inside a recognised forward."""
+    seq = [r for r in rows if _ours(r["Kernel_Name"])]
+    seq.sort(key=lambda r: int(r.get("Dispatch_Id") or 0))
+    out, i = [], 0
+    first = None
+    while i < len(seq):
+        name = seq[i]["Kernel_Name"]
+        if first is None:
+            first = name  # the first dispatch of the first forward defines the start marker
+        if name == first and i + len(ORDER) <= len(seq):
+            for j, pk in enumerate(ORDER):
+                out.append((pk, seq[i + j]))
+            i += len(ORDER)
+        else:
+            i += 1
+    return out
+
+
+def summarise(trace=None, fetch=None, write=None):
+    res = defaultdict(lambda: {"calls": 0})
+    if trace:
+        rows = list(csv.DictReader(open(trace)))
+        for pk, r in dispatch_sequence(rows):
+            d = res[pk]
+            d["calls"] += 1
+            d.setdefault("_ns", []).append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+            d["template"] = r["Kernel_Name"].split("(")[0]
+            d["grid"] = int(r.get("Grid_Size") or r.get("Grid_Size_X") or 0)
+            d["vgpr"] = int(r.get("VGPR_Count") or 0)
+            d["agpr"] = int(r.get("Accum_VGPR_Count") or 0)
+            d["lds"] = int(r.get("LDS_Block_Size") or 0)
+    for path, key in ((fetch, "FETCH_SIZE"), (write, "WRITE_SIZE")):
+        if not path:
+            continue
+        rows = [r for r in csv.DictReader(open(path)) if r["Counter_Name"] == key]
+        for pk, r in dispatch_sequence(rows):
+            res[pk].setdefault("_" + key, []).append(float(r["Counter_Value"]))
+    out = {}
+    for pk in ORDER:
+        if pk not in res:
+            continue
+        d = dict(res[pk])
+        if "_ns" in d:
+            ns = sorted(d.pop("_ns"))
+            d["avg_us"] = round(sum(ns) / len(ns) / 1e3, 2)
+            d["median_us"] = round(ns[len(ns) // 2] / 1e3, 2)
+        for key in ("FETCH_SIZE", "WRITE_SIZE"):
+            v = d.pop("_" + key, None)
+            if v:
+                d[key.lower() + "_kib"] = round(sum(v) / len(v), 1)
+        if "fetch_size_kib" in d and "write_size_kib" in d:
+            d["hbm_bytes_per_launch"] = round((2 * d["fetch_size_kib"] + d["write_size_kib"]) * 1024)
+        out[pk] = d
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--trace")
+    ap.add_argument("--fetch")
+    ap.add_argument("--write")
+    ap.add_argument("--out")
+    ap.add_argument("--note", default="")
+    a = ap.parse_args()
+    s = summarise(a.trace, a.fetch, a.write)
+    doc = {"note": a.note or __doc__.strip().splitlines()[0], "kernels": s}
+    text = json.dumps(doc, indent=1)
+    if a.out:
+        with open(a.out, "w") as f:
+            f.write(text + "\n")
+    for k, d in s.items():
+        print(f"{k:14s} calls={d.get('calls', 0):4d} avg_us={d.get('avg_us', 0):9.2f} "
+              f"fetch={d.get('fetch_size_kib', 0):12.1f}KiB write={d.get('write_size_kib', 0):12.1f}KiB "
+              f"{d.get('template', '')[:60]}")
+
+
+if __name__ == "__main__":
+    main()
