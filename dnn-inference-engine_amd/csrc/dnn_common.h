@@ -68,30 +68,66 @@ struct EpiParams {
   int flags;
 };
 
-// GEMM tile configurations (see kernels.hip). Each has its own BM/BN/BK.
+// GEMM tile configurations (see kernels.hip). Each has its own BM/BN/BK.  The MFMA shape
+// (and so the per-element summation order) depends on N only: 16x16x4 for N <= 32,
+// 32x32x2 above, with the same K permutation in every config of a family.
 enum GemmCfg : int {
-  GEMM_256x16_K32 = 0,   // N <= 16 (conv0), MFMA 16x16x4
-  GEMM_256x32_K16 = 1,   // N <= 32 (conv1), MFMA 16x16x4
-  GEMM_128x64_K32 = 2,   // N <= 64, MFMA 32x32x2
+  GEMM_256x16_K32 = 0,   // N <= 16 (conv0), register-staged, MFMA 16x16x4
+  GEMM_256x32_K16 = 1,   // N <= 32 (conv1), register-staged, MFMA 16x16x4
+  GEMM_128x64_K32 = 2,   // N <= 64, register-staged, MFMA 32x32x2
   GEMM_128x128_K32 = 3,  // long-K wide layers (conv6/7): LDS-DMA 2-stage ring, MFMA 32x32x2
   GEMM_64x128_K32 = 4,   // other N >= 128 layers: LDS-DMA 3-stage ring, MFMA 32x32x2
-  GEMM_NUM_CFGS = 5,
+  GEMM_G128x32_K32 = 5,  // N <= 32 implicit conv: LDS-DMA 3-stage ring, MFMA 16x16x4
+  GEMM_G128x64_K32 = 6,  // N <= 64 implicit conv: LDS-DMA 3-stage ring, MFMA 32x32x2
+  GEMM_NUM_CFGS = 7,
 };
 int gemm_cfg_bm(int cfg);
 int gemm_cfg_bn(int cfg);
 int gemm_cfg_bk(int cfg);
 int choose_gemm_cfg(long long M, int N, int K);
+int choose_gemm_cfg_implicit(long long M, int N, int K);
+
+// Implicit-GEMM conv: the A operand is read straight from the NHWC input by per-lane
+// LDS-DMA addresses (no im2col buffer).  Row m of the GEMM is an output pixel; with pool=1
+// rows are pool-window-major (m = 4*window + 2*dy + dx of a 2x2/stride-2 window) and the
+// epilogue max-pools the 4 rows, writing [B][PH][PW][N].  Needs C == 16 or C % 32 == 0.
+struct ImplicitConv {
+  const float* zero;  // >= 16 B of zeros in device memory (source of padding taps)
+  int H, W, C;        // input
+  int OH, OW;         // conv output
+  int PH, PW;         // pooled output (pool = 1)
+  int kh, kw, sh, sw, pt, pl;
+  int pool;
+};
+bool implicit_conv_supported(int C, int kh, int kw);
+enum GemmMode : int { GEMM_DENSE = 0, GEMM_IMPLICIT = 1, GEMM_IMPLICIT_POOL = 2 };
 
 // ---------------------------------------------------------------- launchers
 // All launchers are asynchronous on `stream` and return 0 / negative on launch error.
 int launch_im2col(const float* in, float* col, const ConvGeom& g, hipStream_t stream);
 int launch_gemm(int cfg, const float* A, int lda, const float* Bt, int ldb, float* C, int ldc,
                 long long M, int N, int Kpad, const EpiParams& epi, hipStream_t stream);
+// implicit conv (mode GEMM_IMPLICIT / GEMM_IMPLICIT_POOL) on the LDS-DMA configs 3..6;
+// `in` is the NHWC input, M = B*OH*OW (or B*PH*PW*4 with pool)
+int launch_gemm_implicit(int cfg, int mode, const float* in, const ImplicitConv& ic, const float* Bt, int ldb,
+                         float* C, int ldc, long long M, int N, int Kpad, const EpiParams& epi, hipStream_t stream);
 int launch_maxpool(const float* in, float* out, const PoolGeom& g, hipStream_t stream);
 // order 0: rows of w are (kh, kw, ic)  [HWIO flattened];  order 1: rows are (ic, kh, kw)
 // [proj3 kernel_r layout, dnn_openblas.py:166-167].  Output bt[Npad][Kpad] zero padded.
 int launch_pack_weights(const float* w, float* bt, int K, int N, int Kpad, int Npad, int order,
                         int kh, int kw, int C, hipStream_t stream);
+// Direct 3x3/stride-1 conv (cin <= 4, 16 outputs) + epilogue + fused 2x2/stride-2 max pool
+// (conv_direct.hip).  w is HWIO [9*cin][16].
+struct DirectGeom {
+  int B, H, W;    // input (unpadded) NHWC, channels = cin
+  int OH, OW;     // conv output
+  int PH, PW;     // pooled output
+  int pt, pl;     // conv front pads
+};
+bool direct_conv_pool_supported(int cin, int nout, int kh, int kw, int sh, int sw);
+int launch_conv3x3_pool2_direct(const float* in, const float* w, float* out, const DirectGeom& g, int cin,
+                                int nout, const EpiParams& epi, hipStream_t stream);
+
 // element-wise ops of the per-op ABI
 int launch_bias_add(const float* in, const float* b, float* out, long long n, int C, hipStream_t s);
 int launch_bn_mvg(const float* in, const float* mean, const float* sq, const float* gamma, float* out,

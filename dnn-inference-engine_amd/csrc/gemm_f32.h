@@ -16,6 +16,7 @@
 //                          SOURCE address so the fragment reads are conflict-free.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <cfloat>
 #include "dnn_common.h"
 
 namespace dnnhip {
@@ -249,20 +250,65 @@ __device__ __forceinline__ void lds_dma16(const float* src, float* dst) {
   __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
 }
 
-template <int BM, int BN, int WM, int WN, int MF, int NS>
+// Pool-fused store (implicit mode with pool): rows are pool-window-major, 4 rows per 2x2
+// window, and both MFMA layouts keep a window's 4 rows in 4 consecutive registers of one
+// lane (32x32x2: regs 4q..4q+3 = rows 8q+4h+0..3; 16x16x4: regs 0..3 = rows 4(l>>4)+0..3).
+// Each lane folds its 4 epilogue values with dnn_openblas.c's `m >= x ? m : x` in window
+// order (0,0),(0,1),(1,0),(1,1); rows past the conv output read -FLT_MAX (SAME pool pad).
+template <int MF, int TM, int TN, int WTM, int WTN>
+__device__ __forceinline__ void store_tile_pool(const typename Mfma<MF>::acc_t (&acc)[TM][TN],
+                                                float* __restrict__ C, int ldc, int M, int N, int m0, int n0,
+                                                int wm, int wn, int lane, const EpiParams& epi,
+                                                const ImplicitConv& ic) {
+  typedef Mfma<MF> MM;
+  const int oc = MM::out_col(lane);
+  const int nwin = M >> 2;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int n = n0 + wn * WTN + j * MF + oc;
+    const float pb = (epi.flags & EPI_BIAS) ? epi.bias[n] : 0.f;
+    const float pm = (epi.flags & (EPI_BN | EPI_BN_AB)) ? epi.mean[n] : 0.f;
+    const float ps = (epi.flags & (EPI_BN | EPI_BN_AB)) ? epi.sq[n] : 1.f;
+    const float pg = (epi.flags & EPI_BN) ? epi.gamma[n] : 1.f;
+    if (n >= N) continue;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+      for (int q = 0; q < MM::REGS / 4; ++q) {
+        const int win = (m0 + wm * WTM + i * MF + MM::out_row(lane, 4 * q)) >> 2;
+        if (win >= nwin) continue;
+        const int px = win % ic.PW, t = win / ic.PW, py = t % ic.PH;
+        float m = 0.f;
+#pragma unroll
+        for (int pos = 0; pos < 4; ++pos) {
+          const int oy = 2 * py + (pos >> 1), ox = 2 * px + (pos & 1);
+          const float v = (oy < ic.OH && ox < ic.OW)
+                              ? apply_epilogue(acc[i][j][4 * q + pos], pb, pm, ps, pg, epi.flags)
+                              : -FLT_MAX;
+          m = pos == 0 ? v : (m >= v ? m : v);
+        }
+        C[(size_t)win * ldc + n] = m;
+      }
+    }
+  }
+}
+
+// MODE 0: dense A (col buffer or 1x1 input), MODE 1: implicit conv, MODE 2: implicit + pool.
+template <int BM, int BN, int WM, int WN, int MF, int NS, int MODE>
 __global__ void __launch_bounds__(WM* WN * 64)
 gemm_f32_glds_kernel(const float* __restrict__ A, int lda, const float* __restrict__ Bt, int ldb,
-                     float* __restrict__ C, int ldc, int M, int N, int K, EpiParams epi, int tilesN) {
+                     float* __restrict__ C, int ldc, int M, int N, int K, EpiParams epi, int tilesN,
+                     ImplicitConv ic) {
   typedef Mfma<MF> MM;
   typedef typename MM::acc_t acc_t;
   constexpr int BK = 32;
   constexpr int NW = WM * WN;
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int TM = WTM / MF, TN = WTN / MF;
-  constexpr int A_CH = BM / 8, B_CH = BN / 8, CH = A_CH + B_CH;
-  constexpr int LPS = CH / NW;              // DMA instructions per wave per stage
-  constexpr int STAGE = (BM + BN) * BK;     // floats per stage
-  static_assert(CH % NW == 0, "chunks must split evenly over the waves");
+  constexpr int A_CH = BM / 8, B_CH = BN / 8;
+  constexpr int LPSA = A_CH / NW, LPSB = B_CH / NW, LPS = LPSA + LPSB;  // DMAs per wave per stage
+  constexpr int STAGE = (BM + BN) * BK;                                  // floats per stage
+  static_assert(A_CH % NW == 0 && B_CH % NW == 0, "chunks must split evenly over the waves");
   static_assert(NS >= 2 && NS <= 4, "ring depth");
   static_assert(WTM % MF == 0 && WTN % MF == 0, "wave tile must be a multiple of the MFMA tile");
 
@@ -275,29 +321,100 @@ gemm_f32_glds_kernel(const float* __restrict__ A, int lda, const float* __restri
   const int wid = wave_uniform(threadIdx.x >> 6);
   const int wm = wid / WN, wn = wid - (wid / WN) * WN;
 
-  // per-lane DMA sources (at k = 0) and wave-uniform chunk destinations
-  const float* src[LPS];
-  int dst[LPS];
+  // ---- A sources.  Chunk c (8 rows) of this wave: c = wid + i*NW; lane -> row 8c + lane/8,
+  // logical 16-B slot ls = (lane&7) ^ ((row>>1)&7) (the source side of the LDS swizzle).
+  const float* srcA[LPSA];  // dense: row pointer + slot (advanced by k0); implicit: pixel base
+  int maskA[LPSA], lsA[LPSA];
 #pragma unroll
-  for (int i = 0; i < LPS; ++i) {
-    const int c = wid + i * NW;
-    const bool isA = c < A_CH;
-    const int r = 8 * (isA ? c : c - A_CH) + (lane >> 3);
-    const int slot = (lane & 7) ^ ((r >> 1) & 7);
-    if (isA) {
-      int gm = m0 + r;
-      gm = gm < M ? gm : M - 1;
-      src[i] = A + (size_t)gm * lda + slot * 4;
+  for (int i = 0; i < LPSA; ++i) {
+    const int r = 8 * (wid + i * NW) + (lane >> 3);
+    const int ls = (lane & 7) ^ ((r >> 1) & 7);
+    lsA[i] = 4 * ls;
+    const int m = m0 + r;
+    if constexpr (MODE == 0) {
+      const int gm = m < M ? m : M - 1;
+      srcA[i] = A + (size_t)gm * lda + 4 * ls;
+      maskA[i] = 0;
     } else {
-      src[i] = Bt + (size_t)(n0 + r) * ldb + slot * 4;
+      int b = 0, oy = 0, ox = 0;
+      bool rv = m < M;
+      if constexpr (MODE == 2) {
+        const int pos = m & 3, w = m >> 2;
+        const int px = w % ic.PW, t = w / ic.PW, py = t % ic.PH;
+        b = t / ic.PH;
+        oy = 2 * py + (pos >> 1);
+        ox = 2 * px + (pos & 1);
+        rv = rv && oy < ic.OH && ox < ic.OW;
+      } else {
+        ox = m % ic.OW;
+        const int t = m / ic.OW;
+        oy = t % ic.OH;
+        b = t / ic.OH;
+      }
+      const int iy0 = oy * ic.sh - ic.pt, ix0 = ox * ic.sw - ic.pl;
+      srcA[i] = A + (((long long)b * ic.H + iy0) * ic.W + ix0) * (long long)ic.C;
+      int mk = 0;
+      if (rv) {
+        for (int dy = 0; dy < ic.kh; ++dy)
+          for (int dx = 0; dx < ic.kw; ++dx)
+            if ((unsigned)(iy0 + dy) < (unsigned)ic.H && (unsigned)(ix0 + dx) < (unsigned)ic.W)
+              mk |= 1 << (dy * ic.kw + dx);
+      }
+      maskA[i] = mk;
     }
-    dst[i] = c * 256;  // 1 KiB chunk, floats
   }
+  const float* srcB[LPSB];
+#pragma unroll
+  for (int j = 0; j < LPSB; ++j) {
+    const int r = 8 * (wid + j * NW) + (lane >> 3);
+    const int ls = (lane & 7) ^ ((r >> 1) & 7);
+    srcB[j] = Bt + (size_t)(n0 + r) * ldb + 4 * ls;
+  }
+
+  // implicit mode: wave-uniform position of the next K-step to issue, k = tap*C + c
+  int cb = 0, tapb = 0, dyb = 0, dxb = 0, dyn = 0, dxn = 1;
+  if constexpr (MODE != 0) {
+    if (ic.kw == 1) {
+      dyn = 1;
+      dxn = 0;
+    }
+  }
+  const long long rowstride = (long long)ic.W * ic.C;
+
   auto issue = [&](int stage, int k0) {
     float* base = smem + stage * STAGE;
 #pragma unroll
-    for (int i = 0; i < LPS; ++i)
-      lds_dma16(src[i] + k0, base + dst[i]);
+    for (int i = 0; i < LPSA; ++i) {
+      const float* s;
+      if constexpr (MODE == 0) {
+        s = srcA[i] + k0;
+      } else {
+        const int e = cb + lsA[i];
+        const bool nx = e >= ic.C;
+        const int c = nx ? e - ic.C : e;
+        const int dy = nx ? dyn : dyb, dx = nx ? dxn : dxb;
+        const int tap = tapb + (nx ? 1 : 0);
+        s = ((maskA[i] >> tap) & 1) ? srcA[i] + dy * rowstride + (long long)dx * ic.C + c : ic.zero;
+      }
+      lds_dma16(s, base + (wid + i * NW) * 256);
+    }
+#pragma unroll
+    for (int j = 0; j < LPSB; ++j) lds_dma16(srcB[j] + k0, base + (A_CH + wid + j * NW) * 256);
+    if constexpr (MODE != 0) {  // advance the uniform tap cursor by one K-step (32 k)
+      cb += BK;
+      while (cb >= ic.C) {
+        cb -= ic.C;
+        ++tapb;
+        dyb = dyn;
+        dxb = dxn;
+        if (dxn + 1 == ic.kw) {
+          dxn = 0;
+          ++dyn;
+        } else {
+          ++dxn;
+        }
+      }
+    }
   };
 
   acc_t acc[TM][TN];
@@ -358,7 +475,10 @@ gemm_f32_glds_kernel(const float* __restrict__ A, int lda, const float* __restri
     wait_lgkm0();
     stage = stage + 1 == NS ? 0 : stage + 1;
   }
-  store_tile<MF, TM, TN, WTM, WTN>(acc, C, ldc, M, N, m0, n0, wm, wn, lane, epi);
+  if constexpr (MODE == 2)
+    store_tile_pool<MF, TM, TN, WTM, WTN>(acc, C, ldc, M, N, m0, n0, wm, wn, lane, epi, ic);
+  else
+    store_tile<MF, TM, TN, WTM, WTN>(acc, C, ldc, M, N, m0, n0, wm, wn, lane, epi);
 }
 
 }  // namespace dnnhip

@@ -118,8 +118,8 @@ int launch_im2col(const float* in, float* col, const ConvGeom& g, hipStream_t st
 struct CfgInfo {
   int bm, bn, bk;
 };
-static const CfgInfo kCfgs[GEMM_NUM_CFGS] = {
-    {256, 16, 32}, {256, 32, 16}, {128, 64, 32}, {128, 128, 32}, {64, 128, 32}};
+static const CfgInfo kCfgs[GEMM_NUM_CFGS] = {{256, 16, 32}, {256, 32, 16}, {128, 64, 32}, {128, 128, 32},
+                                             {64, 128, 32},  {128, 32, 32}, {128, 64, 32}};
 
 int gemm_cfg_bm(int cfg) { return kCfgs[cfg].bm; }
 int gemm_cfg_bn(int cfg) { return kCfgs[cfg].bn; }
@@ -137,6 +137,48 @@ int choose_gemm_cfg(long long M, int N, int K) {
   long long t128 = ((M + 127) / 128) * ((N + 127) / 128);
   if (K >= 4096 && t128 >= 512) return GEMM_128x128_K32;
   return GEMM_64x128_K32;
+}
+
+// Implicit conv uses only LDS-DMA configs (the per-lane DMA source IS the im2col); same MFMA
+// family per N as the dense choice above, so implicit and explicit results are bit-identical.
+int choose_gemm_cfg_implicit(long long M, int N, int K) {
+  if (N <= 16) return -1;
+  if (N <= 32) return GEMM_G128x32_K32;
+  if (N <= 64) return GEMM_G128x64_K32;
+  return choose_gemm_cfg(M, N, K);
+}
+
+bool implicit_conv_supported(int C, int kh, int kw) {
+  return (C == 16 || C % 32 == 0) && kh * kw <= 30;
+}
+
+// LDS-DMA configs 3..6 for one A mode (dense / implicit / implicit + pool)
+template <int MODE>
+static int launch_glds(int cfg, const float* A, int lda, const float* Bt, int ldb, float* C, int ldc, int m, int N,
+                       int Kpad, const EpiParams& epi, int tilesN, const ImplicitConv& ic, dim3 grid,
+                       hipStream_t stream) {
+  switch (cfg) {
+    case GEMM_128x128_K32:
+      hipLaunchKernelGGL((gemm_f32_glds_kernel<128, 128, 2, 2, 32, 2, MODE>), grid, dim3(256), 0, stream, A, lda,
+                         Bt, ldb, C, ldc, m, N, Kpad, epi, tilesN, ic);
+      break;
+    case GEMM_64x128_K32:
+      hipLaunchKernelGGL((gemm_f32_glds_kernel<64, 128, 2, 2, 32, 3, MODE>), grid, dim3(256), 0, stream, A, lda,
+                         Bt, ldb, C, ldc, m, N, Kpad, epi, tilesN, ic);
+      break;
+    case GEMM_G128x32_K32:
+      hipLaunchKernelGGL((gemm_f32_glds_kernel<128, 32, 4, 1, 16, 3, MODE>), grid, dim3(256), 0, stream, A, lda,
+                         Bt, ldb, C, ldc, m, N, Kpad, epi, tilesN, ic);
+      break;
+    case GEMM_G128x64_K32:
+      hipLaunchKernelGGL((gemm_f32_glds_kernel<128, 64, 2, 2, 32, 3, MODE>), grid, dim3(256), 0, stream, A, lda,
+                         Bt, ldb, C, ldc, m, N, Kpad, epi, tilesN, ic);
+      break;
+    default:
+      set_error("gemm: cfg %d is not an LDS-DMA config", cfg);
+      return -2;
+  }
+  return check_launch("gemm_glds");
 }
 
 int launch_gemm(int cfg, const float* A, int lda, const float* Bt, int ldb, float* C, int ldc,
@@ -167,16 +209,32 @@ int launch_gemm(int cfg, const float* A, int lda, const float* Bt, int ldb, floa
       hipLaunchKernelGGL((gemm_f32_mfma_kernel<128, 64, 32, 2, 2, 32>), grid, dim3(256), 0, stream, A, lda,
                          Bt, ldb, C, ldc, m, N, Kpad, epi, tilesN);
       break;
-    case GEMM_128x128_K32:
-      hipLaunchKernelGGL((gemm_f32_glds_kernel<128, 128, 2, 2, 32, 2>), grid, dim3(256), 0, stream, A, lda, Bt,
-                         ldb, C, ldc, m, N, Kpad, epi, tilesN);
-      break;
-    case GEMM_64x128_K32:
-      hipLaunchKernelGGL((gemm_f32_glds_kernel<64, 128, 2, 2, 32, 3>), grid, dim3(256), 0, stream, A, lda, Bt,
-                         ldb, C, ldc, m, N, Kpad, epi, tilesN);
-      break;
+    default:
+      return launch_glds<GEMM_DENSE>(cfg, A, lda, Bt, ldb, C, ldc, m, N, Kpad, epi, tilesN, ImplicitConv{}, grid,
+                                     stream);
   }
   return check_launch("gemm");
+}
+
+int launch_gemm_implicit(int cfg, int mode, const float* in, const ImplicitConv& ic, const float* Bt, int ldb,
+                         float* C, int ldc, long long M, int N, int Kpad, const EpiParams& epi, hipStream_t stream) {
+  if (M == 0 || N == 0) return 0;
+  if (cfg < GEMM_128x128_K32 || cfg >= GEMM_NUM_CFGS || (mode != GEMM_IMPLICIT && mode != GEMM_IMPLICIT_POOL)) {
+    set_error("gemm_implicit: bad cfg %d / mode %d", cfg, mode);
+    return -2;
+  }
+  const CfgInfo ci = kCfgs[cfg];
+  if (Kpad % ci.bk != 0 || !implicit_conv_supported(ic.C, ic.kh, ic.kw) || M > 0x7fffffffLL || !ic.zero ||
+      (mode == GEMM_IMPLICIT_POOL && M % 4 != 0)) {
+    set_error("gemm_implicit: unsupported shape M=%lld C=%d Kpad=%d", M, ic.C, Kpad);
+    return -2;
+  }
+  const int tilesM = ceil_div_i(M, ci.bm), tilesN = ceil_div_i(N, ci.bn);
+  dim3 grid(tilesM * tilesN);
+  if (mode == GEMM_IMPLICIT)
+    return launch_glds<GEMM_IMPLICIT>(cfg, in, 0, Bt, ldb, C, ldc, (int)M, N, Kpad, epi, tilesN, ic, grid, stream);
+  return launch_glds<GEMM_IMPLICIT_POOL>(cfg, in, 0, Bt, ldb, C, ldc, (int)M, N, Kpad, epi, tilesN, ic, grid,
+                                         stream);
 }
 
 // ============================================================================ maxpool

@@ -3,18 +3,26 @@
 // The reference walks its graph node by node and round-trips every intermediate through
 // host numpy arrays (proj3/dnn_openblas.py:29-57; each CUDA/cuBLAS call even mallocs and
 // copies per image, dnn_cuda.cu:193-210).  Here the same node chain is lowered once to a
-// list of device steps:
-//   conv entry  = im2col (skipped for 1x1/stride-1/unpadded layers, where col == input)
-//                 + one fp32-MFMA GEMM whose epilogue applies BiasAdd, BatchNorm, LeakyReLU
-//   pool entry  = one maxpool kernel
-// Weights are packed once into a device arena as Bt[Npad][Kpad] (K order kh,kw,ic) plus
-// four Npad-long epilogue vectors (bias, mean, sqrt(var+eps), gamma).  Activations ping-pong
-// between two workspace buffers; the im2col buffer is shared by all layers.
+// list of device steps.  Each conv entry (Conv2D + its BiasAdd / BatchNorm / LeakyReLU as
+// the GEMM epilogue) runs in one of four modes:
+//   GEMM      explicit im2col into a col buffer + LDS-tiled fp32-MFMA GEMM (the reference's
+//             im2col + sgemm structure, dnn_openblas.c:160-194; generic fallback)
+//   DIRECT_A  1x1 / stride 1 / unpadded: the NHWC input IS the col matrix, GEMM only
+//   IMPLICIT  implicit GEMM: the LDS-DMA loader gathers the im2col rows straight from the
+//             input (per-lane source addresses), no col buffer
+//   DIRECT    3x3 conv with <= 4 input channels (conv0): direct FMA conv, weights in SGPRs
+// and a following 2x2/stride-2 MaxPool2D is fused into the IMPLICIT / DIRECT epilogue
+// (pool-window-major rows), otherwise it is its own pool entry.  Weights are packed once
+// into a device arena as Bt[Npad][Kpad] (K order kh,kw,ic; HWIO as-is for DIRECT) plus four
+// Npad-long epilogue vectors (bias, mean, sqrt(var+eps), gamma).  Activations ping-pong
+// between two workspace buffers.  DNN_HIP_FUSE=0 in the environment at plan creation
+// forces the explicit GEMM path with separate pools (for A/B checks).
 #include <hip/hip_runtime.h>
 #include <algorithm>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -56,30 +64,38 @@ static size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
 using namespace dnnhip;
 
+enum ConvMode : int { MODE_GEMM = 0, MODE_DIRECT_A = 1, MODE_IMPLICIT = 2, MODE_DIRECT = 3 };
+static const char* kModeName[] = {"gemm", "direct_a", "implicit", "direct"};
+
 struct PlanLayer {
   int type = 0;  // 0 conv, 1 pool
-  // shapes (per image)
+  // shapes (per image): input H,W,C -> conv/pool output OH,OW,OC (-> fused pool PH,PW)
   int H = 0, W = 0, C = 0, OH = 0, OW = 0, OC = 0;
   int kh = 0, kw = 0, sh = 1, sw = 1, pt = 0, pl = 0;
   // conv
+  int mode = MODE_GEMM;
   int K = 0, Kpad = 0, Npad = 0, cfg = 0, epi_flags = 0;
-  bool direct = false;  // A operand is the input itself (1x1, stride 1, no pad, C % BK == 0)
+  bool pool = false;  // a 2x2/stride-2 max pool fused into this conv
+  int PH = 0, PW = 0;
   size_t w_off = 0, epi_off = 0;  // float offsets in the weight arena
   bool have_host = false;
   std::vector<float> w, bias, mean, sq, gamma;
   int kernel_idx = 0;  // index of this layer's first kernel in the kernel list
+  int out_h() const { return pool ? PH : OH; }
+  int out_w() const { return pool ? PW : OW; }
 };
 
 struct KernelDesc {
   std::string name;
   int layer;
-  int kind;  // 0 im2col, 1 gemm, 2 pool
+  int kind;             // 0 im2col, 1 gemm / conv, 2 pool
   double flops, bytes;  // algorithmic, full planned batch
 };
 
 struct dnn_plan {
   int batch = 0, in_h = 0, in_w = 0, in_c = 0;
   int cur_h = 0, cur_w = 0, cur_c = 0;
+  bool fuse = true;
   std::vector<PlanLayer> layers;
   std::vector<KernelDesc> kernels;
   int device = -1;
@@ -91,6 +107,7 @@ struct dnn_plan {
   size_t ws_floats = 0;
   bool own_ws = false;
   size_t act_floats = 0, col_floats = 0;
+  static constexpr size_t kZeroFloats = 64;  // zero page: source of padding taps (implicit GEMM)
   // staging for dnn_plan_run_host
   float* h_in_dev = nullptr;
   size_t h_in_floats = 0;
@@ -102,15 +119,15 @@ struct dnn_plan {
 };
 
 static void layout(dnn_plan* p) {
-  // weight arena and workspace sizes
   size_t off = 0, act = (size_t)p->in_h * p->in_w * p->in_c, col = 0;
   int nconv = 0, npool = 0;  // kernel names use conv / pool ordinals: "conv7.gemm" is YOLO's conv7
   p->kernels.clear();
+  const double B = p->batch;
   for (size_t i = 0; i < p->layers.size(); ++i) {
     PlanLayer& L = p->layers[i];
-    act = std::max(act, (size_t)L.OH * L.OW * L.OC);
-    const double B = p->batch;
+    act = std::max(act, (size_t)L.out_h() * L.out_w() * L.OC);
     const double M = B * L.OH * L.OW;
+    const double in_b = 4.0 * B * L.H * L.W * L.C, out_b = 4.0 * B * L.out_h() * L.out_w() * L.OC;
     L.kernel_idx = (int)p->kernels.size();
     char nm[64];
     if (L.type == 0) {
@@ -118,24 +135,31 @@ static void layout(dnn_plan* p) {
       off = align_up(off + (size_t)L.Npad * L.Kpad, 64);
       L.epi_off = off;
       off = align_up(off + 4 * (size_t)L.Npad, 64);
-      if (!L.direct) {
+      const double flops = 2.0 * M * L.OC * L.K, w_b = 4.0 * L.K * L.OC;
+      if (L.mode == MODE_GEMM) {
         col = std::max(col, (size_t)L.OH * L.OW * L.Kpad);
         snprintf(nm, sizeof(nm), "conv%d.im2col", nconv);
         // algorithmic bytes: col written once + input read once
-        p->kernels.push_back({nm, (int)i, 0, 0.0, 4.0 * (M * L.K + B * L.H * L.W * L.C)});
+        p->kernels.push_back({nm, (int)i, 0, 0.0, 4.0 * M * L.K + in_b});
+        snprintf(nm, sizeof(nm), "conv%d.gemm", nconv++);
+        p->kernels.push_back({nm, (int)i, 1, flops, 4.0 * M * L.K + w_b + out_b});
+      } else if (L.mode == MODE_DIRECT) {
+        snprintf(nm, sizeof(nm), "conv%d.direct", nconv++);
+        p->kernels.push_back({nm, (int)i, 1, flops, in_b + w_b + out_b});
+      } else {  // DIRECT_A reads the input as A; IMPLICIT reads it once per tap in the ideal
+        snprintf(nm, sizeof(nm), "conv%d.gemm", nconv++);
+        p->kernels.push_back({nm, (int)i, 1, flops, in_b + w_b + out_b});
       }
-      snprintf(nm, sizeof(nm), "conv%d.gemm", nconv++);
-      p->kernels.push_back({nm, (int)i, 1, 2.0 * M * L.OC * L.K,
-                            4.0 * (M * L.K + (double)L.K * L.OC + M * L.OC)});
+      if (L.pool) npool++;
     } else {
       snprintf(nm, sizeof(nm), "pool%d", npool++);
-      p->kernels.push_back({nm, (int)i, 2, 0.0, 4.0 * (B * L.H * L.W * L.C + M * L.OC)});
+      p->kernels.push_back({nm, (int)i, 2, 0.0, in_b + out_b});
     }
   }
   p->weight_floats = align_up(off, 64);
   p->act_floats = align_up(act * (size_t)p->batch, 64);
   p->col_floats = align_up(col * (size_t)p->batch, 64);
-  p->ws_floats = 2 * p->act_floats + p->col_floats;
+  p->ws_floats = 2 * p->act_floats + p->col_floats + dnn_plan::kZeroFloats;
 }
 
 extern "C" {
@@ -151,6 +175,8 @@ int dnn_plan_create(int batch, int in_h, int in_w, int in_c, dnn_plan** out) {
   p->in_h = p->cur_h = in_h;
   p->in_w = p->cur_w = in_w;
   p->in_c = p->cur_c = in_c;
+  const char* f = getenv("DNN_HIP_FUSE");
+  p->fuse = !(f && f[0] == '0');
   *out = p;
   return 0;
 }
@@ -163,6 +189,13 @@ void dnn_plan_destroy(dnn_plan* p) {
   if (p->own_ws && p->ws) (void)hipFree(p->ws);
   if (p->h_in_dev) (void)hipFree(p->h_in_dev);
   delete p;
+}
+
+static void set_cfg(dnn_plan* p, PlanLayer& L) {
+  const long long M = (long long)p->batch * L.OH * L.OW;
+  L.cfg = L.mode == MODE_IMPLICIT ? choose_gemm_cfg_implicit(M, L.OC, L.K) : choose_gemm_cfg(M, L.OC, L.K);
+  L.Kpad = (int)align_up(L.K, gemm_cfg_bk(L.cfg));
+  L.Npad = (int)align_up(L.OC, gemm_cfg_bn(L.cfg));
 }
 
 int dnn_plan_add_conv(dnn_plan* p, int kh, int kw, int od, int stride_h, int stride_w, int padding,
@@ -188,21 +221,26 @@ int dnn_plan_add_conv(dnn_plan* p, int kh, int kw, int od, int stride_h, int str
               kw);
   L.OC = od;
   L.K = kh * kw * L.C;
-  L.cfg = choose_gemm_cfg((long long)p->batch * L.OH * L.OW, od, L.K);
-  const int bk = gemm_cfg_bk(L.cfg), bn = gemm_cfg_bn(L.cfg);
-  L.Kpad = (int)align_up(L.K, bk);
-  L.Npad = (int)align_up(od, bn);
-  L.direct = kh == 1 && kw == 1 && stride_h == 1 && stride_w == 1 && L.pt == 0 && L.pl == 0 &&
-             L.OH == L.H && L.OW == L.W && L.C % bk == 0;
+  const bool one_by_one = kh == 1 && kw == 1 && stride_h == 1 && stride_w == 1 && L.pt == 0 && L.pl == 0 &&
+                          L.OH == L.H && L.OW == L.W && L.C % 32 == 0;
+  if (one_by_one)
+    L.mode = MODE_DIRECT_A;
+  else if (p->fuse && implicit_conv_supported(L.C, kh, kw) &&
+           choose_gemm_cfg_implicit((long long)p->batch * L.OH * L.OW, od, L.K) >= 0)
+    L.mode = MODE_IMPLICIT;
+  else
+    L.mode = MODE_GEMM;  // may become MODE_DIRECT when a 2x2/s2 pool follows (conv0)
+  set_cfg(p, L);
   L.epi_flags = (biases ? EPI_BIAS : 0) | (mean ? EPI_BN : 0) |
                 (leaky == 1 ? EPI_LEAKY_F64 : leaky == 2 ? EPI_LEAKY_F32 : 0);
   if (kernel) {
     L.have_host = true;
     L.w.assign(kernel, kernel + (size_t)L.K * od);
-    L.bias.assign(L.Npad, 0.f);
-    L.mean.assign(L.Npad, 0.f);
-    L.sq.assign(L.Npad, 1.f);
-    L.gamma.assign(L.Npad, 1.f);
+    const int np = std::max(L.Npad, 32);
+    L.bias.assign(np, 0.f);
+    L.mean.assign(np, 0.f);
+    L.sq.assign(np, 1.f);
+    L.gamma.assign(np, 1.f);
     for (int d = 0; d < od; ++d) {
       if (biases) L.bias[d] = biases[d];
       if (mean) {
@@ -236,6 +274,29 @@ int dnn_plan_add_max_pool(dnn_plan* p, int kh, int kw, int stride_h, int stride_
   out_pads(L.H, kh, stride_h, padding, &L.OH, &L.pt);
   out_pads(L.W, kw, stride_w, padding, &L.OW, &L.pl);
   DNN_REQUIRE(L.OH > 0 && L.OW > 0, "dnn_plan_add_max_pool: empty output");
+  // fuse a 2x2/stride-2 pool (front pads are 0 for both SAME and VALID) into the conv before it
+  if (p->fuse && !p->layers.empty() && kh == 2 && kw == 2 && stride_h == 2 && stride_w == 2 && L.pt == 0 &&
+      L.pl == 0) {
+    PlanLayer& prev = p->layers.back();
+    if (prev.type == 0 && !prev.pool) {
+      bool ok = false;
+      if (prev.mode == MODE_IMPLICIT) {
+        ok = true;
+      } else if (prev.mode == MODE_GEMM && direct_conv_pool_supported(prev.C, prev.OC, prev.kh, prev.kw, prev.sh,
+                                                                      prev.sw)) {
+        prev.mode = MODE_DIRECT;
+        ok = true;
+      }
+      if (ok) {
+        prev.pool = true;
+        prev.PH = L.OH;
+        prev.PW = L.OW;
+        p->cur_h = L.OH;
+        p->cur_w = L.OW;
+        return 0;
+      }
+    }
+  }
   p->layers.push_back(std::move(L));
   p->cur_h = p->layers.back().OH;
   p->cur_w = p->layers.back().OW;
@@ -260,6 +321,41 @@ int dnn_plan_memory(const dnn_plan* pc, size_t* weight_bytes, size_t* workspace_
   return 0;
 }
 
+static int upload_weights(dnn_plan* p) {
+  size_t maxw = 0;
+  for (auto& L : p->layers)
+    if (L.type == 0) maxw = std::max(maxw, L.w.size());
+  float* tmp = nullptr;
+  DNN_HIP_TRY(hipMalloc(&tmp, std::max<size_t>(maxw, 1) * sizeof(float)));
+  int rc = 0;
+  for (auto& L : p->layers) {
+    if (L.type != 0) continue;
+    const size_t wb = L.w.size() * sizeof(float);
+    if (L.mode == MODE_DIRECT) {  // HWIO [K][N] as is: one 16-float row per (tap, cin)
+      if (hipMemcpy(p->weights + L.w_off, L.w.data(), wb, hipMemcpyHostToDevice) != hipSuccess) rc = -1;
+    } else {
+      if (hipMemcpy(tmp, L.w.data(), wb, hipMemcpyHostToDevice) != hipSuccess) rc = -1;
+      if (!rc) rc = launch_pack_weights(tmp, p->weights + L.w_off, L.K, L.OC, L.Kpad, L.Npad, 0, L.kh, L.kw, L.C, 0);
+    }
+    float* e = p->weights + L.epi_off;
+    const size_t nb = (size_t)L.Npad * sizeof(float);
+    if (!rc && (hipMemcpy(e, L.bias.data(), nb, hipMemcpyHostToDevice) != hipSuccess ||
+                hipMemcpy(e + L.Npad, L.mean.data(), nb, hipMemcpyHostToDevice) != hipSuccess ||
+                hipMemcpy(e + 2 * L.Npad, L.sq.data(), nb, hipMemcpyHostToDevice) != hipSuccess ||
+                hipMemcpy(e + 3 * L.Npad, L.gamma.data(), nb, hipMemcpyHostToDevice) != hipSuccess))
+      rc = -1;
+    if (!rc && hipDeviceSynchronize() != hipSuccess) rc = -1;
+    if (rc) {
+      if (last_error()[0] == 0) set_error("dnn_plan_finalize: weight upload failed");
+      break;
+    }
+  }
+  (void)hipFree(tmp);
+  if (rc) return rc;
+  for (auto& L : p->layers) std::vector<float>().swap(L.w);  // host copies no longer needed
+  return 0;
+}
+
 int dnn_plan_finalize(dnn_plan* p, int device, void* weights, void* workspace) {
   DNN_REQUIRE(p && !p->finalized, "dnn_plan_finalize: plan is NULL or already finalized");
   DNN_REQUIRE(!p->layers.empty(), "dnn_plan_finalize: plan has no layers");
@@ -274,52 +370,20 @@ int dnn_plan_finalize(dnn_plan* p, int device, void* weights, void* workspace) {
   }
   if (workspace) {
     p->ws = static_cast<float*>(workspace);
-  } else if (p->ws_floats) {
+  } else {
     DNN_HIP_TRY(hipMalloc(&p->ws, p->ws_floats * sizeof(float)));
     p->own_ws = true;
   }
+  // zero page at the end of the workspace (padding taps of the implicit GEMM read it)
+  DNN_HIP_TRY(hipMemset(p->ws + p->ws_floats - dnn_plan::kZeroFloats, 0, dnn_plan::kZeroFloats * sizeof(float)));
   bool all_host = true;
   for (auto& L : p->layers)
     if (L.type == 0 && !L.have_host) all_host = false;
   if (all_host) {
-    // upload raw HWIO weights through a temporary buffer, pack on the device
-    size_t maxw = 0;
-    for (auto& L : p->layers)
-      if (L.type == 0) maxw = std::max(maxw, L.w.size());
-    float* tmp = nullptr;
-    DNN_HIP_TRY(hipMalloc(&tmp, std::max<size_t>(maxw, 1) * sizeof(float)));
-    int rc = 0;
-    for (auto& L : p->layers) {
-      if (L.type != 0) continue;
-      if (hipMemcpy(tmp, L.w.data(), L.w.size() * sizeof(float), hipMemcpyHostToDevice) != hipSuccess) {
-        set_error("dnn_plan_finalize: weight upload failed");
-        rc = -1;
-        break;
-      }
-      rc = launch_pack_weights(tmp, p->weights + L.w_off, L.K, L.OC, L.Kpad, L.Npad, 0, L.kh, L.kw, L.C, 0);
-      if (rc) break;
-      float* e = p->weights + L.epi_off;
-      const size_t nb = (size_t)L.Npad * sizeof(float);
-      if (hipMemcpy(e, L.bias.data(), nb, hipMemcpyHostToDevice) != hipSuccess ||
-          hipMemcpy(e + L.Npad, L.mean.data(), nb, hipMemcpyHostToDevice) != hipSuccess ||
-          hipMemcpy(e + 2 * L.Npad, L.sq.data(), nb, hipMemcpyHostToDevice) != hipSuccess ||
-          hipMemcpy(e + 3 * L.Npad, L.gamma.data(), nb, hipMemcpyHostToDevice) != hipSuccess) {
-        set_error("dnn_plan_finalize: epilogue upload failed");
-        rc = -1;
-        break;
-      }
-      if (hipDeviceSynchronize() != hipSuccess) {
-        set_error("dnn_plan_finalize: pack failed");
-        rc = -1;
-        break;
-      }
-    }
-    (void)hipFree(tmp);
+    int rc = upload_weights(p);
     if (rc) return rc;
-    for (auto& L : p->layers) {  // host copies no longer needed
-      std::vector<float>().swap(L.w);
-    }
   }
+  DNN_HIP_TRY(hipDeviceSynchronize());
   p->finalized = true;
   return 0;
 }
@@ -348,6 +412,7 @@ int dnn_plan_run(dnn_plan* p, int n, const float* d_in, float* d_out, void* stre
   hipStream_t s = static_cast<hipStream_t>(stream);
   float* act[2] = {p->ws, p->ws + p->act_floats};
   float* col = p->ws + 2 * p->act_floats;
+  const float* zero = p->ws + p->ws_floats - dnn_plan::kZeroFloats;
   const float* cur = d_in;
   const int nl = (int)p->layers.size();
   for (int i = 0; i < nl; ++i) {
@@ -356,22 +421,37 @@ int dnn_plan_run(dnn_plan* p, int n, const float* d_in, float* d_out, void* stre
     int k = L.kernel_idx;
     int rc = 0;
     if (L.type == 0) {
-      const float* A = cur;
-      int lda = L.C;
-      if (!L.direct) {
-        ConvGeom g{n, L.H, L.W, L.C, L.OH, L.OW, L.kh, L.kw, L.sh, L.sw, L.pt, L.pl, L.K, L.Kpad};
-        if ((rc = record(p, k, s))) return rc;
-        if ((rc = launch_im2col(cur, col, g, s))) return rc;
-        A = col;
-        lda = L.Kpad;
-        ++k;
-      }
       const float* e = p->weights + L.epi_off;
-      EpiParams epi{e, e + L.Npad, e + 2 * L.Npad, e + 3 * L.Npad, L.epi_flags};
+      const EpiParams epi{e, e + L.Npad, e + 2 * L.Npad, e + 3 * L.Npad, L.epi_flags};
+      const float* wt = p->weights + L.w_off;
       if ((rc = record(p, k, s))) return rc;
-      if ((rc = launch_gemm(L.cfg, A, lda, p->weights + L.w_off, L.Kpad, dst, L.OC, (long long)n * L.OH * L.OW,
-                            L.OC, L.Kpad, epi, s)))
-        return rc;
+      switch (L.mode) {
+        case MODE_GEMM: {
+          ConvGeom g{n, L.H, L.W, L.C, L.OH, L.OW, L.kh, L.kw, L.sh, L.sw, L.pt, L.pl, L.K, L.Kpad};
+          if ((rc = launch_im2col(cur, col, g, s))) return rc;
+          if ((rc = record(p, k + 1, s))) return rc;
+          rc = launch_gemm(L.cfg, col, L.Kpad, wt, L.Kpad, dst, L.OC, (long long)n * L.OH * L.OW, L.OC, L.Kpad, epi,
+                           s);
+          break;
+        }
+        case MODE_DIRECT_A:
+          rc = launch_gemm(L.cfg, cur, L.C, wt, L.Kpad, dst, L.OC, (long long)n * L.OH * L.OW, L.OC, L.Kpad, epi, s);
+          break;
+        case MODE_IMPLICIT: {
+          ImplicitConv ic{zero, L.H, L.W, L.C, L.OH, L.OW, L.PH, L.PW, L.kh, L.kw, L.sh, L.sw, L.pt, L.pl,
+                          L.pool ? 1 : 0};
+          const long long M = L.pool ? 4LL * n * L.PH * L.PW : (long long)n * L.OH * L.OW;
+          rc = launch_gemm_implicit(L.cfg, L.pool ? GEMM_IMPLICIT_POOL : GEMM_IMPLICIT, cur, ic, wt, L.Kpad, dst,
+                                    L.OC, M, L.OC, L.Kpad, epi, s);
+          break;
+        }
+        case MODE_DIRECT: {
+          DirectGeom g{n, L.H, L.W, L.OH, L.OW, L.PH, L.PW, L.pt, L.pl};
+          rc = launch_conv3x3_pool2_direct(cur, wt, dst, g, L.C, L.OC, epi, s);
+          break;
+        }
+      }
+      if (rc) return rc;
     } else {
       PoolGeom g{n, L.H, L.W, L.C, L.OH, L.OW, L.kh, L.kw, L.sh, L.sw, L.pt, L.pl, 0};
       if ((rc = record(p, k, s))) return rc;
@@ -420,6 +500,25 @@ int dnn_plan_kernel_info(const dnn_plan* pc, int idx, char* name, int name_len, 
   if (name && name_len > 0) snprintf(name, name_len, "%s", k.name.c_str());
   if (flops) *flops = k.flops;
   if (bytes) *bytes = k.bytes;
+  return 0;
+}
+
+int dnn_plan_describe(const dnn_plan* p, char* buf, int buf_len) {
+  DNN_REQUIRE(p && buf && buf_len > 0, "dnn_plan_describe: bad args");
+  std::string s;
+  char line[256];
+  for (size_t i = 0; i < p->layers.size(); ++i) {
+    const PlanLayer& L = p->layers[i];
+    if (L.type == 0)
+      snprintf(line, sizeof(line), "conv %dx%dx%d -> %dx%dx%d k%dx%d s%d mode=%s cfg=%d K=%d Kpad=%d%s\n", L.H, L.W,
+               L.C, L.out_h(), L.out_w(), L.OC, L.kh, L.kw, L.sh, kModeName[L.mode], L.cfg, L.K, L.Kpad,
+               L.pool ? " +pool2x2s2" : "");
+    else
+      snprintf(line, sizeof(line), "pool %dx%dx%d -> %dx%dx%d k%dx%d s%d\n", L.H, L.W, L.C, L.OH, L.OW, L.OC, L.kh,
+               L.kw, L.sh);
+    s += line;
+  }
+  snprintf(buf, buf_len, "%s", s.c_str());
   return 0;
 }
 

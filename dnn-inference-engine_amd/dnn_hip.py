@@ -57,6 +57,7 @@ def _bind_plan_api(lib):
         "dnn_plan_add_conv": (i, [vp, i, i, i, i, i, i, vp, vp, vp, vp, vp, f, i]),
         "dnn_plan_add_max_pool": (i, [vp, i, i, i, i, i]),
         "dnn_plan_output_shape": (i, [vp, P(i), P(i), P(i), P(i)]),
+        "dnn_plan_describe": (i, [vp, ctypes.c_char_p, i]),
         "dnn_plan_memory": (i, [vp, P(sz), P(sz)]),
         "dnn_plan_finalize": (i, [vp, i, vp, vp]),
         "dnn_plan_weight_buffer": (i, [vp, P(vp), P(sz)]),
@@ -558,6 +559,11 @@ class Plan(object):
             return wb.value, sb.value
         finally:
             lib.dnn_plan_destroy(h)
+
+    def describe(self):
+        buf = ctypes.create_string_buffer(8192)
+        _check(self.lib.dnn_plan_describe(self.h, buf, 8192), "dnn_plan_describe", self.lib)
+        return buf.value.decode()
 
     def weight_buffer(self):
         p, n = ctypes.c_void_p(), ctypes.c_size_t()

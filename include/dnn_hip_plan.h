@@ -51,6 +51,14 @@ int dnn_plan_add_max_pool(dnn_plan* plan, int kh, int kw, int stride_h, int stri
 /* Output shape of the plan so far (per image, plus the planned batch). */
 int dnn_plan_output_shape(const dnn_plan* plan, int* batch, int* h, int* w, int* c);
 
+/* Human-readable lowering, one line per plan entry: shapes, execution mode (gemm =
+ * explicit im2col + GEMM, direct_a = 1x1 GEMM on the input, implicit = implicit GEMM,
+ * direct = direct conv), GEMM config and whether a 2x2/s2 max pool is fused.  A 2x2/s2
+ * MaxPool2D directly after an implicit or direct conv is folded into it; set DNN_HIP_FUSE=0
+ * in the environment before dnn_plan_create to keep every conv explicit and every pool
+ * separate. */
+int dnn_plan_describe(const dnn_plan* plan, char* buf, int buf_len);
+
 /* Device bytes the plan needs: packed weights + epilogue params, and workspace
  * (two activation buffers + the im2col buffer) for the planned batch. */
 int dnn_plan_memory(const dnn_plan* plan, size_t* weight_bytes, size_t* workspace_bytes);

@@ -105,16 +105,21 @@ def test_lowering_rejects_unfusable_graph():
     assert dnn_hip.lower_graph(g) is None
 
 
-def test_plan_shape_memory_and_flops_host_only():
+@pytest.mark.parametrize("fuse", ["1", "0"])
+def test_plan_shape_memory_and_flops_host_only(monkeypatch, fuse):
+    monkeypatch.setenv("DNN_HIP_FUSE", fuse)
     ws = synth.yolo_weights()
     g, _ = yolo_graph.build_graph(dnn_hip.DnnGraphBuilder, ws, in_shape=(64, 416, 416, 3))
     entries = dnn_hip.lower_graph(g)
     wb, sb = dnn_hip.Plan.memory(64, (416, 416, 3), entries)
     nparams = sum(w["kernel"].size for w in ws)
     assert wb >= 4 * nparams and wb < 4 * nparams * 1.2
-    # workspace: two activation buffers (conv0 output, 64x416x416x16) + the largest col
-    act = 64 * 416 * 416 * 16 * 4
-    assert sb >= 2 * act
+    if fuse == "0":
+        # two activation buffers (conv0 output, 64x416x416x16) + the largest col buffer
+        assert sb >= 2 * 64 * 416 * 416 * 16 * 4
+    else:
+        # pools fused into the convs, no col buffer: the largest activation is conv0's pooled output
+        assert 2 * 64 * 208 * 208 * 16 * 4 <= sb < 2 * 64 * 208 * 208 * 16 * 4 + 4096
     lib = dnn_hip.mylib
     h = ctypes.c_void_p()
     assert lib.dnn_plan_create(64, 416, 416, 3, ctypes.byref(h)) == 0
@@ -137,10 +142,19 @@ def test_plan_shape_memory_and_flops_host_only():
             names.append(nm.value.decode())
             flops += fl.value
         assert flops == pytest.approx(64 * 6.971e9, rel=1e-3)
-        # the 1x1 conv8 reads its input directly (no im2col), every 3x3 conv has one
+        # the 1x1 conv8 reads its input directly (no im2col)
         assert "conv8.im2col" not in names and "conv8.gemm" in names and "conv7.gemm" in names
-        assert sum(n.endswith(".im2col") for n in names) == 8
-        assert sum(n.startswith("pool") for n in names) == 6
+        if fuse == "0":  # explicit im2col for every 3x3 conv, every pool separate
+            assert len(names) == 23
+            assert sum(n.endswith(".im2col") for n in names) == 8
+            assert sum(n.startswith("pool") for n in names) == 6
+        else:  # conv0 direct + pool, conv1-7 implicit GEMM (conv1-4 with the pool), pool5 (s1)
+            assert names == ["conv0.direct", "conv1.gemm", "conv2.gemm", "conv3.gemm", "conv4.gemm", "conv5.gemm",
+                             "pool5", "conv6.gemm", "conv7.gemm", "conv8.gemm"]
+        buf = ctypes.create_string_buffer(8192)
+        assert lib.dnn_plan_describe(h, buf, 8192) == 0
+        desc = buf.value.decode()
+        assert desc.count("\n") == len(names) - (8 if fuse == "0" else 0)
     finally:
         lib.dnn_plan_destroy(h)
 

@@ -231,6 +231,64 @@ def test_fused_conv_bn_leaky_pool(case):
     assert R.normwise_err(y2, R.conv2d(x, k, strides=(1, s, s, 1), padding=pad)) < LAYER_TOL
 
 
+IMPLICIT_CASES = [
+    # B, H, W, C, od, pool   (C == 16 or C % 32 == 0 -> implicit GEMM; pool 2x2/s2 fused)
+    (2, 26, 22, 16, 32, True),     # conv1-like, MFMA 16x16x4 family
+    (3, 20, 18, 32, 64, True),     # conv2-like
+    (2, 13, 13, 32, 64, True),     # odd 13x13 -> 7x7: SAME pool padding inside the fused epilogue
+    (4, 16, 16, 64, 128, True),    # conv3-like
+    (2, 13, 11, 128, 256, False),  # conv5-like, no pool
+    (1, 9, 9, 16, 125, False),     # ragged N
+]
+
+
+@pytest.mark.parametrize("case", IMPLICIT_CASES)
+def test_implicit_gemm_and_fused_pool_vs_explicit_bit_exact(monkeypatch, case):
+    """The implicit GEMM gathers the same A operand the im2col writes and uses the same MFMA
+    family and K permutation, so fused and explicit paths must agree bit for bit; both are
+    checked against the oracle too."""
+    B, H, W, C, od, pool = case
+    rng = np.random.default_rng(C + od + H)
+    x = rng.standard_normal((B, H, W, C)).astype(np.float32)
+    k = (rng.standard_normal((3, 3, C, od)) * np.sqrt(2.0 / (9 * C))).astype(np.float32)
+    bias = rng.standard_normal(od).astype(np.float32) * 0.1
+    bn = (rng.standard_normal(od).astype(np.float32) * 0.1, rng.uniform(0.5, 1.5, od).astype(np.float32),
+          rng.uniform(0.5, 1.5, od).astype(np.float32))
+    kw = dict(bias=bias, bn=bn, leaky=True, pool=(2, 2, "SAME") if pool else None)
+    outs = {}
+    for fuse in ("1", "0"):
+        monkeypatch.setenv("DNN_HIP_FUSE", fuse)
+        eng = dnn_hip.DnnInferenceEngine(_chain(x.shape, k, **kw), False)
+        outs[fuse] = eng.run(x)
+        desc = eng.plan().describe()
+        assert ("implicit" in desc) == (fuse == "1")
+        assert ("+pool2x2s2" in desc) == (fuse == "1" and pool)
+    assert np.array_equal(outs["1"], outs["0"])
+    assert R.normwise_err(outs["1"], _oracle_chain(x, k, **kw)) < LAYER_TOL
+
+
+@pytest.mark.parametrize("hw", [(40, 38), (13, 13), (17, 22)])
+def test_direct_conv0_pool_vs_oracle(monkeypatch, hw):
+    """conv0's direct kernel (3 input channels, pool fused) vs the oracle and vs the explicit path."""
+    H, W = hw
+    rng = np.random.default_rng(H * W)
+    x = rng.uniform(0, 1, (3, H, W, 3)).astype(np.float32)
+    k = (rng.standard_normal((3, 3, 3, 16)) * 0.3).astype(np.float32)
+    bias = rng.standard_normal(16).astype(np.float32) * 0.1
+    bn = (rng.standard_normal(16).astype(np.float32) * 0.1, rng.uniform(0.5, 1.5, 16).astype(np.float32),
+          rng.uniform(0.5, 1.5, 16).astype(np.float32))
+    kw = dict(bias=bias, bn=bn, leaky=True, pool=(2, 2, "SAME"))
+    eng = dnn_hip.DnnInferenceEngine(_chain(x.shape, k, **kw), False)
+    y = eng.run(x)
+    assert "mode=direct " in eng.plan().describe()
+    ref = _oracle_chain(x, k, **kw)
+    assert y.shape == ref.shape
+    assert R.normwise_err(y, ref) < LAYER_TOL
+    monkeypatch.setenv("DNN_HIP_FUSE", "0")
+    y0 = dnn_hip.DnnInferenceEngine(_chain(x.shape, k, **kw), False).run(x)
+    assert R.normwise_err(y, y0) < LAYER_TOL
+
+
 def test_fused_epilogue_is_reference_order():
     """With an exactly representable conv (integer data, small K) the fused epilogue must equal
     bias_add -> batch_norm -> leaky_relu applied separately, bit for bit."""
@@ -314,6 +372,6 @@ def test_plan_timing_api(yolo_b1):
         plan.run_host(x)
     ms, cnt = plan.timing_end()
     ks = plan.kernels()
-    assert len(ms) == len(ks) == 23
+    assert len(ms) == len(ks) == 10
     assert all(c == 3 for c in cnt)
     assert all(m > 0 for m in ms)
