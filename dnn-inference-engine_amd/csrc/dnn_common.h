@@ -76,9 +76,9 @@ enum GemmCfg : int {
   GEMM_256x32_K16 = 1,   // N <= 32 (conv1), register-staged, MFMA 16x16x4
   GEMM_128x64_K32 = 2,   // N <= 64, register-staged, MFMA 32x32x2
   GEMM_128x128_K32 = 3,  // long-K wide layers (conv6/7): LDS-DMA 2-stage ring, MFMA 32x32x2
-  GEMM_64x128_K32 = 4,   // other N >= 128 layers: LDS-DMA 3-stage ring, MFMA 32x32x2
-  GEMM_G128x32_K32 = 5,  // N <= 32 implicit conv: LDS-DMA 3-stage ring, MFMA 16x16x4
-  GEMM_G128x64_K32 = 6,  // N <= 64 implicit conv: LDS-DMA 3-stage ring, MFMA 32x32x2
+  GEMM_64x128_K32 = 4,   // other N >= 128 layers: LDS-DMA 2-stage ring, MFMA 32x32x2
+  GEMM_G64x32_K32 = 5,   // N <= 32 implicit conv: LDS-DMA 2-stage ring, 64x32 tile, MFMA 16x16x4
+  GEMM_G256x64_K32 = 6,  // N <= 64 implicit conv: LDS-DMA 2-stage ring, 256x64 tile, 8 waves, MFMA 32x32x2
   GEMM_NUM_CFGS = 7,
 };
 int gemm_cfg_bm(int cfg);

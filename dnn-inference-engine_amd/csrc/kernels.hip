@@ -119,15 +119,16 @@ struct CfgInfo {
   int bm, bn, bk;
 };
 static const CfgInfo kCfgs[GEMM_NUM_CFGS] = {{256, 16, 32}, {256, 32, 16}, {128, 64, 32}, {128, 128, 32},
-                                             {64, 128, 32},  {128, 32, 32}, {128, 64, 32}};
+                                             {64, 128, 32},  {64, 32, 32},  {256, 64, 32}};
 
 int gemm_cfg_bm(int cfg) { return kCfgs[cfg].bm; }
 int gemm_cfg_bn(int cfg) { return kCfgs[cfg].bn; }
 int gemm_cfg_bk(int cfg) { return kCfgs[cfg].bk; }
 
-// Measured on MI355X at the batch-64 shapes (tools/gemm_bench.hip, profiles/r01_gemm_bench.txt):
-// the LDS-DMA 128x128 two-stage ring wins the long-K layers (conv6/7: 118 TF), the 64x128
-// three-stage ring everything else with N >= 128 (conv3-5: 103-104 TF).  Every N >= 128 config
+// Measured on MI355X at the batch-64 shapes (tools/gemm_bench.hip, tools/conv_bench.hip,
+// profiles/r01_*): the LDS-DMA 128x128 two-stage ring wins the long-K layers (conv6/7:
+// 110-118 TF), the 64x128 two-stage ring the other N >= 128 layers (conv3-5: 97 TF); two
+// stages beat three (more workgroups per CU fit the LDS).  Every N >= 128 config
 // uses 32x32x2 MFMAs with the same K permutation, so an output element's summation order does
 // not depend on M: results are bit-identical across batch sizes.
 int choose_gemm_cfg(long long M, int N, int K) {
@@ -143,8 +144,8 @@ int choose_gemm_cfg(long long M, int N, int K) {
 // family per N as the dense choice above, so implicit and explicit results are bit-identical.
 int choose_gemm_cfg_implicit(long long M, int N, int K) {
   if (N <= 16) return -1;
-  if (N <= 32) return GEMM_G128x32_K32;
-  if (N <= 64) return GEMM_G128x64_K32;
+  if (N <= 32) return GEMM_G64x32_K32;
+  if (N <= 64) return GEMM_G256x64_K32;
   return choose_gemm_cfg(M, N, K);
 }
 
@@ -163,15 +164,15 @@ static int launch_glds(int cfg, const float* A, int lda, const float* Bt, int ld
                          Bt, ldb, C, ldc, m, N, Kpad, epi, tilesN, ic);
       break;
     case GEMM_64x128_K32:
-      hipLaunchKernelGGL((gemm_f32_glds_kernel<64, 128, 2, 2, 32, 3, MODE>), grid, dim3(256), 0, stream, A, lda,
+      hipLaunchKernelGGL((gemm_f32_glds_kernel<64, 128, 2, 2, 32, 2, MODE>), grid, dim3(256), 0, stream, A, lda,
                          Bt, ldb, C, ldc, m, N, Kpad, epi, tilesN, ic);
       break;
-    case GEMM_G128x32_K32:
-      hipLaunchKernelGGL((gemm_f32_glds_kernel<128, 32, 4, 1, 16, 3, MODE>), grid, dim3(256), 0, stream, A, lda,
+    case GEMM_G64x32_K32:
+      hipLaunchKernelGGL((gemm_f32_glds_kernel<64, 32, 4, 1, 16, 2, MODE>), grid, dim3(256), 0, stream, A, lda,
                          Bt, ldb, C, ldc, m, N, Kpad, epi, tilesN, ic);
       break;
-    case GEMM_G128x64_K32:
-      hipLaunchKernelGGL((gemm_f32_glds_kernel<128, 64, 2, 2, 32, 3, MODE>), grid, dim3(256), 0, stream, A, lda,
+    case GEMM_G256x64_K32:
+      hipLaunchKernelGGL((gemm_f32_glds_kernel<256, 64, 4, 2, 32, 2, MODE>), grid, dim3(512), 0, stream, A, lda,
                          Bt, ldb, C, ldc, m, N, Kpad, epi, tilesN, ic);
       break;
     default:

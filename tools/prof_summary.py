@@ -17,15 +17,19 @@ import csv
 import json
 from collections import defaultdict
 
-ORDER = []
-for i in range(9):
-    if i < 8:
-        ORDER.append(f"conv{i}.im2col")
-    ORDER.append(f"conv{i}.gemm")
-    if i < 6:
-        ORDER.append(f"pool{i}")
+# kernel order of one YOLOv2-tiny forward in the default (fused) plan
+ORDER = ["conv0.direct", "conv1.gemm", "conv2.gemm", "conv3.gemm", "conv4.gemm", "conv5.gemm", "pool5",
+         "conv6.gemm", "conv7.gemm", "conv8.gemm"]
+# ... and with DNN_HIP_FUSE=0 (explicit im2col + GEMM, separate pools)
+ORDER_UNFUSED = []
+for _i in range(9):
+    if _i < 8:
+        ORDER_UNFUSED.append(f"conv{_i}.im2col")
+    ORDER_UNFUSED.append(f"conv{_i}.gemm")
+    if _i < 6:
+        ORDER_UNFUSED.append(f"pool{_i}")
 
-OURS = ("dnnhip::im2col", "dnnhip::gemm", "dnnhip::maxpool", "dnnhip::conv0_", "dnnhip::conv_")
+OURS = ("dnnhip::im2col", "dnnhip::gemm", "dnnhip::maxpool", "dnnhip::conv3x3_pool2_direct")
 
 
 def _ours(name):
@@ -96,7 +100,10 @@ def main():
     ap.add_argument("--write")
     ap.add_argument("--out")
     ap.add_argument("--note", default="")
+    ap.add_argument("--unfused", action="store_true", help="trace of a DNN_HIP_FUSE=0 run")
     a = ap.parse_args()
+    if a.unfused:
+        ORDER[:] = ORDER_UNFUSED
     s = summarise(a.trace, a.fetch, a.write)
     doc = {"note": a.note or __doc__.strip().splitlines()[0], "kernels": s}
     text = json.dumps(doc, indent=1)
