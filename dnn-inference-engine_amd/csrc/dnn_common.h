@@ -105,12 +105,20 @@ enum GemmMode : int { GEMM_DENSE = 0, GEMM_IMPLICIT = 1, GEMM_IMPLICIT_POOL = 2 
 // ---------------------------------------------------------------- launchers
 // All launchers are asynchronous on `stream` and return 0 / negative on launch error.
 int launch_im2col(const float* in, float* col, const ConvGeom& g, hipStream_t stream);
+// With splits > 1 (LDS-DMA configs only) the GEMM writes `splits` raw fp32 partials
+// [splits][M][N] to `slab` and NO epilogue; launch_splitk_reduce then sums them in split order
+// and applies the epilogue into C.  choose_splitk depends on (N, K) only.
+int choose_splitk(int N, int K);
 int launch_gemm(int cfg, const float* A, int lda, const float* Bt, int ldb, float* C, int ldc,
-                long long M, int N, int Kpad, const EpiParams& epi, hipStream_t stream);
+                long long M, int N, int Kpad, const EpiParams& epi, hipStream_t stream, int splits = 1,
+                float* slab = nullptr);
 // implicit conv (mode GEMM_IMPLICIT / GEMM_IMPLICIT_POOL) on the LDS-DMA configs 3..6;
-// `in` is the NHWC input, M = B*OH*OW (or B*PH*PW*4 with pool)
+// `in` is the NHWC input, M = B*OH*OW (or B*PH*PW*4 with pool; no split-K with pool)
 int launch_gemm_implicit(int cfg, int mode, const float* in, const ImplicitConv& ic, const float* Bt, int ldb,
-                         float* C, int ldc, long long M, int N, int Kpad, const EpiParams& epi, hipStream_t stream);
+                         float* C, int ldc, long long M, int N, int Kpad, const EpiParams& epi, hipStream_t stream,
+                         int splits = 1, float* slab = nullptr);
+int launch_splitk_reduce(const float* slab, int splits, long long M, int N, float* C, int ldc,
+                         const EpiParams& epi, hipStream_t stream);
 int launch_maxpool(const float* in, float* out, const PoolGeom& g, hipStream_t stream);
 // order 0: rows of w are (kh, kw, ic)  [HWIO flattened];  order 1: rows are (ic, kh, kw)
 // [proj3 kernel_r layout, dnn_openblas.py:166-167].  Output bt[Npad][Kpad] zero padded.

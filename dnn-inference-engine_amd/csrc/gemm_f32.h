@@ -293,12 +293,51 @@ __device__ __forceinline__ void store_tile_pool(const typename Mfma<MF>::acc_t (
   }
 }
 
+// Split-K: with sk.steps > 0 the grid is sk.splits x (tilesM x tilesN); workgroup split s
+// covers K-steps [s*steps, (s+1)*steps) and stores its raw fp32 partial tile (no epilogue) to
+// C + s*sk.slab; splitk_reduce_kernel then sums the partials in split order and applies the
+// epilogue.  The split is chosen from (N, K) only, so summation order stays independent of M.
+struct SplitK {
+  int steps;         // K-steps (of 32) per split; 0 = no split
+  int ntile;         // tilesM * tilesN
+  long long slab;    // floats between consecutive split partials
+};
+
+// Sum of the split-K partials in split order, ((p0 + p1) + p2) ..., then the fused epilogue.
+// part: [splits][M][N] (slab floats apart), C: [M][ldc].  HBM-bound: (splits + 1) * M * N * 4 B.
+static __global__ void __launch_bounds__(256) __attribute__((unused))
+splitk_reduce_kernel(const float* __restrict__ part, int splits, long long slab, float* __restrict__ C, int M,
+                     int N, int ldc, EpiParams epi) {
+  const int nq = N >> 2;  // N % 4 == 0 (checked by the launcher)
+  const long long total = (long long)M * nq;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int m = (int)(i / nq), n = (int)(i - (long long)m * nq) * 4;
+    const float* p = part + (size_t)m * N + n;
+    f32x4 v = *reinterpret_cast<const f32x4*>(p);
+    for (int s = 1; s < splits; ++s) {
+      const f32x4 w = *reinterpret_cast<const f32x4*>(p + s * slab);
+      v = v + w;
+    }
+    float* c = C + (size_t)m * ldc + n;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int ne = n + e;
+      const float pb = (epi.flags & EPI_BIAS) ? epi.bias[ne] : 0.f;
+      const float pm = (epi.flags & (EPI_BN | EPI_BN_AB)) ? epi.mean[ne] : 0.f;
+      const float ps = (epi.flags & (EPI_BN | EPI_BN_AB)) ? epi.sq[ne] : 1.f;
+      const float pg = (epi.flags & EPI_BN) ? epi.gamma[ne] : 1.f;
+      c[e] = apply_epilogue(v[e], pb, pm, ps, pg, epi.flags);
+    }
+  }
+}
+
 // MODE 0: dense A (col buffer or 1x1 input), MODE 1: implicit conv, MODE 2: implicit + pool.
 template <int BM, int BN, int WM, int WN, int MF, int NS, int MODE>
 __global__ void __launch_bounds__(WM* WN * 64)
 gemm_f32_glds_kernel(const float* __restrict__ A, int lda, const float* __restrict__ Bt, int ldb,
                      float* __restrict__ C, int ldc, int M, int N, int K, EpiParams epi, int tilesN,
-                     ImplicitConv ic) {
+                     ImplicitConv ic, SplitK sk) {
   typedef Mfma<MF> MM;
   typedef typename MM::acc_t acc_t;
   constexpr int BK = 32;
@@ -314,7 +353,16 @@ gemm_f32_glds_kernel(const float* __restrict__ A, int lda, const float* __restri
 
   __shared__ __attribute__((aligned(1024))) float smem[NS * STAGE];
 
-  const int tile = xcd_tile(blockIdx.x, gridDim.x);
+  int tile = xcd_tile(blockIdx.x, gridDim.x);
+  int kbeg = 0;  // first k of this workgroup's K range
+  if (sk.steps > 0) {
+    const int s = tile / sk.ntile;
+    tile -= s * sk.ntile;
+    kbeg = s * sk.steps * BK;
+    K = sk.steps * BK;
+    C += s * sk.slab;
+    epi.flags = 0;  // raw partial sums; the reduce kernel applies the epilogue
+  }
   const int tm_ = tile / tilesN, tn_ = tile - tm_ * tilesN;
   const int m0 = tm_ * BM, n0 = tn_ * BN;
   const int lane = threadIdx.x & 63;
@@ -333,7 +381,7 @@ gemm_f32_glds_kernel(const float* __restrict__ A, int lda, const float* __restri
     const int m = m0 + r;
     if constexpr (MODE == 0) {
       const int gm = m < M ? m : M - 1;
-      srcA[i] = A + (size_t)gm * lda + 4 * ls;
+      srcA[i] = A + (size_t)gm * lda + kbeg + 4 * ls;
       maskA[i] = 0;
     } else {
       int b = 0, oy = 0, ox = 0;
@@ -368,16 +416,18 @@ gemm_f32_glds_kernel(const float* __restrict__ A, int lda, const float* __restri
   for (int j = 0; j < LPSB; ++j) {
     const int r = 8 * (wid + j * NW) + (lane >> 3);
     const int ls = (lane & 7) ^ ((r >> 1) & 7);
-    srcB[j] = Bt + (size_t)(n0 + r) * ldb + 4 * ls;
+    srcB[j] = Bt + (size_t)(n0 + r) * ldb + kbeg + 4 * ls;
   }
 
   // implicit mode: wave-uniform position of the next K-step to issue, k = tap*C + c
   int cb = 0, tapb = 0, dyb = 0, dxb = 0, dyn = 0, dxn = 1;
   if constexpr (MODE != 0) {
-    if (ic.kw == 1) {
-      dyn = 1;
-      dxn = 0;
-    }
+    tapb = kbeg / ic.C;
+    cb = kbeg - tapb * ic.C;
+    dyb = tapb / ic.kw;
+    dxb = tapb - dyb * ic.kw;
+    dyn = dxb + 1 == ic.kw ? dyb + 1 : dyb;
+    dxn = dxb + 1 == ic.kw ? 0 : dxb + 1;
   }
   const long long rowstride = (long long)ic.W * ic.C;
 

@@ -153,27 +153,36 @@ bool implicit_conv_supported(int C, int kh, int kw) {
   return (C == 16 || C % 32 == 0) && kh * kw <= 30;
 }
 
+// Split-K for the long-K wide layers: 680 tiles of conv6/7 at batch 64 fill 512 two-per-CU
+// slots 1.33 times; three K splits make it 3.98 (measured conv7 116 -> 127 TF including the
+// reduce, tools/gemm_bench.hip, profiles/r01_gemm_bench_v2.txt).  Chosen from (N, K) only so
+// every batch size sums in the same order.
+int choose_splitk(int N, int K) {
+  if (N >= 512 && N % 4 == 0 && K >= 4096 && (K / 32) % 3 == 0) return 3;
+  return 1;
+}
+
 // LDS-DMA configs 3..6 for one A mode (dense / implicit / implicit + pool)
 template <int MODE>
 static int launch_glds(int cfg, const float* A, int lda, const float* Bt, int ldb, float* C, int ldc, int m, int N,
-                       int Kpad, const EpiParams& epi, int tilesN, const ImplicitConv& ic, dim3 grid,
-                       hipStream_t stream) {
+                       int Kpad, const EpiParams& epi, int tilesN, const ImplicitConv& ic, const SplitK& sk,
+                       dim3 grid, hipStream_t stream) {
   switch (cfg) {
     case GEMM_128x128_K32:
       hipLaunchKernelGGL((gemm_f32_glds_kernel<128, 128, 2, 2, 32, 2, MODE>), grid, dim3(256), 0, stream, A, lda,
-                         Bt, ldb, C, ldc, m, N, Kpad, epi, tilesN, ic);
+                         Bt, ldb, C, ldc, m, N, Kpad, epi, tilesN, ic, sk);
       break;
     case GEMM_64x128_K32:
       hipLaunchKernelGGL((gemm_f32_glds_kernel<64, 128, 2, 2, 32, 2, MODE>), grid, dim3(256), 0, stream, A, lda,
-                         Bt, ldb, C, ldc, m, N, Kpad, epi, tilesN, ic);
+                         Bt, ldb, C, ldc, m, N, Kpad, epi, tilesN, ic, sk);
       break;
     case GEMM_G64x32_K32:
       hipLaunchKernelGGL((gemm_f32_glds_kernel<64, 32, 4, 1, 16, 2, MODE>), grid, dim3(256), 0, stream, A, lda,
-                         Bt, ldb, C, ldc, m, N, Kpad, epi, tilesN, ic);
+                         Bt, ldb, C, ldc, m, N, Kpad, epi, tilesN, ic, sk);
       break;
     case GEMM_G256x64_K32:
       hipLaunchKernelGGL((gemm_f32_glds_kernel<256, 64, 4, 2, 32, 2, MODE>), grid, dim3(512), 0, stream, A, lda,
-                         Bt, ldb, C, ldc, m, N, Kpad, epi, tilesN, ic);
+                         Bt, ldb, C, ldc, m, N, Kpad, epi, tilesN, ic, sk);
       break;
     default:
       set_error("gemm: cfg %d is not an LDS-DMA config", cfg);
@@ -182,8 +191,27 @@ static int launch_glds(int cfg, const float* A, int lda, const float* Bt, int ld
   return check_launch("gemm_glds");
 }
 
+// grid and SplitK descriptor for `splits` (> 1: the kernel writes raw partials to `slab`)
+static int split_setup(int cfg, long long M, int N, int Kpad, int splits, float* slab, SplitK* sk, int* grid,
+                       int* tilesN) {
+  const CfgInfo ci = kCfgs[cfg];
+  const int tilesM = ceil_div_i(M, ci.bm);
+  *tilesN = ceil_div_i(N, ci.bn);
+  *grid = tilesM * *tilesN;
+  *sk = SplitK{0, 0, 0};
+  if (splits > 1) {
+    if (cfg < GEMM_128x128_K32 || !slab || (Kpad / 32) % splits != 0 || N % 4 != 0) {
+      set_error("gemm: split-K %d unsupported for cfg %d Kpad %d N %d", splits, cfg, Kpad, N);
+      return -2;
+    }
+    *sk = SplitK{Kpad / 32 / splits, *grid, M * (long long)N};
+    *grid *= splits;
+  }
+  return 0;
+}
+
 int launch_gemm(int cfg, const float* A, int lda, const float* Bt, int ldb, float* C, int ldc,
-                long long M, int N, int Kpad, const EpiParams& epi, hipStream_t stream) {
+                long long M, int N, int Kpad, const EpiParams& epi, hipStream_t stream, int splits, float* slab) {
   if (M == 0 || N == 0) return 0;
   if (cfg < 0 || cfg >= GEMM_NUM_CFGS) {
     set_error("gemm: bad cfg %d", cfg);
@@ -194,8 +222,10 @@ int launch_gemm(int cfg, const float* A, int lda, const float* Bt, int ldb, floa
     set_error("gemm: unsupported shape M=%lld Kpad=%d lda=%d ldb=%d for cfg %d", M, Kpad, lda, ldb, cfg);
     return -2;
   }
-  const int tilesM = ceil_div_i(M, ci.bm), tilesN = ceil_div_i(N, ci.bn);
-  dim3 grid(tilesM * tilesN);
+  SplitK sk;
+  int g = 0, tilesN = 0;
+  if (int rc = split_setup(cfg, M, N, Kpad, splits, slab, &sk, &g, &tilesN)) return rc;
+  dim3 grid(g);
   const int m = (int)M;
   switch (cfg) {
     case GEMM_256x16_K32:
@@ -211,14 +241,15 @@ int launch_gemm(int cfg, const float* A, int lda, const float* Bt, int ldb, floa
                          Bt, ldb, C, ldc, m, N, Kpad, epi, tilesN);
       break;
     default:
-      return launch_glds<GEMM_DENSE>(cfg, A, lda, Bt, ldb, C, ldc, m, N, Kpad, epi, tilesN, ImplicitConv{}, grid,
-                                     stream);
+      return launch_glds<GEMM_DENSE>(cfg, A, lda, Bt, ldb, sk.steps ? slab : C, sk.steps ? N : ldc, m, N, Kpad,
+                                     epi, tilesN, ImplicitConv{}, sk, grid, stream);
   }
   return check_launch("gemm");
 }
 
 int launch_gemm_implicit(int cfg, int mode, const float* in, const ImplicitConv& ic, const float* Bt, int ldb,
-                         float* C, int ldc, long long M, int N, int Kpad, const EpiParams& epi, hipStream_t stream) {
+                         float* C, int ldc, long long M, int N, int Kpad, const EpiParams& epi, hipStream_t stream,
+                         int splits, float* slab) {
   if (M == 0 || N == 0) return 0;
   if (cfg < GEMM_128x128_K32 || cfg >= GEMM_NUM_CFGS || (mode != GEMM_IMPLICIT && mode != GEMM_IMPLICIT_POOL)) {
     set_error("gemm_implicit: bad cfg %d / mode %d", cfg, mode);
@@ -226,16 +257,35 @@ int launch_gemm_implicit(int cfg, int mode, const float* in, const ImplicitConv&
   }
   const CfgInfo ci = kCfgs[cfg];
   if (Kpad % ci.bk != 0 || !implicit_conv_supported(ic.C, ic.kh, ic.kw) || M > 0x7fffffffLL || !ic.zero ||
-      (mode == GEMM_IMPLICIT_POOL && M % 4 != 0)) {
-    set_error("gemm_implicit: unsupported shape M=%lld C=%d Kpad=%d", M, ic.C, Kpad);
+      (mode == GEMM_IMPLICIT_POOL && (M % 4 != 0 || splits > 1))) {
+    set_error("gemm_implicit: unsupported shape M=%lld C=%d Kpad=%d splits=%d", M, ic.C, Kpad, splits);
     return -2;
   }
-  const int tilesM = ceil_div_i(M, ci.bm), tilesN = ceil_div_i(N, ci.bn);
-  dim3 grid(tilesM * tilesN);
+  SplitK sk;
+  int g = 0, tilesN = 0;
+  if (int rc = split_setup(cfg, M, N, Kpad, splits, slab, &sk, &g, &tilesN)) return rc;
+  float* out = sk.steps ? slab : C;
+  const int ldo = sk.steps ? N : ldc;
   if (mode == GEMM_IMPLICIT)
-    return launch_glds<GEMM_IMPLICIT>(cfg, in, 0, Bt, ldb, C, ldc, (int)M, N, Kpad, epi, tilesN, ic, grid, stream);
-  return launch_glds<GEMM_IMPLICIT_POOL>(cfg, in, 0, Bt, ldb, C, ldc, (int)M, N, Kpad, epi, tilesN, ic, grid,
-                                         stream);
+    return launch_glds<GEMM_IMPLICIT>(cfg, in, 0, Bt, ldb, out, ldo, (int)M, N, Kpad, epi, tilesN, ic, sk, dim3(g),
+                                      stream);
+  return launch_glds<GEMM_IMPLICIT_POOL>(cfg, in, 0, Bt, ldb, out, ldo, (int)M, N, Kpad, epi, tilesN, ic, sk,
+                                         dim3(g), stream);
+}
+
+int launch_splitk_reduce(const float* slab, int splits, long long M, int N, float* C, int ldc,
+                         const EpiParams& epi, hipStream_t stream) {
+  if (M == 0 || N == 0) return 0;
+  if (N % 4 != 0 || splits < 1) {
+    set_error("splitk_reduce: N %d must be a multiple of 4", N);
+    return -2;
+  }
+  long long total = M * (N / 4);
+  long long blocks = (total + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, slab, splits,
+                     M * (long long)N, C, (int)M, N, ldc, epi);
+  return check_launch("splitk_reduce");
 }
 
 // ============================================================================ maxpool

@@ -97,7 +97,16 @@ int legacy_conv(const float* in, const float* w, int order, float* out, int B, i
   ConvGeom g{B, ih, iw, ic, oh, ow, kh, kw, sh, sw, 0, 0, K, Kpad};
   if (int rc = launch_im2col(d_in, d_col, g, 0)) return rc;
   EpiParams epi{nullptr, nullptr, nullptr, nullptr, 0};
-  if (int rc = launch_gemm(cfg, d_col, Kpad, d_bt, Kpad, d_out, od, M, od, Kpad, epi, 0)) return rc;
+  // same split-K rule as the plan, so per-op and fused results agree bit for bit
+  const int splits = (cfg >= GEMM_128x128_K32 && Kpad == K) ? choose_splitk(od, K) : 1;
+  float* d_slab = nullptr;
+  if (splits > 1) {
+    d_slab = slot(5, (size_t)splits * M * od);
+    if (!d_slab) return -1;
+  }
+  if (int rc = launch_gemm(cfg, d_col, Kpad, d_bt, Kpad, d_out, od, M, od, Kpad, epi, 0, splits, d_slab)) return rc;
+  if (splits > 1)
+    if (int rc = launch_splitk_reduce(d_slab, splits, M, od, d_out, od, epi, 0)) return rc;
   return d2h(out, d_out, n_out);
 }
 

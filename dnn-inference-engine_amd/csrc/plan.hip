@@ -75,6 +75,7 @@ struct PlanLayer {
   // conv
   int mode = MODE_GEMM;
   int K = 0, Kpad = 0, Npad = 0, cfg = 0, epi_flags = 0;
+  int splits = 1;  // split-K partial count (> 1: GEMM writes partials, a reduce kernel finishes)
   bool pool = false;  // a 2x2/stride-2 max pool fused into this conv
   int PH = 0, PW = 0;
   size_t w_off = 0, epi_off = 0;  // float offsets in the weight arena
@@ -106,7 +107,7 @@ struct dnn_plan {
   float* ws = nullptr;
   size_t ws_floats = 0;
   bool own_ws = false;
-  size_t act_floats = 0, col_floats = 0;
+  size_t act_floats = 0, col_floats = 0, slab_floats = 0;
   static constexpr size_t kZeroFloats = 64;  // zero page: source of padding taps (implicit GEMM)
   // staging for dnn_plan_run_host
   float* h_in_dev = nullptr;
@@ -119,7 +120,7 @@ struct dnn_plan {
 };
 
 static void layout(dnn_plan* p) {
-  size_t off = 0, act = (size_t)p->in_h * p->in_w * p->in_c, col = 0;
+  size_t off = 0, act = (size_t)p->in_h * p->in_w * p->in_c, col = 0, slab = 0;
   int nconv = 0, npool = 0;  // kernel names use conv / pool ordinals: "conv7.gemm" is YOLO's conv7
   p->kernels.clear();
   const double B = p->batch;
@@ -147,8 +148,14 @@ static void layout(dnn_plan* p) {
         snprintf(nm, sizeof(nm), "conv%d.direct", nconv++);
         p->kernels.push_back({nm, (int)i, 1, flops, in_b + w_b + out_b});
       } else {  // DIRECT_A reads the input as A; IMPLICIT reads it once per tap in the ideal
-        snprintf(nm, sizeof(nm), "conv%d.gemm", nconv++);
+        snprintf(nm, sizeof(nm), "conv%d.gemm", nconv);
         p->kernels.push_back({nm, (int)i, 1, flops, in_b + w_b + out_b});
+        ++nconv;
+      }
+      if (L.splits > 1) {  // partials written by the GEMM, summed + epilogue by the reduce kernel
+        slab = std::max(slab, (size_t)L.splits * L.OH * L.OW * L.OC);
+        snprintf(nm, sizeof(nm), "conv%d.reduce", nconv - 1);
+        p->kernels.push_back({nm, (int)i, 3, (L.splits - 1) * M * L.OC, 4.0 * (L.splits + 1) * M * L.OC});
       }
       if (L.pool) npool++;
     } else {
@@ -159,7 +166,8 @@ static void layout(dnn_plan* p) {
   p->weight_floats = align_up(off, 64);
   p->act_floats = align_up(act * (size_t)p->batch, 64);
   p->col_floats = align_up(col * (size_t)p->batch, 64);
-  p->ws_floats = 2 * p->act_floats + p->col_floats + dnn_plan::kZeroFloats;
+  p->slab_floats = align_up(slab * (size_t)p->batch, 64);
+  p->ws_floats = 2 * p->act_floats + p->col_floats + p->slab_floats + dnn_plan::kZeroFloats;
 }
 
 extern "C" {
@@ -196,6 +204,7 @@ static void set_cfg(dnn_plan* p, PlanLayer& L) {
   L.cfg = L.mode == MODE_IMPLICIT ? choose_gemm_cfg_implicit(M, L.OC, L.K) : choose_gemm_cfg(M, L.OC, L.K);
   L.Kpad = (int)align_up(L.K, gemm_cfg_bk(L.cfg));
   L.Npad = (int)align_up(L.OC, gemm_cfg_bn(L.cfg));
+  L.splits = (L.cfg >= GEMM_128x128_K32 && L.Kpad == L.K) ? choose_splitk(L.OC, L.K) : 1;
 }
 
 int dnn_plan_add_conv(dnn_plan* p, int kh, int kw, int od, int stride_h, int stride_w, int padding,
@@ -278,7 +287,7 @@ int dnn_plan_add_max_pool(dnn_plan* p, int kh, int kw, int stride_h, int stride_
   if (p->fuse && !p->layers.empty() && kh == 2 && kw == 2 && stride_h == 2 && stride_w == 2 && L.pt == 0 &&
       L.pl == 0) {
     PlanLayer& prev = p->layers.back();
-    if (prev.type == 0 && !prev.pool) {
+    if (prev.type == 0 && !prev.pool && prev.splits == 1) {
       bool ok = false;
       if (prev.mode == MODE_IMPLICIT) {
         ok = true;
@@ -412,6 +421,7 @@ int dnn_plan_run(dnn_plan* p, int n, const float* d_in, float* d_out, void* stre
   hipStream_t s = static_cast<hipStream_t>(stream);
   float* act[2] = {p->ws, p->ws + p->act_floats};
   float* col = p->ws + 2 * p->act_floats;
+  float* slab = col + p->col_floats;
   const float* zero = p->ws + p->ws_floats - dnn_plan::kZeroFloats;
   const float* cur = d_in;
   const int nl = (int)p->layers.size();
@@ -425,24 +435,24 @@ int dnn_plan_run(dnn_plan* p, int n, const float* d_in, float* d_out, void* stre
       const EpiParams epi{e, e + L.Npad, e + 2 * L.Npad, e + 3 * L.Npad, L.epi_flags};
       const float* wt = p->weights + L.w_off;
       if ((rc = record(p, k, s))) return rc;
+      const long long Mc = (long long)n * L.OH * L.OW;
       switch (L.mode) {
         case MODE_GEMM: {
           ConvGeom g{n, L.H, L.W, L.C, L.OH, L.OW, L.kh, L.kw, L.sh, L.sw, L.pt, L.pl, L.K, L.Kpad};
           if ((rc = launch_im2col(cur, col, g, s))) return rc;
-          if ((rc = record(p, k + 1, s))) return rc;
-          rc = launch_gemm(L.cfg, col, L.Kpad, wt, L.Kpad, dst, L.OC, (long long)n * L.OH * L.OW, L.OC, L.Kpad, epi,
-                           s);
+          if ((rc = record(p, ++k, s))) return rc;
+          rc = launch_gemm(L.cfg, col, L.Kpad, wt, L.Kpad, dst, L.OC, Mc, L.OC, L.Kpad, epi, s, L.splits, slab);
           break;
         }
         case MODE_DIRECT_A:
-          rc = launch_gemm(L.cfg, cur, L.C, wt, L.Kpad, dst, L.OC, (long long)n * L.OH * L.OW, L.OC, L.Kpad, epi, s);
+          rc = launch_gemm(L.cfg, cur, L.C, wt, L.Kpad, dst, L.OC, Mc, L.OC, L.Kpad, epi, s, L.splits, slab);
           break;
         case MODE_IMPLICIT: {
           ImplicitConv ic{zero, L.H, L.W, L.C, L.OH, L.OW, L.PH, L.PW, L.kh, L.kw, L.sh, L.sw, L.pt, L.pl,
                           L.pool ? 1 : 0};
-          const long long M = L.pool ? 4LL * n * L.PH * L.PW : (long long)n * L.OH * L.OW;
+          const long long M = L.pool ? 4LL * n * L.PH * L.PW : Mc;
           rc = launch_gemm_implicit(L.cfg, L.pool ? GEMM_IMPLICIT_POOL : GEMM_IMPLICIT, cur, ic, wt, L.Kpad, dst,
-                                    L.OC, M, L.OC, L.Kpad, epi, s);
+                                    L.OC, M, L.OC, L.Kpad, epi, s, L.splits, slab);
           break;
         }
         case MODE_DIRECT: {
@@ -452,6 +462,10 @@ int dnn_plan_run(dnn_plan* p, int n, const float* d_in, float* d_out, void* stre
         }
       }
       if (rc) return rc;
+      if (L.splits > 1) {
+        if ((rc = record(p, ++k, s))) return rc;
+        if ((rc = launch_splitk_reduce(slab, L.splits, Mc, L.OC, dst, L.OC, epi, s))) return rc;
+      }
     } else {
       PoolGeom g{n, L.H, L.W, L.C, L.OH, L.OW, L.kh, L.kw, L.sh, L.sw, L.pt, L.pl, 0};
       if ((rc = record(p, k, s))) return rc;
@@ -510,9 +524,9 @@ int dnn_plan_describe(const dnn_plan* p, char* buf, int buf_len) {
   for (size_t i = 0; i < p->layers.size(); ++i) {
     const PlanLayer& L = p->layers[i];
     if (L.type == 0)
-      snprintf(line, sizeof(line), "conv %dx%dx%d -> %dx%dx%d k%dx%d s%d mode=%s cfg=%d K=%d Kpad=%d%s\n", L.H, L.W,
-               L.C, L.out_h(), L.out_w(), L.OC, L.kh, L.kw, L.sh, kModeName[L.mode], L.cfg, L.K, L.Kpad,
-               L.pool ? " +pool2x2s2" : "");
+      snprintf(line, sizeof(line), "conv %dx%dx%d -> %dx%dx%d k%dx%d s%d mode=%s cfg=%d K=%d Kpad=%d%s%s\n", L.H,
+               L.W, L.C, L.out_h(), L.out_w(), L.OC, L.kh, L.kw, L.sh, kModeName[L.mode], L.cfg, L.K, L.Kpad,
+               L.pool ? " +pool2x2s2" : "", L.splits > 1 ? (L.splits == 3 ? " splitK=3" : " splitK") : "");
     else
       snprintf(line, sizeof(line), "pool %dx%dx%d -> %dx%dx%d k%dx%d s%d\n", L.H, L.W, L.C, L.OH, L.OW, L.OC, L.kh,
                L.kw, L.sh);

@@ -114,12 +114,14 @@ def test_plan_shape_memory_and_flops_host_only(monkeypatch, fuse):
     wb, sb = dnn_hip.Plan.memory(64, (416, 416, 3), entries)
     nparams = sum(w["kernel"].size for w in ws)
     assert wb >= 4 * nparams and wb < 4 * nparams * 1.2
+    slab = 3 * 64 * 13 * 13 * 1024 * 4  # split-K partials of conv6/conv7 (3 splits)
     if fuse == "0":
         # two activation buffers (conv0 output, 64x416x416x16) + the largest col buffer
-        assert sb >= 2 * 64 * 416 * 416 * 16 * 4
+        assert sb >= 2 * 64 * 416 * 416 * 16 * 4 + slab
     else:
         # pools fused into the convs, no col buffer: the largest activation is conv0's pooled output
-        assert 2 * 64 * 208 * 208 * 16 * 4 <= sb < 2 * 64 * 208 * 208 * 16 * 4 + 4096
+        act2 = 2 * 64 * 208 * 208 * 16 * 4
+        assert act2 + slab <= sb < act2 + slab + 4096
     lib = dnn_hip.mylib
     h = ctypes.c_void_p()
     assert lib.dnn_plan_create(64, 416, 416, 3, ctypes.byref(h)) == 0
@@ -144,17 +146,20 @@ def test_plan_shape_memory_and_flops_host_only(monkeypatch, fuse):
         assert flops == pytest.approx(64 * 6.971e9, rel=1e-3)
         # the 1x1 conv8 reads its input directly (no im2col)
         assert "conv8.im2col" not in names and "conv8.gemm" in names and "conv7.gemm" in names
+        # conv6 / conv7 (N >= 512, K >= 4096) run split-K = 3 + an ordered reduce kernel
+        assert "conv6.reduce" in names and "conv7.reduce" in names
         if fuse == "0":  # explicit im2col for every 3x3 conv, every pool separate
-            assert len(names) == 23
+            assert len(names) == 25
             assert sum(n.endswith(".im2col") for n in names) == 8
             assert sum(n.startswith("pool") for n in names) == 6
         else:  # conv0 direct + pool, conv1-7 implicit GEMM (conv1-4 with the pool), pool5 (s1)
             assert names == ["conv0.direct", "conv1.gemm", "conv2.gemm", "conv3.gemm", "conv4.gemm", "conv5.gemm",
-                             "pool5", "conv6.gemm", "conv7.gemm", "conv8.gemm"]
+                             "pool5", "conv6.gemm", "conv6.reduce", "conv7.gemm", "conv7.reduce", "conv8.gemm"]
         buf = ctypes.create_string_buffer(8192)
         assert lib.dnn_plan_describe(h, buf, 8192) == 0
         desc = buf.value.decode()
-        assert desc.count("\n") == len(names) - (8 if fuse == "0" else 0)
+        assert desc.count("\n") == len(names) - 2 - (8 if fuse == "0" else 0)
+        assert desc.count("splitK=3") == 2
     finally:
         lib.dnn_plan_destroy(h)
 

@@ -55,14 +55,25 @@ Variant reg_variant(const char* nm) {
           }};
 }
 
-template <int BM, int BN, int WM, int WN, int MF, int NS>
+static float* g_slab = nullptr;  // split-K partials (allocated in main)
+
+template <int BM, int BN, int WM, int WN, int MF, int NS, int SPLIT = 1>
 Variant glds_variant(const char* nm) {
   return {nm, BM, BN,
           [](const float* A, int lda, const float* B, int ldb, float* C, int ldc, int M, int N, int K, EpiParams e,
              int grid, hipStream_t s) {
             int tilesN = (N + BN - 1) / BN;
-            hipLaunchKernelGGL((gemm_f32_glds_kernel<BM, BN, WM, WN, MF, NS>), dim3(grid), dim3(WM * WN * 64), 0, s,
-                               A, lda, B, ldb, C, ldc, M, N, K, e, tilesN);
+            if (SPLIT == 1) {
+              hipLaunchKernelGGL((gemm_f32_glds_kernel<BM, BN, WM, WN, MF, NS, 0>), dim3(grid), dim3(WM * WN * 64), 0,
+                                 s, A, lda, B, ldb, C, ldc, M, N, K, e, tilesN, ImplicitConv{}, SplitK{0, 0, 0});
+            } else {
+              SplitK sk{K / 32 / SPLIT, grid, (long long)M * N};
+              hipLaunchKernelGGL((gemm_f32_glds_kernel<BM, BN, WM, WN, MF, NS, 0>), dim3(grid * SPLIT),
+                                 dim3(WM * WN * 64), 0, s, A, lda, B, ldb, g_slab, N, M, N, K, e, tilesN,
+                                 ImplicitConv{}, sk);
+              hipLaunchKernelGGL(splitk_reduce_kernel, dim3(2048), dim3(256), 0, s, g_slab, SPLIT, sk.slab, C, M, N,
+                                 ldc, e);
+            }
           }};
 }
 
@@ -75,21 +86,23 @@ int main(int argc, char** argv) {
   int iters = argc > 1 ? atoi(argv[1]) : 10;
   const char* filt = argc > 2 ? argv[2] : "";
   std::vector<Shape> shapes = {{"conv7", 10816, 1024, 9216}, {"conv6", 10816, 1024, 4608},
-                               {"conv5", 10816, 512, 2304},  {"conv4", 43264, 256, 1152},
-                               {"conv3", 173056, 128, 576}};
+                               {"conv7big", 65536, 1024, 9216}, {"conv5", 10816, 512, 2304},
+                               {"conv4", 43264, 256, 1152},  {"conv3", 173056, 128, 576}};
   std::vector<Variant> vars = {
-      reg_variant<128, 128, 32, 2, 2, 32>("reg 128x128"),
-      reg_variant<64, 128, 32, 2, 2, 32>("reg 64x128"),
       glds_variant<128, 128, 2, 2, 32, 2>("glds 128x128 ns2"),
-      glds_variant<128, 128, 2, 2, 32, 3>("glds 128x128 ns3"),
-      glds_variant<128, 128, 2, 2, 32, 4>("glds 128x128 ns4"),
+      glds_variant<128, 128, 2, 2, 32, 2, 2>("glds 128x128 ns2 sk2"),
+      glds_variant<128, 128, 2, 2, 32, 2, 3>("glds 128x128 ns2 sk3"),
+      glds_variant<128, 128, 2, 2, 32, 2, 4>("glds 128x128 ns2 sk4"),
       glds_variant<256, 128, 4, 2, 32, 2>("glds 256x128 w8 ns2"),
-      glds_variant<256, 128, 4, 2, 32, 3>("glds 256x128 w8 ns3"),
-      glds_variant<128, 256, 2, 4, 32, 2>("glds 128x256 w8 ns2"),
-      glds_variant<64, 128, 2, 2, 32, 3>("glds 64x128 ns3"),
+      glds_variant<256, 128, 4, 2, 32, 2, 3>("glds 256x128 w8 sk3"),
+      glds_variant<256, 128, 4, 2, 32, 2, 4>("glds 256x128 w8 sk4"),
+      glds_variant<256, 128, 4, 2, 32, 2, 8>("glds 256x128 w8 sk8"),
+      glds_variant<64, 128, 2, 2, 32, 2>("glds 64x128 ns2"),
+      glds_variant<64, 128, 2, 2, 32, 2, 3>("glds 64x128 ns2 sk3"),
   };
   hipStream_t st;
   CK(hipStreamCreate(&st));
+  CK(hipMalloc(&g_slab, (size_t)8 * 65536 * 1024 * 4));  // up to 8 partials of the largest C
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));

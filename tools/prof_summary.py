@@ -19,17 +19,20 @@ from collections import defaultdict
 
 # kernel order of one YOLOv2-tiny forward in the default (fused) plan
 ORDER = ["conv0.direct", "conv1.gemm", "conv2.gemm", "conv3.gemm", "conv4.gemm", "conv5.gemm", "pool5",
-         "conv6.gemm", "conv7.gemm", "conv8.gemm"]
+         "conv6.gemm", "conv6.reduce", "conv7.gemm", "conv7.reduce", "conv8.gemm"]
 # ... and with DNN_HIP_FUSE=0 (explicit im2col + GEMM, separate pools)
 ORDER_UNFUSED = []
 for _i in range(9):
     if _i < 8:
         ORDER_UNFUSED.append(f"conv{_i}.im2col")
     ORDER_UNFUSED.append(f"conv{_i}.gemm")
+    if _i in (6, 7):
+        ORDER_UNFUSED.append(f"conv{_i}.reduce")
     if _i < 6:
         ORDER_UNFUSED.append(f"pool{_i}")
 
-OURS = ("dnnhip::im2col", "dnnhip::gemm", "dnnhip::maxpool", "dnnhip::conv3x3_pool2_direct")
+OURS = ("dnnhip::im2col", "dnnhip::gemm", "dnnhip::maxpool", "dnnhip::conv3x3_pool2_direct",
+        "dnnhip::splitk_reduce")
 
 
 def _ours(name):
