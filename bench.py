@@ -184,9 +184,9 @@ def main():
         # the conv-level figures below charge its time to the GEMM
         red = by_name.get(DOMINANT.replace(".gemm", ".reduce"))
         red_s = red[1] / max(red[2], 1) / 1e3 if red else 0.0
-        gemm_fl = sum(v[0]["flops"] for n, v in by_name.items() if n.endswith(".gemm"))
-        gemm_s = sum(v[1] / max(v[2], 1) for n, v in by_name.items()
-                     if n.endswith(".gemm") or n.endswith(".reduce")) / 1e3
+        mfma = (".gemm", ".patch", ".reduce")  # the MFMA conv kernels (+ their split-K reduces)
+        gemm_fl = sum(v[0]["flops"] for n, v in by_name.items() if n.endswith(mfma))
+        gemm_s = sum(v[1] / max(v[2], 1) for n, v in by_name.items() if n.endswith(mfma)) / 1e3
         conv67 = [by_name[n] for n in ("conv6.gemm", "conv6.reduce", "conv7.gemm", "conv7.reduce") if n in by_name]
         c67_fl = sum(v[0]["flops"] for v in conv67)
         c67_s = sum(v[1] / max(v[2], 1) for v in conv67) / 1e3

@@ -1,0 +1,184 @@
+// Patch conv: 3x3 / stride 1 / SAME conv with 16 or 32 input channels (YOLOv2-tiny conv1:
+// 208x208x16 -> 32) + bias/BN/leaky epilogue + the following 2x2/stride-2 max pool, on
+// fp32 MFMA 16x16x4.
+//
+// With K = 144 the implicit GEMM (gemm_f32_glds_kernel MODE 2) spends more vector issue on
+// per-row setup, per-tap DMA address arithmetic and the 4 epilogues of every pooled output
+// than the MFMAs take (≈1,100 VALU instructions per wave against 80 MFMAs, SQ counters in
+// profiles/).  Here a workgroup owns a 16x16-pixel output tile and 32 output channels:
+//   * one LDS-DMA pass stages the (16+2)x(16+2)xC input patch (halo and SAME padding from
+//     the zero page) and the 32 x Kpad weight block; nothing else is loaded;
+//   * every tap (dy, dx) is then a constant LDS offset from a per-lane base, so the main
+//     loop is ds_read_b128 + MFMA only;
+//   * A rows are pool-window-major (row = 4*window + 2*dy + dx), so the 16x16x4 result keeps
+//     a window's 4 conv outputs in one lane's 4 registers; the lane pools first and runs the
+//     epilogue once per pooled output (see pool_then_epilogue).
+// K order: tap-major, channels in groups of 16 with the K permutation of gemm_f32.h (lane part
+// p reads channels 4p..4p+3 and feeds them to 4 consecutive MFMAs), i.e. the exact MFMA
+// sequence per accumulator of the implicit-GEMM path with the 16x16x4 family, so both give
+// the same bits (tests/test_gpu_parity.py).
+#include <hip/hip_runtime.h>
+#include <cfloat>
+#include "dnn_common.h"
+#include "gemm_f32.h"
+
+namespace dnnhip {
+
+constexpr int PT_EDGE = 16;           // conv-output pixels per tile edge (8 x 8 pool windows)
+constexpr int PT_PATCH = PT_EDGE + 2;  // patch edge: 1-pixel halo on each side
+constexpr int PT_NB = 32;             // output channels per workgroup
+
+__host__ __device__ constexpr int patch_kpad(int C) { return (9 * C + 31) / 32 * 32; }
+
+// max (or min, for a channel whose epilogue is non-increasing) of a window's 4 raw conv
+// outputs, then the epilogue once.  The epilogue f = leaky(((v + b) - mean) / sq * gamma) is
+// a chain of IEEE-rounded monotone steps (sq > 0), non-decreasing for gamma >= 0 and
+// non-increasing for gamma < 0 (alpha < 0 for the avx alpha/beta form), so
+// max_i f(v_i) == f(max_i v_i) (resp. f(min_i v_i)) value for value — the same result as the
+// reference's epilogue-then-pool (dnn_openblas.c:220-254), with 1 epilogue per pooled output.
+__device__ __forceinline__ float pool_then_epilogue(f32x4 v, float pb, float pm, float ps, float pg, int flags) {
+  const bool dec = ((flags & EPI_BN) && pg < 0.f) || ((flags & EPI_BN_AB) && pm < 0.f);
+  const float hi = __builtin_fmaxf(__builtin_fmaxf(v[0], v[1]), __builtin_fmaxf(v[2], v[3]));
+  const float lo = __builtin_fminf(__builtin_fminf(v[0], v[1]), __builtin_fminf(v[2], v[3]));
+  return apply_epilogue(dec ? lo : hi, pb, pm, ps, pg, flags);
+}
+
+template <int C>
+__global__ void __launch_bounds__(256)
+conv3x3_patch_pool_kernel(const float* __restrict__ in, const float* __restrict__ Bt, float* __restrict__ out,
+                          DirectGeom g, int N, int tilesX, int tilesY, int nblkN, const float* __restrict__ zero,
+                          EpiParams epi) {
+  typedef Mfma<16> MM;
+  constexpr int KP = patch_kpad(C);
+  constexpr int PATCH = PT_PATCH * PT_PATCH * C;  // floats
+  constexpr int PATCH_CH = (PATCH + 255) / 256;    // 1-KiB DMA chunks (64 lanes x 16 B)
+  constexpr int W_CH = PT_NB * KP / 256;
+  static_assert(C % 16 == 0 && (PT_NB * KP) % 256 == 0, "patch conv shape");
+  __shared__ __attribute__((aligned(1024))) float smem[(PATCH_CH + W_CH) * 256];
+
+  // tile order: output-channel block fastest, then x, y, image (neighbours share halo rows)
+  int t = xcd_tile(blockIdx.x, gridDim.x);
+  const int nb = t % nblkN;
+  t /= nblkN;
+  const int tx = t % tilesX;
+  t /= tilesX;
+  const int ty = t % tilesY;
+  const int b = t / tilesY;
+  const int y0 = ty * PT_EDGE, x0 = tx * PT_EDGE;
+  const int lane = threadIdx.x & 63;
+  const int wid = wave_uniform(threadIdx.x >> 6);
+
+  // ---- stage the input patch and the weight block (LDS-DMA, lane-linear destinations)
+  const float* inb = in + (size_t)b * g.H * g.W * C;
+  for (int c = wid; c < PATCH_CH; c += 4) {
+    const int f = c * 256 + 4 * lane;
+    const int pp = f / C, ch = f - pp * C;
+    const int py = pp / PT_PATCH, px = pp - py * PT_PATCH;
+    const int iy = y0 - 1 + py, ix = x0 - 1 + px;
+    const bool ok = pp < PT_PATCH * PT_PATCH && (unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W;
+    lds_dma16(ok ? inb + ((size_t)iy * g.W + ix) * C + ch : zero, smem + c * 256);
+  }
+  const float* wsrc = Bt + (size_t)nb * PT_NB * KP + 4 * lane;
+  for (int c = wid; c < W_CH; c += 4) lds_dma16(wsrc + c * 256, smem + (PATCH_CH + c) * 256);
+  wait_vmcnt<0>();
+  raw_barrier();
+
+  // ---- fragments.  Wave w owns conv rows 4w..4w+3 x 16 columns = 4 M-tiles of 16 rows;
+  // M-tile i covers window row (i>>1) and window columns 4(i&1)..4(i&1)+3; its row r is
+  // window r>>2, position r&3 = (dy, dx) = (pos>>1, pos&1).
+  const int fr = lane & 15, fp = lane >> 4;
+  int abase[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int wi = fr >> 2, pos = fr & 3;
+    const int y = 4 * wid + 2 * (i >> 1) + (pos >> 1);
+    const int x = 2 * (4 * (i & 1) + wi) + (pos & 1);
+    abase[i] = (y * PT_PATCH + x) * C + 4 * fp;
+  }
+  const float* Ws = smem + PATCH_CH * 256;
+  const int bbase = fr * KP + 4 * fp;
+
+  MM::acc_t acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int tap = 0; tap < 9; ++tap) {
+#pragma unroll
+    for (int cc = 0; cc < C / 16; ++cc) {
+      const int aoff = ((tap / 3) * PT_PATCH + (tap % 3)) * C + 16 * cc;
+      const int boff = tap * C + 16 * cc;
+      f32x4 af[4], bf[2];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = *reinterpret_cast<const f32x4*>(smem + abase[i] + aoff);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bf[j] = *reinterpret_cast<const f32x4*>(Ws + bbase + 16 * j * KP + boff);
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[i][j] = MM::op(af[i][s], bf[j][s], acc[i][j]);
+    }
+  }
+
+  // ---- pool + epilogue + store: lane holds window fp of M-tile i, channel 16j + fr
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int n = nb * PT_NB + 16 * j + fr;
+    const float pb = (epi.flags & EPI_BIAS) ? epi.bias[n] : 0.f;
+    const float pm = (epi.flags & (EPI_BN | EPI_BN_AB)) ? epi.mean[n] : 0.f;
+    const float ps = (epi.flags & (EPI_BN | EPI_BN_AB)) ? epi.sq[n] : 1.f;
+    const float pg = (epi.flags & EPI_BN) ? epi.gamma[n] : 1.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int wy = (y0 >> 1) + 2 * wid + (i >> 1), wx = (x0 >> 1) + 4 * (i & 1) + fp;
+      const float v = pool_then_epilogue(acc[i][j], pb, pm, ps, pg, epi.flags);
+      if (wy < g.PH && wx < g.PW && n < N) out[(((size_t)b * g.PH + wy) * g.PW + wx) * N + n] = v;
+    }
+  }
+}
+
+// OC == 32 only: the implicit/explicit GEMMs use the 16x16x4 family for N <= 32 and 32x32x2
+// above, and the plan keeps one MFMA family per layer shape so every path of a layer gives the
+// same bits (the kernel itself handles any OC % 32 == 0).
+bool patch_conv_pool_supported(int C, int OC, int H, int W, int OH, int OW, int kh, int kw, int sh, int sw, int pt,
+                               int pl) {
+  return kh == 3 && kw == 3 && sh == 1 && sw == 1 && pt == 1 && pl == 1 && OH == H && OW == W &&
+         (C == 16 || C == 32) && OC == PT_NB && OH % 2 == 0 && OW % 2 == 0;
+}
+
+int patch_conv_kpad(int C) { return patch_kpad(C); }
+
+int launch_conv3x3_patch_pool(const float* in, const float* Bt, int ldb, float* out, const DirectGeom& g, int C,
+                              int N, const float* zero, const EpiParams& epi, hipStream_t stream) {
+  if (g.B == 0) return 0;
+  if (!(C == 16 || C == 32) || N % PT_NB != 0 || ldb != patch_kpad(C) || g.OH % 2 || g.OW % 2 ||
+      g.PH != g.OH / 2 || g.PW != g.OW / 2 || g.OH != g.H || g.OW != g.W || g.pt != 1 || g.pl != 1) {
+    set_error("patch conv: unsupported shape C=%d N=%d ldb=%d %dx%d", C, N, ldb, g.OH, g.OW);
+    return -2;
+  }
+  const int tilesX = (g.OW + PT_EDGE - 1) / PT_EDGE, tilesY = (g.OH + PT_EDGE - 1) / PT_EDGE;
+  const int nblkN = N / PT_NB;
+  const long long blocks = (long long)g.B * tilesY * tilesX * nblkN;
+  if (blocks > 0x7fffffffLL) {
+    set_error("patch conv: grid too large");
+    return -2;
+  }
+  if (C == 16)
+    hipLaunchKernelGGL((conv3x3_patch_pool_kernel<16>), dim3((unsigned)blocks), dim3(256), 0, stream, in, Bt, out, g,
+                       N, tilesX, tilesY, nblkN, zero, epi);
+  else
+    hipLaunchKernelGGL((conv3x3_patch_pool_kernel<32>), dim3((unsigned)blocks), dim3(256), 0, stream, in, Bt, out, g,
+                       N, tilesX, tilesY, nblkN, zero, epi);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    set_error("launch conv3x3_patch_pool: %s", hipGetErrorString(e));
+    return -1;
+  }
+  return 0;
+}
+
+}  // namespace dnnhip

@@ -136,6 +136,15 @@ bool direct_conv_pool_supported(int cin, int nout, int kh, int kw, int sh, int s
 int launch_conv3x3_pool2_direct(const float* in, const float* w, float* out, const DirectGeom& g, int cin,
                                 int nout, const EpiParams& epi, hipStream_t stream);
 
+// Patch conv (conv_patch.hip): 3x3 / stride 1 / SAME, C in {16, 32}, OC % 32 == 0, even
+// output, + epilogue + fused 2x2/stride-2 max pool on fp32 MFMA 16x16x4.  Bt is the packed
+// [Npad][Kpad] weight block with Kpad == patch_conv_kpad(C); `zero` >= 16 B of zeros.
+bool patch_conv_pool_supported(int C, int OC, int H, int W, int OH, int OW, int kh, int kw, int sh, int sw, int pt,
+                               int pl);
+int patch_conv_kpad(int C);
+int launch_conv3x3_patch_pool(const float* in, const float* Bt, int ldb, float* out, const DirectGeom& g, int C,
+                              int N, const float* zero, const EpiParams& epi, hipStream_t stream);
+
 // element-wise ops of the per-op ABI
 int launch_bias_add(const float* in, const float* b, float* out, long long n, int C, hipStream_t s);
 int launch_bn_mvg(const float* in, const float* mean, const float* sq, const float* gamma, float* out,

@@ -10,13 +10,16 @@
 //   DIRECT_A  1x1 / stride 1 / unpadded: the NHWC input IS the col matrix, GEMM only
 //   IMPLICIT  implicit GEMM: the LDS-DMA loader gathers the im2col rows straight from the
 //             input (per-lane source addresses), no col buffer
-//   DIRECT    3x3 conv with <= 4 input channels (conv0): direct FMA conv, weights in SGPRs
+//   DIRECT    3x3 conv with <= 4 input channels (conv0): direct FMA conv, weights in LDS
+//   PATCH     3x3 SAME conv with 16/32 input channels + 2x2 pool (conv1): input patch and
+//             weights DMA'd to LDS once per tile, taps are constant LDS offsets (conv_patch.hip)
 // and a following 2x2/stride-2 MaxPool2D is fused into the IMPLICIT / DIRECT epilogue
 // (pool-window-major rows), otherwise it is its own pool entry.  Weights are packed once
 // into a device arena as Bt[Npad][Kpad] (K order kh,kw,ic; HWIO as-is for DIRECT) plus four
 // Npad-long epilogue vectors (bias, mean, sqrt(var+eps), gamma).  Activations ping-pong
 // between two workspace buffers.  DNN_HIP_FUSE=0 in the environment at plan creation
-// forces the explicit GEMM path with separate pools (for A/B checks).
+// forces the explicit GEMM path with separate pools (for A/B checks); DNN_HIP_PATCH=0 keeps
+// PATCH-eligible layers on the implicit GEMM.
 #include <hip/hip_runtime.h>
 #include <algorithm>
 #include <cmath>
@@ -64,8 +67,8 @@ static size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
 using namespace dnnhip;
 
-enum ConvMode : int { MODE_GEMM = 0, MODE_DIRECT_A = 1, MODE_IMPLICIT = 2, MODE_DIRECT = 3 };
-static const char* kModeName[] = {"gemm", "direct_a", "implicit", "direct"};
+enum ConvMode : int { MODE_GEMM = 0, MODE_DIRECT_A = 1, MODE_IMPLICIT = 2, MODE_DIRECT = 3, MODE_PATCH = 4 };
+static const char* kModeName[] = {"gemm", "direct_a", "implicit", "direct", "patch"};
 
 struct PlanLayer {
   int type = 0;  // 0 conv, 1 pool
@@ -97,6 +100,7 @@ struct dnn_plan {
   int batch = 0, in_h = 0, in_w = 0, in_c = 0;
   int cur_h = 0, cur_w = 0, cur_c = 0;
   bool fuse = true;
+  bool patch = true;
   std::vector<PlanLayer> layers;
   std::vector<KernelDesc> kernels;
   int device = -1;
@@ -144,8 +148,8 @@ static void layout(dnn_plan* p) {
         p->kernels.push_back({nm, (int)i, 0, 0.0, 4.0 * M * L.K + in_b});
         snprintf(nm, sizeof(nm), "conv%d.gemm", nconv++);
         p->kernels.push_back({nm, (int)i, 1, flops, 4.0 * M * L.K + w_b + out_b});
-      } else if (L.mode == MODE_DIRECT) {
-        snprintf(nm, sizeof(nm), "conv%d.direct", nconv++);
+      } else if (L.mode == MODE_DIRECT || L.mode == MODE_PATCH) {
+        snprintf(nm, sizeof(nm), L.mode == MODE_DIRECT ? "conv%d.direct" : "conv%d.patch", nconv++);
         p->kernels.push_back({nm, (int)i, 1, flops, in_b + w_b + out_b});
       } else {  // DIRECT_A reads the input as A; IMPLICIT reads it once per tap in the ideal
         snprintf(nm, sizeof(nm), "conv%d.gemm", nconv);
@@ -185,6 +189,8 @@ int dnn_plan_create(int batch, int in_h, int in_w, int in_c, dnn_plan** out) {
   p->in_c = p->cur_c = in_c;
   const char* f = getenv("DNN_HIP_FUSE");
   p->fuse = !(f && f[0] == '0');
+  const char* pe = getenv("DNN_HIP_PATCH");
+  p->patch = !(pe && pe[0] == '0');
   *out = p;
   return 0;
 }
@@ -291,6 +297,10 @@ int dnn_plan_add_max_pool(dnn_plan* p, int kh, int kw, int stride_h, int stride_
       bool ok = false;
       if (prev.mode == MODE_IMPLICIT) {
         ok = true;
+        if (p->patch && patch_conv_pool_supported(prev.C, prev.OC, prev.H, prev.W, prev.OH, prev.OW, prev.kh, prev.kw,
+                                                  prev.sh, prev.sw, prev.pt, prev.pl) &&
+            prev.Kpad == patch_conv_kpad(prev.C))
+          prev.mode = MODE_PATCH;  // same packed weights (Bt[Npad][Kpad]) as the implicit GEMM
       } else if (prev.mode == MODE_GEMM && direct_conv_pool_supported(prev.C, prev.OC, prev.kh, prev.kw, prev.sh,
                                                                       prev.sw)) {
         prev.mode = MODE_DIRECT;
@@ -458,6 +468,11 @@ int dnn_plan_run(dnn_plan* p, int n, const float* d_in, float* d_out, void* stre
         case MODE_DIRECT: {
           DirectGeom g{n, L.H, L.W, L.OH, L.OW, L.PH, L.PW, L.pt, L.pl};
           rc = launch_conv3x3_pool2_direct(cur, wt, dst, g, L.C, L.OC, epi, s);
+          break;
+        }
+        case MODE_PATCH: {
+          DirectGeom g{n, L.H, L.W, L.OH, L.OW, L.PH, L.PW, L.pt, L.pl};
+          rc = launch_conv3x3_patch_pool(cur, wt, L.Kpad, dst, g, L.C, L.OC, zero, epi, s);
           break;
         }
       }

@@ -152,8 +152,8 @@ def test_plan_shape_memory_and_flops_host_only(monkeypatch, fuse):
             assert len(names) == 25
             assert sum(n.endswith(".im2col") for n in names) == 8
             assert sum(n.startswith("pool") for n in names) == 6
-        else:  # conv0 direct + pool, conv1-7 implicit GEMM (conv1-4 with the pool), pool5 (s1)
-            assert names == ["conv0.direct", "conv1.gemm", "conv2.gemm", "conv3.gemm", "conv4.gemm", "conv5.gemm",
+        else:  # conv0 direct + pool, conv1 patch + pool, conv2-7 implicit GEMM (2-5 with the pool), pool5 (s1)
+            assert names == ["conv0.direct", "conv1.patch", "conv2.gemm", "conv3.gemm", "conv4.gemm", "conv5.gemm",
                              "pool5", "conv6.gemm", "conv6.reduce", "conv7.gemm", "conv7.reduce", "conv8.gemm"]
         buf = ctypes.create_string_buffer(8192)
         assert lib.dnn_plan_describe(h, buf, 8192) == 0

@@ -261,10 +261,53 @@ def test_implicit_gemm_and_fused_pool_vs_explicit_bit_exact(monkeypatch, case):
         eng = dnn_hip.DnnInferenceEngine(_chain(x.shape, k, **kw), False)
         outs[fuse] = eng.run(x)
         desc = eng.plan().describe()
-        assert ("implicit" in desc) == (fuse == "1")
+        assert ("implicit" in desc or "patch" in desc) == (fuse == "1")
         assert ("+pool2x2s2" in desc) == (fuse == "1" and pool)
     assert np.array_equal(outs["1"], outs["0"])
     assert R.normwise_err(outs["1"], _oracle_chain(x, k, **kw)) < LAYER_TOL
+
+
+PATCH_CASES = [
+    # B, H, W, C, epilogue   (3x3 SAME, 32 outputs, 2x2/s2 pool -> patch kernel)
+    (2, 26, 22, 16, "bn"),        # partial 16x16 tiles on both edges
+    (1, 208, 208, 16, "bn"),      # YOLOv2-tiny conv1 at batch 1
+    (3, 34, 18, 32, "bn"),        # C = 32 (two 16-channel groups per tap)
+    (2, 16, 16, 16, "bn_neg"),    # negative gamma: min-pool before the epilogue
+    (2, 18, 20, 16, "bias"),      # bias + leaky only
+    (1, 12, 14, 16, "none"),      # bare conv + pool
+]
+
+
+@pytest.mark.parametrize("case", PATCH_CASES)
+def test_patch_conv_pool_bit_exact(monkeypatch, case):
+    """The patch kernel issues the implicit GEMM's exact MFMA sequence per accumulator and
+    pools before the (monotone) epilogue: patch == implicit == explicit im2col+GEMM+pool, bit
+    for bit (value equality), and within tolerance of the oracle."""
+    B, H, W, C, ep = case
+    od = 32
+    rng = np.random.default_rng(H * W + C)
+    x = rng.standard_normal((B, H, W, C)).astype(np.float32)
+    k = (rng.standard_normal((3, 3, C, od)) * np.sqrt(2.0 / (9 * C))).astype(np.float32)
+    bias = rng.standard_normal(od).astype(np.float32) * 0.1
+    gamma = rng.uniform(0.5, 1.5, od).astype(np.float32)
+    if ep == "bn_neg":
+        gamma[::3] *= -1
+    bn = (rng.standard_normal(od).astype(np.float32) * 0.1, rng.uniform(0.5, 1.5, od).astype(np.float32), gamma)
+    kw = dict(pool=(2, 2, "SAME"))
+    if ep in ("bn", "bn_neg"):
+        kw.update(bias=bias, bn=bn, leaky=True)
+    elif ep == "bias":
+        kw.update(bias=bias, leaky=True)
+    outs = {}
+    for fuse, patch, mode in (("1", "1", "patch"), ("1", "0", "implicit"), ("0", "1", "gemm")):
+        monkeypatch.setenv("DNN_HIP_FUSE", fuse)
+        monkeypatch.setenv("DNN_HIP_PATCH", patch)
+        eng = dnn_hip.DnnInferenceEngine(_chain(x.shape, k, **kw), False)
+        outs[mode] = eng.run(x)
+        assert f"mode={mode} " in eng.plan().describe()
+    assert np.array_equal(outs["patch"], outs["implicit"])
+    assert np.array_equal(outs["patch"], outs["gemm"])
+    assert R.normwise_err(outs["patch"], _oracle_chain(x, k, **kw)) < LAYER_TOL
 
 
 @pytest.mark.parametrize("hw", [(40, 38), (13, 13), (17, 22)])

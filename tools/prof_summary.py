@@ -18,7 +18,7 @@ import json
 from collections import defaultdict
 
 # kernel order of one YOLOv2-tiny forward in the default (fused) plan
-ORDER = ["conv0.direct", "conv1.gemm", "conv2.gemm", "conv3.gemm", "conv4.gemm", "conv5.gemm", "pool5",
+ORDER = ["conv0.direct", "conv1.patch", "conv2.gemm", "conv3.gemm", "conv4.gemm", "conv5.gemm", "pool5",
          "conv6.gemm", "conv6.reduce", "conv7.gemm", "conv7.reduce", "conv8.gemm"]
 # ... and with DNN_HIP_FUSE=0 (explicit im2col + GEMM, separate pools)
 ORDER_UNFUSED = []
@@ -32,7 +32,7 @@ for _i in range(9):
         ORDER_UNFUSED.append(f"pool{_i}")
 
 OURS = ("dnnhip::im2col", "dnnhip::gemm", "dnnhip::maxpool", "dnnhip::conv3x3_pool2_direct",
-        "dnnhip::splitk_reduce")
+        "dnnhip::splitk_reduce", "dnnhip::conv3x3_patch_pool")
 
 
 def _ours(name):
