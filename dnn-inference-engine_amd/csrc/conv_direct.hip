@@ -9,9 +9,10 @@
 // and writes only the pooled tensor: 13 MB in + 2.8 MB out per image.
 //
 // Per output element the math is the reference's: conv (fp32, FMA accumulation in (kh,kw,c)
-// order), then bias_add, batch_norm and leaky_relu in apply_epilogue's order, then the
-// max over the window with dnn_openblas.c's comparison `m >= x ? m : x`, window cells past
-// the conv output (odd sizes, SAME pool padding) reading -FLT_MAX (dnn_openblas.py:232-235).
+// order), then bias_add, batch_norm and leaky_relu in apply_epilogue's order and the window
+// max (dnn_openblas.c:220-254) — evaluated as pool-then-epilogue (pool_then_epilogue in
+// gemm_f32.h: equal values, one epilogue per pooled output), window cells past the conv output
+// (odd sizes, SAME pool padding, -FLT_MAX in dnn_openblas.py:232-235) left out.
 #include <hip/hip_runtime.h>
 #include <cfloat>
 #include "dnn_common.h"
@@ -80,14 +81,11 @@ conv3x3_pool2_direct_kernel(const float* __restrict__ in, const float* __restric
     const float pm = (epi.flags & (EPI_BN | EPI_BN_AB)) ? epi.mean[o] : 0.f;
     const float ps = (epi.flags & (EPI_BN | EPI_BN_AB)) ? epi.sq[o] : 1.f;
     const float pg = (epi.flags & EPI_BN) ? epi.gamma[o] : 1.f;
-    float m = 0.f;
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      const int oy = 2 * py + (p >> 1), ox = 2 * px + (p & 1);
-      const float v = (oy < g.OH && ox < g.OW) ? apply_epilogue(acc[p][o], pb, pm, ps, pg, epi.flags) : -FLT_MAX;
-      m = p == 0 ? v : (m >= v ? m : v);
-    }
-    pooled[o] = m;
+    // window cells past the conv output (SAME pool padding) repeat cell (0,0)
+    const bool x1 = 2 * px + 1 < g.OW, y1 = 2 * py + 1 < g.OH;
+    const f32x4 v = {acc[0][o], x1 ? acc[1][o] : acc[0][o], y1 ? acc[2][o] : acc[0][o],
+                     x1 && y1 ? acc[3][o] : acc[0][o]};
+    pooled[o] = pool_then_epilogue(v, pb, pm, ps, pg, epi.flags);
   }
   if (py < g.PH && px < g.PW) {
     float* dst = out + (((size_t)b * g.PH + py) * g.PW + px) * NOUT;

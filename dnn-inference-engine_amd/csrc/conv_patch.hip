@@ -30,19 +30,6 @@ constexpr int PT_NB = 32;             // output channels per workgroup
 
 __host__ __device__ constexpr int patch_kpad(int C) { return (9 * C + 31) / 32 * 32; }
 
-// max (or min, for a channel whose epilogue is non-increasing) of a window's 4 raw conv
-// outputs, then the epilogue once.  The epilogue f = leaky(((v + b) - mean) / sq * gamma) is
-// a chain of IEEE-rounded monotone steps (sq > 0), non-decreasing for gamma >= 0 and
-// non-increasing for gamma < 0 (alpha < 0 for the avx alpha/beta form), so
-// max_i f(v_i) == f(max_i v_i) (resp. f(min_i v_i)) value for value — the same result as the
-// reference's epilogue-then-pool (dnn_openblas.c:220-254), with 1 epilogue per pooled output.
-__device__ __forceinline__ float pool_then_epilogue(f32x4 v, float pb, float pm, float ps, float pg, int flags) {
-  const bool dec = ((flags & EPI_BN) && pg < 0.f) || ((flags & EPI_BN_AB) && pm < 0.f);
-  const float hi = __builtin_fmaxf(__builtin_fmaxf(v[0], v[1]), __builtin_fmaxf(v[2], v[3]));
-  const float lo = __builtin_fminf(__builtin_fminf(v[0], v[1]), __builtin_fminf(v[2], v[3]));
-  return apply_epilogue(dec ? lo : hi, pb, pm, ps, pg, flags);
-}
-
 template <int C>
 __global__ void __launch_bounds__(256)
 conv3x3_patch_pool_kernel(const float* __restrict__ in, const float* __restrict__ Bt, float* __restrict__ out,

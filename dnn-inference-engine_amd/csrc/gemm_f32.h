@@ -250,11 +250,24 @@ __device__ __forceinline__ void lds_dma16(const float* src, float* dst) {
   __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
 }
 
+// max (or min, for a channel whose epilogue is non-increasing) of a pool window's raw conv
+// outputs, then the epilogue once.  The epilogue f = leaky(((v + b) - mean) / sq * gamma) is a
+// chain of IEEE-rounded monotone steps (sq > 0): non-decreasing for gamma >= 0, non-increasing
+// for gamma < 0 (alpha < 0 for the avx alpha/beta form).  So max_i f(v_i) == f(max_i v_i)
+// (resp. f(min_i v_i)) value for value: the reference's epilogue-then-pool result
+// (dnn_openblas.c:220-254) with one epilogue per pooled output instead of four.
+__device__ __forceinline__ float pool_then_epilogue(f32x4 v, float pb, float pm, float ps, float pg, int flags) {
+  const bool dec = ((flags & EPI_BN) && pg < 0.f) || ((flags & EPI_BN_AB) && pm < 0.f);
+  const float hi = __builtin_fmaxf(__builtin_fmaxf(v[0], v[1]), __builtin_fmaxf(v[2], v[3]));
+  const float lo = __builtin_fminf(__builtin_fminf(v[0], v[1]), __builtin_fminf(v[2], v[3]));
+  return apply_epilogue(dec ? lo : hi, pb, pm, ps, pg, flags);
+}
+
 // Pool-fused store (implicit mode with pool): rows are pool-window-major, 4 rows per 2x2
 // window, and both MFMA layouts keep a window's 4 rows in 4 consecutive registers of one
 // lane (32x32x2: regs 4q..4q+3 = rows 8q+4h+0..3; 16x16x4: regs 0..3 = rows 4(l>>4)+0..3).
-// Each lane folds its 4 epilogue values with dnn_openblas.c's `m >= x ? m : x` in window
-// order (0,0),(0,1),(1,0),(1,1); rows past the conv output read -FLT_MAX (SAME pool pad).
+// Window cells past the conv output (odd OH/OW: the SAME pool's padding, -FLT_MAX in the
+// reference) are left out by repeating cell (0,0), which always exists.
 template <int MF, int TM, int TN, int WTM, int WTN>
 __device__ __forceinline__ void store_tile_pool(const typename Mfma<MF>::acc_t (&acc)[TM][TN],
                                                 float* __restrict__ C, int ldc, int M, int N, int m0, int n0,
@@ -263,6 +276,7 @@ __device__ __forceinline__ void store_tile_pool(const typename Mfma<MF>::acc_t (
   typedef Mfma<MF> MM;
   const int oc = MM::out_col(lane);
   const int nwin = M >> 2;
+  const bool ragged = ((ic.OH | ic.OW) & 1) != 0;
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int n = n0 + wn * WTN + j * MF + oc;
@@ -277,17 +291,15 @@ __device__ __forceinline__ void store_tile_pool(const typename Mfma<MF>::acc_t (
       for (int q = 0; q < MM::REGS / 4; ++q) {
         const int win = (m0 + wm * WTM + i * MF + MM::out_row(lane, 4 * q)) >> 2;
         if (win >= nwin) continue;
-        const int px = win % ic.PW, t = win / ic.PW, py = t % ic.PH;
-        float m = 0.f;
-#pragma unroll
-        for (int pos = 0; pos < 4; ++pos) {
-          const int oy = 2 * py + (pos >> 1), ox = 2 * px + (pos & 1);
-          const float v = (oy < ic.OH && ox < ic.OW)
-                              ? apply_epilogue(acc[i][j][4 * q + pos], pb, pm, ps, pg, epi.flags)
-                              : -FLT_MAX;
-          m = pos == 0 ? v : (m >= v ? m : v);
+        f32x4 v = {acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]};
+        if (ragged) {
+          const int px = win % ic.PW, py = (win / ic.PW) % ic.PH;
+          const bool x1 = 2 * px + 1 < ic.OW, y1 = 2 * py + 1 < ic.OH;
+          if (!x1) v[1] = v[0];
+          if (!y1) v[2] = v[0];
+          if (!(x1 && y1)) v[3] = v[0];
         }
-        C[(size_t)win * ldc + n] = m;
+        C[(size_t)win * ldc + n] = pool_then_epilogue(v, pb, pm, ps, pg, epi.flags);
       }
     }
   }
@@ -305,29 +317,32 @@ struct SplitK {
 
 // Sum of the split-K partials in split order, ((p0 + p1) + p2) ..., then the fused epilogue.
 // part: [splits][M][N] (slab floats apart), C: [M][ldc].  HBM-bound: (splits + 1) * M * N * 4 B.
+// Thread layout (no per-element index division): a block row of nqb threads covers channel
+// quads q0, q0 + nqb, ... (epilogue parameters loaded once per quad); the block's rp rows
+// stride over M.
 static __global__ void __launch_bounds__(256) __attribute__((unused))
 splitk_reduce_kernel(const float* __restrict__ part, int splits, long long slab, float* __restrict__ C, int M,
-                     int N, int ldc, EpiParams epi) {
+                     int N, int ldc, EpiParams epi, int nqb, int rp) {
   const int nq = N >> 2;  // N % 4 == 0 (checked by the launcher)
-  const long long total = (long long)M * nq;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
-       i += (long long)gridDim.x * blockDim.x) {
-    const int m = (int)(i / nq), n = (int)(i - (long long)m * nq) * 4;
-    const float* p = part + (size_t)m * N + n;
-    f32x4 v = *reinterpret_cast<const f32x4*>(p);
-    for (int s = 1; s < splits; ++s) {
-      const f32x4 w = *reinterpret_cast<const f32x4*>(p + s * slab);
-      v = v + w;
+  const int q0 = threadIdx.x % nqb, r = threadIdx.x / nqb;
+  if (r >= rp) return;
+  for (int q = q0; q < nq; q += nqb) {
+    const int n = 4 * q;
+    f32x4 pb = {0.f, 0.f, 0.f, 0.f}, pm = {0.f, 0.f, 0.f, 0.f}, ps = {1.f, 1.f, 1.f, 1.f}, pg = {1.f, 1.f, 1.f, 1.f};
+    if (epi.flags & EPI_BIAS) pb = *reinterpret_cast<const f32x4*>(epi.bias + n);
+    if (epi.flags & (EPI_BN | EPI_BN_AB)) {
+      pm = *reinterpret_cast<const f32x4*>(epi.mean + n);
+      ps = *reinterpret_cast<const f32x4*>(epi.sq + n);
     }
-    float* c = C + (size_t)m * ldc + n;
+    if (epi.flags & EPI_BN) pg = *reinterpret_cast<const f32x4*>(epi.gamma + n);
+    for (int m = blockIdx.x * rp + r; m < M; m += gridDim.x * rp) {
+      const float* p = part + (size_t)m * N + n;
+      f32x4 v = *reinterpret_cast<const f32x4*>(p);
+      for (int s = 1; s < splits; ++s) v = v + *reinterpret_cast<const f32x4*>(p + s * slab);
+      f32x4 o;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int ne = n + e;
-      const float pb = (epi.flags & EPI_BIAS) ? epi.bias[ne] : 0.f;
-      const float pm = (epi.flags & (EPI_BN | EPI_BN_AB)) ? epi.mean[ne] : 0.f;
-      const float ps = (epi.flags & (EPI_BN | EPI_BN_AB)) ? epi.sq[ne] : 1.f;
-      const float pg = (epi.flags & EPI_BN) ? epi.gamma[ne] : 1.f;
-      c[e] = apply_epilogue(v[e], pb, pm, ps, pg, epi.flags);
+      for (int e = 0; e < 4; ++e) o[e] = apply_epilogue(v[e], pb[e], pm[e], ps[e], pg[e], epi.flags);
+      *reinterpret_cast<f32x4*>(C + (size_t)m * ldc + n) = o;
     }
   }
 }

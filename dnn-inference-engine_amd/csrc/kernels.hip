@@ -280,11 +280,15 @@ int launch_splitk_reduce(const float* slab, int splits, long long M, int N, floa
     set_error("splitk_reduce: N %d must be a multiple of 4", N);
     return -2;
   }
-  long long total = M * (N / 4);
-  long long blocks = (total + 255) / 256;
-  if (blocks > 4096) blocks = 4096;
+  if (M > 0x7fffffffLL || ldc % 4 != 0) {
+    set_error("splitk_reduce: M %lld / ldc %d unsupported", M, ldc);
+    return -2;
+  }
+  const int nq = N / 4, nqb = nq < 256 ? nq : 256, rp = 256 / nqb;
+  long long blocks = (M + rp - 1) / rp;
+  if (blocks > 2048) blocks = 2048;
   hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, slab, splits,
-                     M * (long long)N, C, (int)M, N, ldc, epi);
+                     M * (long long)N, C, (int)M, N, ldc, epi, nqb, rp);
   return check_launch("splitk_reduce");
 }
 
