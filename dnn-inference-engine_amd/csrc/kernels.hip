@@ -135,8 +135,12 @@ int choose_gemm_cfg(long long M, int N, int K) {
   if (N <= 16) return GEMM_256x16_K32;
   if (N <= 32) return GEMM_256x32_K16;
   if (N <= 64) return GEMM_128x64_K32;
+  // 128x128 tiles (2 per CU) when the long K split into choose_splitk(N, K) parts still gives
+  // at least 512 work units; else 64x128 (3 per CU).  Both are the 32x32x2 family with the same
+  // K permutation, and the split itself depends on (N, K) only, so the summation order of an
+  // output element never depends on M.
   long long t128 = ((M + 127) / 128) * ((N + 127) / 128);
-  if (K >= 4096 && t128 >= 512) return GEMM_128x128_K32;
+  if (K >= 2048 && t128 * choose_splitk(N, K) >= 512) return GEMM_128x128_K32;
   return GEMM_64x128_K32;
 }
 
@@ -153,12 +157,13 @@ bool implicit_conv_supported(int C, int kh, int kw) {
   return (C == 16 || C % 32 == 0) && kh * kw <= 30;
 }
 
-// Split-K for the long-K wide layers: 680 tiles of conv6/7 at batch 64 fill 512 two-per-CU
-// slots 1.33 times; three K splits make it 3.98 (measured conv7 116 -> 127 TF including the
-// reduce, tools/gemm_bench.hip, profiles/r01_gemm_bench_v2.txt).  Chosen from (N, K) only so
-// every batch size sums in the same order.
+// Split-K for the long-K wide layers: 680 128x128 tiles of conv6/7 at batch 64 fill 512
+// two-per-CU slots 1.33 times; three K splits make it 3.98 (measured conv7 116 -> 127 TF
+// including the reduce, tools/gemm_bench.hip, profiles/r01_gemm_bench_v2.txt); conv5's 340
+// tiles become 1020 units (1.99 rounds).  Chosen from (N, K) only so every batch size sums in
+// the same order.
 int choose_splitk(int N, int K) {
-  if (N >= 512 && N % 4 == 0 && K >= 4096 && (K / 32) % 3 == 0) return 3;
+  if (N >= 512 && N % 4 == 0 && K >= 2048 && (K / 32) % 3 == 0) return 3;
   return 1;
 }
 

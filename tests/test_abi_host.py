@@ -114,7 +114,7 @@ def test_plan_shape_memory_and_flops_host_only(monkeypatch, fuse):
     wb, sb = dnn_hip.Plan.memory(64, (416, 416, 3), entries)
     nparams = sum(w["kernel"].size for w in ws)
     assert wb >= 4 * nparams and wb < 4 * nparams * 1.2
-    slab = 3 * 64 * 13 * 13 * 1024 * 4  # split-K partials of conv6/conv7 (3 splits)
+    slab = 3 * 64 * 13 * 13 * 1024 * 4  # split-K partials of conv5/conv6/conv7 (3 splits)
     if fuse == "0":
         # two activation buffers (conv0 output, 64x416x416x16) + the largest col buffer
         assert sb >= 2 * 64 * 416 * 416 * 16 * 4 + slab
@@ -146,20 +146,20 @@ def test_plan_shape_memory_and_flops_host_only(monkeypatch, fuse):
         assert flops == pytest.approx(64 * 6.971e9, rel=1e-3)
         # the 1x1 conv8 reads its input directly (no im2col)
         assert "conv8.im2col" not in names and "conv8.gemm" in names and "conv7.gemm" in names
-        # conv6 / conv7 (N >= 512, K >= 4096) run split-K = 3 + an ordered reduce kernel
-        assert "conv6.reduce" in names and "conv7.reduce" in names
+        # conv5-7 (N >= 512, K >= 2048) run split-K = 3 + an ordered reduce kernel
+        assert "conv5.reduce" in names and "conv6.reduce" in names and "conv7.reduce" in names
         if fuse == "0":  # explicit im2col for every 3x3 conv, every pool separate
-            assert len(names) == 25
+            assert len(names) == 26
             assert sum(n.endswith(".im2col") for n in names) == 8
             assert sum(n.startswith("pool") for n in names) == 6
         else:  # conv0 direct + pool, conv1 patch + pool, conv2-7 implicit GEMM (2-5 with the pool), pool5 (s1)
             assert names == ["conv0.direct", "conv1.patch", "conv2.gemm", "conv3.gemm", "conv4.gemm", "conv5.gemm",
-                             "pool5", "conv6.gemm", "conv6.reduce", "conv7.gemm", "conv7.reduce", "conv8.gemm"]
+                             "conv5.reduce", "pool5", "conv6.gemm", "conv6.reduce", "conv7.gemm", "conv7.reduce", "conv8.gemm"]
         buf = ctypes.create_string_buffer(8192)
         assert lib.dnn_plan_describe(h, buf, 8192) == 0
         desc = buf.value.decode()
-        assert desc.count("\n") == len(names) - 2 - (8 if fuse == "0" else 0)
-        assert desc.count("splitK=3") == 2
+        assert desc.count("\n") == len(names) - 3 - (8 if fuse == "0" else 0)
+        assert desc.count("splitK=3") == 3
     finally:
         lib.dnn_plan_destroy(h)
 

@@ -415,6 +415,6 @@ def test_plan_timing_api(yolo_b1):
         plan.run_host(x)
     ms, cnt = plan.timing_end()
     ks = plan.kernels()
-    assert len(ms) == len(ks) == 12  # 10 layers + the conv6/conv7 split-K reduces
+    assert len(ms) == len(ks) == 13  # 10 layers + the conv5/6/7 split-K reduces
     assert all(c == 3 for c in cnt)
     assert all(m > 0 for m in ms)

@@ -18,7 +18,7 @@ import json
 from collections import defaultdict
 
 # kernel order of one YOLOv2-tiny forward in the default (fused) plan
-ORDER = ["conv0.direct", "conv1.patch", "conv2.gemm", "conv3.gemm", "conv4.gemm", "conv5.gemm", "pool5",
+ORDER = ["conv0.direct", "conv1.patch", "conv2.gemm", "conv3.gemm", "conv4.gemm", "conv5.gemm", "conv5.reduce", "pool5",
          "conv6.gemm", "conv6.reduce", "conv7.gemm", "conv7.reduce", "conv8.gemm"]
 # ... and with DNN_HIP_FUSE=0 (explicit im2col + GEMM, separate pools)
 ORDER_UNFUSED = []
@@ -26,7 +26,7 @@ for _i in range(9):
     if _i < 8:
         ORDER_UNFUSED.append(f"conv{_i}.im2col")
     ORDER_UNFUSED.append(f"conv{_i}.gemm")
-    if _i in (6, 7):
+    if _i in (5, 6, 7):
         ORDER_UNFUSED.append(f"conv{_i}.reduce")
     if _i < 6:
         ORDER_UNFUSED.append(f"pool{_i}")
