@@ -18,9 +18,10 @@ Rank 0 prints one JSON line: images/s for the whole job, plus
                 the 157.3 TFLOP/s fp32 MFMA peak (MI355X_MICROARCH.md); traffic from the
                 committed PMC summary (profiles/pmc_summary.json) when present;
   conv_mfma     all 9 conv GEMMs together: flops / summed GEMM time as % of fp32 peak;
-  cpu_baseline  the numpy/OpenBLAS restatement of the reference's OpenBLAS engine
-                (oracle/ref_numpy.py: im2col + sgemm, batch 1 per image) timed on this
-                host's cores on a bounded sample (N=1, rank 0 only).
+  cpu_baseline  clean-room restatements of the reference's OpenBLAS engine (value:
+                oracle/ref_numpy.py im2col + sgemm) and AVX engine (avx_equivalent: direct
+                conv, 4 pthreads, and all cores), batch 1 per image, timed on this host's
+                cores on a bounded sample (N=1, rank 0 only).
 """
 import argparse
 import json
@@ -73,12 +74,51 @@ def pmc_traffic(kernel):
         return None
 
 
+def _timed(fn, seconds, min_runs=3, max_runs=200):
+    fn()  # warm
+    times, t0 = [], time.perf_counter()
+    while True:
+        t = time.perf_counter()
+        fn()
+        times.append(time.perf_counter() - t)
+        if (time.perf_counter() - t0 > seconds and len(times) >= min_runs) or len(times) >= max_runs:
+            break
+    return sorted(times)[len(times) // 2], len(times)
+
+
+def _host_info():
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except AttributeError:
+        usable = os.cpu_count() or 1
+    # a shared GPU box grants this job a CPU share (OMP_NUM_THREADS) smaller than nproc
+    share = os.environ.get("OMP_NUM_THREADS", "")
+    if share.isdigit() and int(share) > 0:
+        usable = min(usable, int(share))
+    return {"nproc": os.cpu_count(), "usable_cpus": usable, "cpu": model}
+
+
 def cpu_baseline(seconds):
-    """numpy/OpenBLAS restatement of proj3's OpenBLAS engine: per image im2col + fp32 sgemm
-    (numpy's bundled OpenBLAS), bias/bn/leaky/pool in numpy — the same work per image as
-    dnn_openblas.c:160-194 plus its element-wise passes.  Bounded sample."""
+    """Clean-room CPU restatements of proj3's two CPU engines (oracle/, test infrastructure),
+    timed on this host's cores on a bounded sample (N=1, rank 0 only), batch 1 per image as
+    the reference engines run:
+      value          "OpenBLAS-equivalent": oracle/ref_numpy.py im2col + numpy/OpenBLAS sgemm
+                     + numpy element-wise ops (dnn_openblas.c:160-194 and its passes);
+      avx_equivalent direct conv over 4 pthreads as dnn_avx.c:13,33-126 (oracle/dnn_oracle.c,
+                     gcc -O3 -mavx2, mul+add like _mm256_mul_ps/_mm256_add_ps), folded BN,
+                     leaky max(x, 0.1x), pools; plus the same on all usable cores."""
     sys.path.insert(0, ORACLE)
     import numpy as np
+    import oracle_c
     import ref_numpy as R
     import synth
     try:
@@ -87,22 +127,21 @@ def cpu_baseline(seconds):
                     or [1])
     except Exception:
         cores = os.cpu_count() or 1
+    host = _host_info()
     ws = synth.yolo_weights()
     x = synth.frame(0)
-    R.yolo_forward(ws, x, acc=np.float32)  # warm
-    n, t0 = 0, time.perf_counter()
-    times = []
-    while True:
-        t = time.perf_counter()
-        R.yolo_forward(ws, x, acc=np.float32)
-        times.append(time.perf_counter() - t)
-        n += 1
-        if (time.perf_counter() - t0 > seconds and n >= 3) or n >= 200:
-            break
-    med = sorted(times)[len(times) // 2]
-    return {"value": round(1.0 / med, 3), "unit": "images/s", "cores": int(cores), "kind": "port",
-            "sample": f"{n} single-frame YOLOv2-tiny forwards (median {med * 1e3:.0f} ms), "
-                      "oracle/ref_numpy.py im2col + numpy/OpenBLAS sgemm, batch 1 like dnn_openblas.c"}
+    med, n = _timed(lambda: R.yolo_forward(ws, x, acc=np.float32), 0.6 * seconds)
+    res = {"value": round(1.0 / med, 3), "unit": "images/s", "cores": int(cores), "kind": "port",
+           "sample": f"{n} single-frame YOLOv2-tiny forwards (median {med * 1e3:.0f} ms), "
+                     "oracle/ref_numpy.py im2col + numpy/OpenBLAS sgemm, batch 1 like dnn_openblas.c",
+           "host": host}
+    oc = oracle_c.OracleC()
+    for key, nt in (("avx_equivalent", 4), ("avx_equivalent_all_cores", host["usable_cpus"])):
+        med, n = _timed(lambda: oracle_c.yolo_forward_avx(oc, ws, x, nt), 0.2 * seconds)
+        res[key] = {"value": round(1.0 / med, 3), "unit": "images/s", "cores": int(nt), "kind": "port",
+                    "sample": f"{n} single-frame forwards (median {med * 1e3:.0f} ms), direct conv "
+                              f"{nt} pthreads (oracle/dnn_oracle.c)"}
+    return res
 
 
 def main():

@@ -101,3 +101,29 @@ class OracleC(object):
         out = np.empty((B, oh, ow, c), np.float32)
         self.lib.oracle_max_pool2d(_p(x), _p(out), B, h, w, c, oh, ow, kh, kw, sh, sw, pt, pl, int(gt_below))
         return out
+
+
+def yolo_forward_avx(oc, weights, x, nthreads=4):
+    """The AVX engine's per-node work for one YOLOv2-tiny forward (proj3/dnn_avx.py node
+    order): host pad, direct conv over `nthreads` pthreads (P_THREADS = 4, dnn_avx.c:13),
+    bias_add, batch_norm in the folded alpha/beta form (dnn_avx.py:301-303), leaky max(x, 0.1x)
+    and max pool.  CPU-baseline timing only (bench.py); the numerics oracle is ref_numpy."""
+    from ref_numpy import pad_nhwc  # noqa: E402  (same directory)
+    y = _f32(x)
+    last = len(weights) - 1
+    for i, w in enumerate(weights):
+        k = w["kernel"]
+        kh, kw = k.shape[0], k.shape[1]
+        xp, oh, ow = pad_nhwc(y, kh, kw, 1, 1, "SAME")
+        y = oc.conv2d_direct(xp, k, oh, ow, 1, 1, nthreads=nthreads)
+        y = oc.bias_add(y, w["biases"])
+        if i == last:
+            break
+        alpha = (w["gamma"] / np.sqrt(w["moving_variance"] + np.float32(1e-5))).astype(np.float32)
+        y = oc.batch_norm_ab(y, alpha, (alpha * w["moving_mean"]).astype(np.float32))
+        y = oc.leaky_relu(y, f32_variant=1)
+        if i < 5:
+            y = oc.max_pool2d(y, [1, 2, 2, 1], [1, 2, 2, 1], "SAME")
+        elif i == 5:
+            y = oc.max_pool2d(y, [1, 2, 2, 1], [1, 1, 1, 1], "SAME")
+    return y
