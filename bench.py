@@ -1,10 +1,12 @@
 #!/usr/bin/env python3
 """YOLOv2-tiny 416x416 images/s on 1..8 MI355X through the fused HIP plan.
 
-Workload (BASELINE.json configs[2]/[3]): a step is one forward of YOLOv2-tiny (9 convs as
-im2col + fp32-MFMA GEMM with fused bias/BN/leaky, 6 max pools) over this GPU's batch of 64
-synthetic 416x416x3 fp32 frames already resident in HBM, followed by the gather of all
-ranks' [64,13,13,125] outputs to rank 0 over RCCL.  Weights (random-init, tiny-yolo-voc
+Workload (BASELINE.json configs[2]/[3]): a step is one forward of YOLOv2-tiny (9 convs on
+fp32 MFMA with fused bias/BN/leaky and 2x2 pools, the stride-1 pool) over this GPU's batch of
+64 synthetic 416x416x3 fp32 frames already resident in HBM, then (default --gather
+detections) the on-GPU postprocessing (decode, 0.3 threshold, sort, greedy NMS) and the
+gather of every rank's packed post-NMS detections to rank 0 over RCCL — the north star's
+"gather of detections"; --gather outputs gathers the raw [64,13,13,125] outputs instead.  Weights (random-init, tiny-yolo-voc
 channel plan, synth.py) are broadcast from rank 0 once before timing.  Weak scaling:
 64 frames per GPU at every N.
 
@@ -50,6 +52,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="bound on the CPU-baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--kernels", action="store_true", help="add the per-kernel table to the JSON")
+    ap.add_argument("--gather", choices=("detections", "outputs"), default="detections",
+                    help="per step, gather post-NMS detections (on-GPU postprocessing, the north star's "
+                         "detection gather) or the raw [n,13,13,125] outputs to rank 0")
     return ap.parse_args()
 
 
@@ -149,6 +154,7 @@ def main():
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         relaunch(args)
 
+    import numpy as np
     import torch
     import torch.distributed as tdist
 
@@ -187,9 +193,22 @@ def main():
         plan.run_device(n, inp.data_ptr(), out.data_ptr(), stream)
 
     runner = D.ShardedRunner(compute, B * world, (416, 416, 3), (13, 13, 125), dev)
+    if args.gather == "detections":
+        import yolo_post
+        dbuf = yolo_post.DetectionBuffers(runner.shard_cap, dev)
+
+        def post(out, n):
+            dbuf.run(out.data_ptr(), n, stream)
+            return dbuf.pack(n, stream)
+
+        def one_step():
+            return runner.step_detections(frames, post)
+    else:
+        def one_step():
+            return runner.step(frames)
 
     for _ in range(args.warmup):
-        runner.step(frames)
+        one_step()
     torch.cuda.synchronize()
     if world > 1:
         tdist.barrier()
@@ -200,7 +219,7 @@ def main():
         tdist.barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        full = runner.step(frames)
+        full = one_step()
     torch.cuda.synchronize()
     if world > 1:
         tdist.barrier()
@@ -211,8 +230,22 @@ def main():
         tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
         elapsed = float(t.item())
 
+    post_ms = None
+    if args.gather == "detections":  # the postprocess kernel alone, for the per-kernel table
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(10):
+            dbuf.run(runner.out.data_ptr(), runner.count, stream)
+        e1.record()
+        torch.cuda.synchronize()
+        post_ms = e0.elapsed_time(e1) / 10
     if rank == 0:
-        assert full is not None and full.shape[0] == B * world
+        if args.gather == "detections":
+            dets_u8, counts = full
+            assert len(counts) == B * world
+            n_det = int(np.clip(counts, 0, None).sum())
+        else:
+            assert full is not None and full.shape[0] == B * world
         kinfo = plan.kernels()
         by_name = {k["name"]: (k, ms[i], cnt[i]) for i, k in enumerate(kinfo)}
         k, kms, kc = by_name[DOMINANT]
@@ -245,7 +278,9 @@ def main():
             "dtype": "fp32",
             "data": "synthetic (uniform [0,1) frames, random-init weights, tiny-yolo-voc channel plan)",
             "config": {"workload": "YOLOv2-tiny forward, 416x416x3 NHWC fp32, 64 frames per GPU in HBM, "
-                                   "outputs gathered to rank 0",
+                                   + ("on-GPU postprocessing (decode, 0.3 threshold, sort, NMS), post-NMS "
+                                      "detections gathered to rank 0" if args.gather == "detections"
+                                      else "raw outputs gathered to rank 0"),
                        "model": "yolov2-tiny (9 conv, 6 maxpool)", "global_batch": B * world,
                        "per_gpu_batch": B, "seq_len": None, "parallelism": f"dp{world}"},
             "roofline": {"kernel": DOMINANT, "bound": "mfma", "achieved": round(achieved, 2),
@@ -260,6 +295,9 @@ def main():
                                                      2)},
             "kernel_ms_per_step": round(total_kernel_ms, 4),
         }
+        if args.gather == "detections":
+            res["postprocess"] = {"ms": round(post_ms, 4), "detections_last_step": n_det,
+                                  "gathered_bytes_last_step": int(dets_u8.nbytes + counts.nbytes)}
         if args.kernels:
             res["kernels"] = {n: {"ms": round(v[1] / max(v[2], 1), 4),
                                   "tflops": round(v[0]["flops"] / (v[1] / max(v[2], 1) / 1e3) / 1e12, 2)

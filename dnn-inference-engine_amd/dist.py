@@ -2,17 +2,25 @@
 
 The reference is single-process and single-device; the multi-GPU layer is new.  Frames
 are independent, so a global batch is split into contiguous per-rank shards with no
-exchange between layers.  The only collectives are the two the north star names:
+exchange between layers.  The only collectives are the ones the north star names:
   * one broadcast of the packed weight buffer from rank 0 at start-up (63.5 MB fp32);
-  * one gather of the per-rank outputs to rank 0 per batch ([n,13,13,125] fp32 per rank).
+  * per batch, a gather to rank 0 of either the raw outputs ([n,13,13,125] fp32 per rank,
+    gather_outputs) or — after the on-GPU postprocessing (yolo_post.py) — only the packed
+    detections (40 B each, gather_detections: a few kB per image instead of 84.5 kB).
 One process per GPU, torch.distributed over RCCL ("nccl" backend) on the GPU box, gloo
 for the CPU tests; the compute step is injected, so the same runner drives the HIP plan
 (bench.py) and a CPU stand-in (tests/test_dist_cpu.py).
 """
 import os
 
+import numpy as np
 import torch
 import torch.distributed as dist
+
+# dnn_detection of include/dnn_hip_post.h (= yolo_post.DETECTION_DTYPE; kept here so the
+# gather needs no HIP library)
+DETECTION_DTYPE = np.dtype([("cls", "<i4"), ("score", "<f4"), ("left", "<i8"), ("top", "<i8"), ("right", "<i8"),
+                            ("bottom", "<i8")])
 
 
 def shard_range(total, world, rank):
@@ -60,6 +68,60 @@ def gather_outputs(local, dst=0):
     return torch.cat(parts, 0) if rank == dst else None
 
 
+def gather_detections(packed, total, counts, n, dst=0):
+    """Gather this rank's packed detections to `dst`.
+
+    packed  [rows, 40] uint8 tensor: the rank's detections image-major (yolo_post
+            DetectionBuffers.pack / dnn_yolo_pack_detections), rows >= total
+    total   [1] int32 tensor: valid rows of `packed`
+    counts  [cap] int32 tensor: detections per image (< 0: the image's error code)
+    n       valid images of this rank's shard
+    Returns on `dst` (dets_u8 [P, 40] numpy, counts [sum of n over ranks] numpy int32) in
+    global (rank, image) order; None elsewhere.  One scalar sync for the row count, then
+    (N > 1) an all_gather of two scalars and gathers of max_rank(P) * 40 B and the counts."""
+    p = int(total.item())
+    if not dist.is_initialized() or dist.get_world_size() == 1:
+        return packed[:p].cpu().numpy(), counts[:n].cpu().numpy()
+    rank, world = dist.get_rank(), dist.get_world_size()
+    dev = packed.device
+    sizes = [torch.zeros(2, dtype=torch.int64, device=dev) for _ in range(world)]
+    dist.all_gather(sizes, torch.tensor([p, n], dtype=torch.int64, device=dev))
+    sizes = [tuple(int(v) for v in t.cpu()) for t in sizes]
+    pmax, nmax = max(max(sz[0] for sz in sizes), 1), max(max(sz[1] for sz in sizes), 1)
+    if packed.shape[0] >= pmax:
+        pbuf = packed[:pmax].contiguous()
+    else:
+        pbuf = torch.zeros((pmax, packed.shape[1]), dtype=torch.uint8, device=dev)
+        pbuf[:p] = packed[:p]
+    cbuf = torch.zeros(nmax, dtype=torch.int32, device=dev)
+    cbuf[:n] = counts[:n]
+    pparts = [torch.empty_like(pbuf) for _ in range(world)] if rank == dst else None
+    cparts = [torch.empty_like(cbuf) for _ in range(world)] if rank == dst else None
+    dist.gather(pbuf, pparts, dst=dst)
+    dist.gather(cbuf, cparts, dst=dst)
+    if rank != dst:
+        return None
+    d = torch.cat([pparts[r][:sizes[r][0]] for r in range(world)], 0).cpu().numpy()
+    cnt = torch.cat([cparts[r][:sizes[r][1]] for r in range(world)], 0).cpu().numpy()
+    return d, cnt
+
+
+def unpack_detections(dets_u8, counts):
+    """(packed [P, 40] uint8, counts) from gather_detections -> per image a list of
+    (class, left, top, right, bottom, score), or the negative error code."""
+    rows = np.ascontiguousarray(dets_u8).reshape(-1, 40).view(DETECTION_DTYPE).reshape(-1) if len(dets_u8) else []
+    out, pos = [], 0
+    for n in counts:
+        n = int(n)
+        if n < 0:
+            out.append(n)
+            continue
+        out.append([(int(d["cls"]), int(d["left"]), int(d["top"]), int(d["right"]), int(d["bottom"]),
+                     float(d["score"])) for d in rows[pos:pos + n]])
+        pos += n
+    return out
+
+
 class ShardedRunner(object):
     """Runs `compute(inp, out, n)` on this rank's shard of a global batch and gathers.
 
@@ -95,3 +157,13 @@ class ShardedRunner(object):
             s, c = shard_range(self.global_batch, self.world, r)
             rows.append(full[r * self.shard_cap:r * self.shard_cap + c])
         return torch.cat(rows, 0)
+
+    def step_detections(self, local_in, post):
+        """One batch ending in detections: local compute, then `post(out, n)` -> (packed
+        [rows, 40] uint8, total [1] int32, counts [cap] int32) on this rank's device (the
+        on-GPU postprocessing + pack), then the packed detection gather.  Returns (dets_u8
+        [P, 40], counts [global_batch]) on rank 0 (unpack_detections turns them into rows),
+        None elsewhere."""
+        self.compute(local_in, self.out, self.count)
+        packed, total, counts = post(self.out, self.count)
+        return gather_detections(packed, total, counts, self.count)

@@ -63,3 +63,17 @@ def gpu_available():
         return torch.cuda.is_available()
     except Exception:
         return False
+
+
+@pytest.fixture(scope="session")
+def post_golden():
+    """Postprocessing fixtures (tests/golden/make_golden_post.py): name -> (pred [13,13,125],
+    reference label_boxes as [name, [l, t], [r, b]])."""
+    with open(os.path.join(GOLDEN, "post_golden.json")) as f:
+        gold = json.load(f)["cases"]
+    d = np.load(os.path.join(GOLDEN, "post_cases.npz"))
+    preds = dict(zip([str(n) for n in d["names"]], d["preds"]))
+    for i in range(4):
+        preds[f"net_frame{i}"] = np.load(os.path.join(GOLDEN, f"net_frame{i}.npy")).reshape(13, 13, 125)
+    assert sorted(preds) == sorted(gold)
+    return {k: (preds[k], gold[k]) for k in sorted(gold)}

@@ -18,8 +18,8 @@ import yolo_graph
 import ref_numpy as R
 
 HEADERS = {
-    "libdnn_hip.so": ["dnn_hip_plan.h", "dnn_hip.h"],
-    "libdnn_hip_avx.so": ["dnn_hip_plan.h", "dnn_hip_avx.h"],
+    "libdnn_hip.so": ["dnn_hip_plan.h", "dnn_hip.h", "dnn_hip_post.h"],
+    "libdnn_hip_avx.so": ["dnn_hip_plan.h", "dnn_hip_avx.h", "dnn_hip_post.h"],
 }
 
 
@@ -177,3 +177,16 @@ def test_plan_errors_are_reported():
     finally:
         lib.dnn_plan_destroy(h)
     assert lib.dnn_plan_create(-1, 4, 4, 3, ctypes.byref(h)) != 0
+
+
+def test_postprocess_api_host_checks():
+    import yolo_post
+    assert ctypes.sizeof(yolo_post.Detection) == 40
+    assert "dnn_yolo_postprocess" in declared_functions("dnn_hip_post.h")
+    with pytest.raises(ValueError):
+        yolo_post.postprocessing(np.zeros((13, 13, 124), np.float32))
+    with pytest.raises(ValueError):
+        yolo_post.detect_batch(np.zeros((2, 13, 13, 120), np.float32))
+    # argument validation happens before any GPU call
+    assert dnn_hip.mylib.dnn_yolo_postprocess_host(None, -1, None, 0, None) != 0
+    assert "bad arguments" in dnn_hip.last_error()

@@ -84,3 +84,65 @@ def test_sharded_broadcast_gather_gloo_world2(total):
     root = [r for r in res if r[1] is not None][0]
     assert root[2] == (total, 9, 7, 6)
     assert root[1] == 0.0
+
+
+def _det_worker(rank, world, port, total, q):
+    for p in (REPO, PKG, ORACLE):
+        sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import dist as Dw
+    import post_numpy as PN
+    Dw.init("gloo")
+    try:
+        rng = np.random.default_rng(11)
+        preds = np.stack([PN.synthetic_predictions(rng, n_hot=(i * 7) % 40) for i in range(total)])
+        max_det = 64
+
+        def compute(inp, out, n):  # the "network": predictions are the input frames
+            out[:n] = inp[:n]
+
+        def post(out, n):  # CPU stand-in for dnn_yolo_postprocess + pack: same packed layout
+            packed = np.zeros(out.shape[0] * max_det, Dw.DETECTION_DTYPE)
+            counts = np.zeros(out.shape[0], np.int32)
+            p = 0
+            for i in range(n):
+                rows = PN.detect(out[i].numpy())
+                counts[i] = len(rows)
+                for (c, l, t, r, b, sc) in rows:
+                    packed[p] = (c, sc, l, t, r, b)
+                    p += 1
+            return (torch.from_numpy(packed.view(np.uint8).reshape(-1, 40)), torch.tensor([p], dtype=torch.int32),
+                    torch.from_numpy(counts))
+
+        runner = Dw.ShardedRunner(compute, total, (13, 13, 125), (13, 13, 125), device="cpu")
+        g = runner.step_detections(torch.from_numpy(runner.local_slice(preds)), post)
+        if rank == 0:
+            got = Dw.unpack_detections(*g)
+            expect = [[(c, l, t, r, b, float(np.float32(sc))) for c, l, t, r, b, sc in PN.detect(p)] for p in preds]
+            q.put(("ok", got == expect, sum(len(e) for e in expect)))
+        else:
+            q.put(("ok", None, g is None))
+    except Exception as e:  # pragma: no cover
+        q.put(("err", repr(e), None))
+    finally:
+        torch.distributed.destroy_process_group()
+
+
+@pytest.mark.parametrize("total", [6, 5])
+def test_sharded_detection_gather_gloo_world2(total):
+    """Per-rank postprocessing + packed detection gather (dist.gather_detections) gives rank 0
+    every image's detections in global order, with unequal per-rank detection counts."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_det_worker, args=(r, 2, port, total, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=180) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=60)
+    assert all(r[0] == "ok" for r in res), res
+    root = [r for r in res if r[1] is not None][0]
+    assert root[1] is True and root[2] > 10
+    other = [r for r in res if r[1] is None][0]
+    assert other[2] is True

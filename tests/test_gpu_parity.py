@@ -418,3 +418,76 @@ def test_plan_timing_api(yolo_b1):
     assert len(ms) == len(ks) == 13  # 10 layers + the conv5/6/7 split-K reduces
     assert all(c == 3 for c in cnt)
     assert all(m > 0 for m in ms)
+
+
+# ------------------------------------------------------------------ on-GPU postprocessing
+def test_postprocess_gpu_vs_reference_golden(post_golden):
+    """dnn_yolo_postprocess == the reference's postprocessing() on every fixture case
+    (yolov2tiny.py:94-234), one batched launch."""
+    import yolo_post
+    names = list(post_golden)
+    preds = np.stack([post_golden[n][0] for n in names])
+    rows = yolo_post.detect_batch(preds, raise_errors=False)
+    for name, r in zip(names, rows):
+        if isinstance(post_golden[name][1], dict):  # the reference raises ZeroDivisionError
+            assert r == -2, name
+            continue
+        got = [[b[0], list(b[1]), list(b[2])] for b in yolo_post.label_boxes(r)]
+        assert got == post_golden[name][1], name
+    # the single-image drop-in returns the reference's tuples, colors included
+    lb = yolo_post.postprocessing(post_golden["net_frame0"][0].reshape(1, 13, 13, 125))
+    assert [list(t[:1]) + [list(t[1]), list(t[2])] for t in lb] == post_golden["net_frame0"][1]
+    assert all(t[3] == yolo_post.COLORS[yolo_post.CLASSES.index(t[0])] for t in lb)
+
+
+def test_postprocess_gpu_vs_oracle_random_batch():
+    """64 seeded synthetic images in one launch vs oracle/post_numpy.py: identical boxes,
+    classes and order; scores equal up to the last bits of exp/pow."""
+    import post_numpy as PN
+    import yolo_post
+    rng = np.random.default_rng(77)
+    preds = np.stack([PN.synthetic_predictions(rng, tw_scale=(1.0 if i % 4 else 6.0)) for i in range(64)])
+    rows = yolo_post.detect_batch(preds, raise_errors=False)
+    n_total = n_err = 0
+    for p, r in zip(preds, rows):
+        try:
+            ref = PN.detect(p)
+        except ZeroDivisionError:  # the reference raises on this image: so must we
+            assert r == -2
+            n_err += 1
+            continue
+        assert [x[:5] for x in r] == [x[:5] for x in ref]
+        np.testing.assert_allclose([x[5] for x in r], [x[5] for x in ref], rtol=1e-6)
+        n_total += len(r)
+    assert n_total > 1000 and n_err < 16
+
+
+def test_postprocess_gpu_error_cases():
+    """Non-finite corners raise like the reference's int(); empty input and no detections."""
+    import yolo_post
+    p = np.zeros((2, 13, 13, 125), np.float32)
+    p.reshape(2, 845, 25)[1, 17, 2] = 100.0  # exp(100) = inf in fp32 -> int(inf) raises in the reference
+    with pytest.raises(dnn_hip.DnnHipError):
+        yolo_post.detect_batch(p)
+    assert yolo_post.detect_batch(p[:1]) == [[]]  # all-zero logits: score 0.5 * 0.05 < 0.3
+    assert yolo_post.detect_batch(np.zeros((0, 13, 13, 125), np.float32)) == []
+
+
+def test_postprocess_device_buffers_match_host_api(post_golden):
+    import torch
+    import yolo_post
+    names = list(post_golden)
+    preds = np.stack([post_golden[n][0] for n in names])
+    dev = torch.device("cuda", 0)
+    buf = yolo_post.DetectionBuffers(len(names), dev)
+    t = torch.from_numpy(preds).to(dev)
+    buf.run(t.data_ptr(), len(names), torch.cuda.current_stream(dev).cuda_stream)
+    torch.cuda.synchronize()
+    rows = yolo_post.DetectionBuffers.to_rows(buf.dets.cpu().numpy(), buf.counts.cpu().numpy(), raise_errors=False)
+    assert rows == yolo_post.detect_batch(preds, raise_errors=False)
+    # device-side packing + the (single-rank) detection gather round-trip
+    import dist as D
+    packed, total, counts = buf.pack(len(names), torch.cuda.current_stream(dev).cuda_stream)
+    d, c = D.gather_detections(packed, total, counts, len(names))
+    assert D.unpack_detections(d, c) == rows
+    assert len(d) == sum(len(r) for r in rows if not isinstance(r, int))

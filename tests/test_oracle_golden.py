@@ -124,3 +124,29 @@ def test_node_stats_vs_golden(yolo_weights):
         samp = r.reshape(-1)[idx]
         assert R.normwise_err(samp, st[f"sample_{k}"]) < TOL
         assert abs(float(np.abs(r).max()) - float(st[f"maxabs_{k}"])) <= TOL * float(st[f"maxabs_{k}"])
+
+
+def test_postprocessing_restatement_vs_reference_golden(post_golden):
+    """oracle/post_numpy.py == the reference's own postprocessing() on every fixture case
+    (dense, empty, single, ties, >64-bit IoU products, and the 4 whole-net outputs)."""
+    import post_numpy as PN
+    total = 0
+    for name, (pred, gold) in post_golden.items():
+        if isinstance(gold, dict):  # the reference raises on this input
+            with pytest.raises(ZeroDivisionError):
+                PN.postprocessing(pred)
+            continue
+        got = [[b[0], list(b[1]), list(b[2])] for b in PN.postprocessing(pred)]
+        assert got == gold, name
+        total += len(gold)
+    assert total > 400
+
+
+def test_postprocessing_restatement_edge_semantics():
+    import post_numpy as PN
+    # IoU has no clamp: two far-apart boxes with negative overlaps in x AND y get a positive
+    # "intersection" (yolov2tiny.py:186-190)
+    a, b = [0, 0, 10, 10], [100, 100, 110, 110]
+    assert PN.iou(a, b) == 7921 / float(121 + 121 - 7921)
+    # float32 threshold: a score equal to float32(0.3) is not kept (numpy compares in fp32)
+    assert not (np.float32(0.3) > np.float32(0.3)) and (float(np.float32(0.3)) > 0.3)
