@@ -51,6 +51,7 @@ def parse():
     ap.add_argument("--batch", type=int, default=64, help="frames per GPU")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="bound on the CPU-baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-latency", action="store_true", help="skip the batch-1 latency measurement")
     ap.add_argument("--kernels", action="store_true", help="add the per-kernel table to the JSON")
     ap.add_argument("--gather", choices=("detections", "outputs"), default="detections",
                     help="per step, gather post-NMS detections (on-GPU postprocessing, the north star's "
@@ -147,6 +148,55 @@ def cpu_baseline(seconds):
                     "sample": f"{n} single-frame forwards (median {med * 1e3:.0f} ms), direct conv "
                               f"{nt} pthreads (oracle/dnn_oracle.c)"}
     return res
+
+
+def latency_b1(dnn_hip, yolo_graph, ws, dev, iters=200):
+    """BASELINE.json configs[1]: one 416x416 frame, fp32, 1 GPU — issue-to-completion time of a
+    single-frame forward (frame resident in HBM), eager (13 launches) and as one HIP-graph
+    launch (dnn_plan_run_graph), median over `iters` synchronised runs."""
+    import torch
+    g1, _ = yolo_graph.build_graph(dnn_hip.DnnGraphBuilder, ws, in_shape=(1, 416, 416, 3))
+    entries = dnn_hip.lower_graph(g1)
+    wb, sb = dnn_hip.Plan.memory(1, (416, 416, 3), entries)
+    wbuf = torch.empty(wb, dtype=torch.uint8, device=dev)
+    sbuf = torch.empty(max(sb, 1), dtype=torch.uint8, device=dev)
+    p1 = dnn_hip.Plan(1, (416, 416, 3), entries, device=dev.index, weights_ptr=wbuf.data_ptr(),
+                      workspace_ptr=sbuf.data_ptr())
+    x = torch.rand((1, 416, 416, 3), device=dev)
+    y = torch.empty((1, 13, 13, 125), device=dev)
+    s = torch.cuda.Stream(dev)
+    sp = s.cuda_stream
+    out = {}
+    for mode in ("eager", "graph"):
+        run = p1.run_device if mode == "eager" else p1.run_graph
+        for _ in range(10):
+            run(1, x.data_ptr(), y.data_ptr(), sp)
+        s.synchronize()
+        t = []
+        for _ in range(iters):
+            t0 = time.perf_counter()
+            run(1, x.data_ptr(), y.data_ptr(), sp)
+            s.synchronize()
+            t.append(time.perf_counter() - t0)
+        out[mode + "_ms"] = round(sorted(t)[len(t) // 2] * 1e3, 4)
+    # device-side duration of one graph replay (HIP events on the same stream)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    with torch.cuda.stream(s):
+        e0.record(s)
+        for _ in range(50):
+            p1.run_graph(1, x.data_ptr(), y.data_ptr(), sp)
+        e1.record(s)
+    s.synchronize()
+    out["graph_device_ms"] = round(e0.elapsed_time(e1) / 50, 4)
+    out["images_per_s_graph"] = round(1e3 / out["graph_ms"], 1)
+    p1.timing_begin(20)
+    for _ in range(20):
+        p1.run_device(1, x.data_ptr(), y.data_ptr(), sp)
+    ms, cnt = p1.timing_end()
+    out["kernel_ms"] = {k["name"]: round(m / max(c, 1), 4) for k, m, c in zip(p1.kernels(), ms, cnt)}
+    out["note"] = "median issue-to-completion wall time of one synchronised single-frame forward"
+    p1.close()
+    return out
 
 
 def main():
@@ -304,6 +354,10 @@ def main():
                                   if v[0]["flops"] else None,
                                   "gbs": round(v[0]["bytes"] / (v[1] / max(v[2], 1) / 1e3) / 1e9, 1)}
                               for n, v in by_name.items()}
+
+    if rank == 0 and world == 1 and not args.no_latency:
+        res["latency_b1"] = latency_b1(dnn_hip, yolo_graph, ws, dev)
+    if rank == 0:
         res["cpu_baseline"] = None if (world > 1 or args.no_cpu) else cpu_baseline(args.cpu_seconds)
         print(json.dumps(res), flush=True)
 

@@ -79,7 +79,9 @@ enum GemmCfg : int {
   GEMM_64x128_K32 = 4,   // other N >= 128 layers: LDS-DMA 2-stage ring, MFMA 32x32x2
   GEMM_G64x32_K32 = 5,   // N <= 32 implicit conv: LDS-DMA 2-stage ring, 64x32 tile, MFMA 16x16x4
   GEMM_G256x64_K32 = 6,  // N <= 64 implicit conv: LDS-DMA 2-stage ring, 256x64 tile, 8 waves, MFMA 32x32x2
-  GEMM_NUM_CFGS = 7,
+  GEMM_G32x128_NS4 = 7,  // N >= 128, small M (batch 1): LDS-DMA 4-stage ring, 32x128 tile, MFMA 32x32x2
+  GEMM_G32x64_NS4 = 8,   // N <= 64 implicit conv, small M: LDS-DMA 4-stage ring, 32x64 tile, 2 waves
+  GEMM_NUM_CFGS = 9,
 };
 int gemm_cfg_bm(int cfg);
 int gemm_cfg_bn(int cfg);

@@ -119,7 +119,8 @@ struct CfgInfo {
   int bm, bn, bk;
 };
 static const CfgInfo kCfgs[GEMM_NUM_CFGS] = {{256, 16, 32}, {256, 32, 16}, {128, 64, 32}, {128, 128, 32},
-                                             {64, 128, 32},  {64, 32, 32},  {256, 64, 32}};
+                                             {64, 128, 32},  {64, 32, 32},  {256, 64, 32}, {32, 128, 32},
+                                             {32, 64, 32}};
 
 int gemm_cfg_bm(int cfg) { return kCfgs[cfg].bm; }
 int gemm_cfg_bn(int cfg) { return kCfgs[cfg].bn; }
@@ -140,7 +141,12 @@ int choose_gemm_cfg(long long M, int N, int K) {
   // K permutation, and the split itself depends on (N, K) only, so the summation order of an
   // output element never depends on M.
   long long t128 = ((M + 127) / 128) * ((N + 127) / 128);
-  if (K >= 2048 && t128 * choose_splitk(N, K) >= 512) return GEMM_128x128_K32;
+  const int s = choose_splitk(N, K);
+  if (K >= 2048 && t128 * s >= 512) return GEMM_128x128_K32;
+  // small M (batch 1 and the like): 64x128 would leave most CUs idle and each workgroup
+  // waiting on a 2-stage ring; 32-row tiles with a 4-stage ring (same family, same K order)
+  long long t64 = ((M + 63) / 64) * ((N + 127) / 128);
+  if (t64 * s < 256) return GEMM_G32x128_NS4;
   return GEMM_64x128_K32;
 }
 
@@ -149,7 +155,7 @@ int choose_gemm_cfg(long long M, int N, int K) {
 int choose_gemm_cfg_implicit(long long M, int N, int K) {
   if (N <= 16) return -1;
   if (N <= 32) return GEMM_G64x32_K32;
-  if (N <= 64) return GEMM_G256x64_K32;
+  if (N <= 64) return ((M + 255) / 256) < 256 ? GEMM_G32x64_NS4 : GEMM_G256x64_K32;
   return choose_gemm_cfg(M, N, K);
 }
 
@@ -189,6 +195,14 @@ static int launch_glds(int cfg, const float* A, int lda, const float* Bt, int ld
       hipLaunchKernelGGL((gemm_f32_glds_kernel<256, 64, 4, 2, 32, 2, MODE>), grid, dim3(512), 0, stream, A, lda,
                          Bt, ldb, C, ldc, m, N, Kpad, epi, tilesN, ic, sk);
       break;
+    case GEMM_G32x128_NS4:
+      hipLaunchKernelGGL((gemm_f32_glds_kernel<32, 128, 1, 4, 32, 4, MODE>), grid, dim3(256), 0, stream, A, lda,
+                         Bt, ldb, C, ldc, m, N, Kpad, epi, tilesN, ic, sk);
+      break;
+    case GEMM_G32x64_NS4:
+      hipLaunchKernelGGL((gemm_f32_glds_kernel<32, 64, 1, 2, 32, 4, MODE>), grid, dim3(128), 0, stream, A, lda,
+                         Bt, ldb, C, ldc, m, N, Kpad, epi, tilesN, ic, sk);
+      break;
     default:
       set_error("gemm: cfg %d is not an LDS-DMA config", cfg);
       return -2;
@@ -203,7 +217,7 @@ static int split_setup(int cfg, long long M, int N, int Kpad, int splits, float*
   const int tilesM = ceil_div_i(M, ci.bm);
   *tilesN = ceil_div_i(N, ci.bn);
   *grid = tilesM * *tilesN;
-  *sk = SplitK{0, 0, 0};
+  *sk = SplitK{0, *grid, 0};
   if (splits > 1) {
     if (cfg < GEMM_128x128_K32 || !slab || (Kpad / 32) % splits != 0 || N % 4 != 0) {
       set_error("gemm: split-K %d unsupported for cfg %d Kpad %d N %d", splits, cfg, Kpad, N);

@@ -121,7 +121,21 @@ struct dnn_plan {
   int ev_cap = 0, ev_used = 0;
   std::vector<hipEvent_t> ev;
   std::vector<int> ev_kernel;
+  // captured forward (dnn_plan_run_graph)
+  hipGraph_t graph = nullptr;
+  hipGraphExec_t gexec = nullptr;
+  int g_n = -1;
+  const float* g_in = nullptr;
+  float* g_out = nullptr;
 };
+
+static void drop_graph(dnn_plan* p) {
+  if (p->gexec) (void)hipGraphExecDestroy(p->gexec);
+  if (p->graph) (void)hipGraphDestroy(p->graph);
+  p->gexec = nullptr;
+  p->graph = nullptr;
+  p->g_n = -1;
+}
 
 static void layout(dnn_plan* p) {
   size_t off = 0, act = (size_t)p->in_h * p->in_w * p->in_c, col = 0, slab = 0;
@@ -198,6 +212,7 @@ int dnn_plan_create(int batch, int in_h, int in_w, int in_c, dnn_plan** out) {
 void dnn_plan_destroy(dnn_plan* p) {
   if (!p) return;
   if (p->device >= 0) (void)hipSetDevice(p->device);
+  drop_graph(p);
   for (auto e : p->ev) (void)hipEventDestroy(e);
   if (p->own_weights && p->weights) (void)hipFree(p->weights);
   if (p->own_ws && p->ws) (void)hipFree(p->ws);
@@ -510,6 +525,34 @@ int dnn_plan_run_host(dnn_plan* p, int n, const float* h_in, float* h_out) {
   int rc = dnn_plan_run(p, n, d_in, d_out, nullptr);
   if (rc) return rc;
   DNN_HIP_TRY(hipMemcpy(h_out, d_out, out_f * sizeof(float), hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int dnn_plan_run_graph(dnn_plan* p, int n, const float* d_in, float* d_out, void* stream) {
+  DNN_REQUIRE(p && p->finalized, "dnn_plan_run_graph: plan not finalized");
+  DNN_REQUIRE(stream != nullptr, "dnn_plan_run_graph: needs a created stream (NULL cannot be captured)");
+  DNN_REQUIRE(!p->timing, "dnn_plan_run_graph: per-kernel timing is active");
+  DNN_REQUIRE(n >= 0 && n <= p->batch, "dnn_plan_run_graph: n=%d outside [0, %d]", n, p->batch);
+  if (n == 0) return 0;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (!p->gexec || p->g_n != n || p->g_in != d_in || p->g_out != d_out) {
+    drop_graph(p);
+    DNN_HIP_TRY(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+    const int rc = dnn_plan_run(p, n, d_in, d_out, stream);
+    hipGraph_t g = nullptr;
+    const hipError_t e = hipStreamEndCapture(s, &g);
+    if (rc) {
+      if (e == hipSuccess && g) (void)hipGraphDestroy(g);
+      return rc;
+    }
+    DNN_HIP_TRY(e);
+    p->graph = g;
+    DNN_HIP_TRY(hipGraphInstantiate(&p->gexec, g, nullptr, nullptr, 0));
+    p->g_n = n;
+    p->g_in = d_in;
+    p->g_out = d_out;
+  }
+  DNN_HIP_TRY(hipGraphLaunch(p->gexec, s));
   return 0;
 }
 

@@ -63,6 +63,7 @@ def _bind_plan_api(lib):
         "dnn_plan_weight_buffer": (i, [vp, P(vp), P(sz)]),
         "dnn_plan_run": (i, [vp, i, vp, vp, vp]),
         "dnn_plan_run_host": (i, [vp, i, vp, vp]),
+        "dnn_plan_run_graph": (i, [vp, i, vp, vp, vp]),
         "dnn_plan_num_kernels": (i, [vp]),
         "dnn_plan_kernel_info": (i, [vp, i, ctypes.c_char_p, i, P(ctypes.c_double), P(ctypes.c_double)]),
         "dnn_plan_timing_begin": (i, [vp, i]),
@@ -583,6 +584,12 @@ class Plan(object):
         _check(self.lib.dnn_plan_run(self.h, int(n), ctypes.c_void_p(in_ptr), ctypes.c_void_p(out_ptr),
                                      ctypes.c_void_p(stream_ptr) if stream_ptr else None),
                "dnn_plan_run", self.lib)
+
+    def run_graph(self, n, in_ptr, out_ptr, stream_ptr):
+        """run_device through a captured HIP graph (dnn_plan_run_graph): one submission per
+        forward after the first call for these (n, in, out)."""
+        _check(self.lib.dnn_plan_run_graph(self.h, int(n), ctypes.c_void_p(in_ptr), ctypes.c_void_p(out_ptr),
+                                           ctypes.c_void_p(stream_ptr)), "dnn_plan_run_graph", self.lib)
 
     def kernels(self):
         out = []

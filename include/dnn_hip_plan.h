@@ -53,10 +53,11 @@ int dnn_plan_output_shape(const dnn_plan* plan, int* batch, int* h, int* w, int*
 
 /* Human-readable lowering, one line per plan entry: shapes, execution mode (gemm =
  * explicit im2col + GEMM, direct_a = 1x1 GEMM on the input, implicit = implicit GEMM,
- * direct = direct conv), GEMM config and whether a 2x2/s2 max pool is fused.  A 2x2/s2
- * MaxPool2D directly after an implicit or direct conv is folded into it; set DNN_HIP_FUSE=0
- * in the environment before dnn_plan_create to keep every conv explicit and every pool
- * separate. */
+ * direct = direct conv, patch = LDS-patch MFMA conv), GEMM config, whether a 2x2/s2 max
+ * pool is fused and whether the GEMM is split along K (splitK=3: partials + an ordered
+ * reduce/epilogue kernel).  A 2x2/s2 MaxPool2D directly after an implicit, patch or direct
+ * conv is folded into it; set DNN_HIP_FUSE=0 in the environment before dnn_plan_create to
+ * keep every conv explicit and every pool separate (DNN_HIP_PATCH=0: no patch mode). */
 int dnn_plan_describe(const dnn_plan* plan, char* buf, int buf_len);
 
 /* Device bytes the plan needs: packed weights + epilogue params, and workspace
@@ -77,6 +78,13 @@ int dnn_plan_run(dnn_plan* plan, int n, const float* d_in, float* d_out, void* s
 
 /* Host-pointer convenience: H2D copy, run, D2H copy, synchronise. */
 int dnn_plan_run_host(dnn_plan* plan, int n, const float* h_in, float* h_out);
+
+/* dnn_plan_run through a HIP graph: the first call for a given (n, d_in, d_out) captures the
+ * plan's kernel sequence on `stream` (hipStreamBeginCapture) and instantiates it; every call
+ * then submits the whole forward with one hipGraphLaunch — the launch-bound batch-1 case.
+ * A different (n, d_in, d_out) re-captures.  `stream` must be a created stream (the NULL
+ * stream cannot be captured); per-kernel timing must be off. */
+int dnn_plan_run_graph(dnn_plan* plan, int n, const float* d_in, float* d_out, void* stream);
 
 /* Per-kernel timing with HIP events recorded on the run stream.
  * begin: allocate events for up to max_runs runs and start recording;

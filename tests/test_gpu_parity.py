@@ -491,3 +491,27 @@ def test_postprocess_device_buffers_match_host_api(post_golden):
     d, c = D.gather_detections(packed, total, counts, len(names))
     assert D.unpack_detections(d, c) == rows
     assert len(d) == sum(len(r) for r in rows if not isinstance(r, int))
+
+
+def test_plan_graph_replay_matches_eager(yolo_b1):
+    """dnn_plan_run_graph (captured HIP graph) == dnn_plan_run, re-captures on new buffers."""
+    import torch
+    plan = yolo_b1.plan()
+    dev = torch.device("cuda", 0)
+    s = torch.cuda.Stream(dev)
+    x = torch.from_numpy(synth.frame(2)).to(dev)
+    y_e = torch.empty((1, 13, 13, 125), device=dev)
+    y_g = torch.empty_like(y_e)
+    plan.run_device(1, x.data_ptr(), y_e.data_ptr(), s.cuda_stream)
+    for _ in range(3):
+        plan.run_graph(1, x.data_ptr(), y_g.data_ptr(), s.cuda_stream)
+    s.synchronize()
+    assert torch.equal(y_e, y_g)
+    x2 = torch.from_numpy(synth.frame(3)).to(dev)
+    y2 = torch.empty_like(y_e)
+    plan.run_graph(1, x2.data_ptr(), y2.data_ptr(), s.cuda_stream)
+    plan.run_device(1, x2.data_ptr(), y_e.data_ptr(), s.cuda_stream)
+    s.synchronize()
+    assert torch.equal(y_e, y2)
+    with pytest.raises(dnn_hip.DnnHipError):
+        plan.run_graph(1, x.data_ptr(), y_g.data_ptr(), 0)  # the NULL stream cannot be captured
