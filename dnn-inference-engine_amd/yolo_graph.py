@@ -6,8 +6,9 @@ MaxPool2D (five 2x2/s2 SAME, then one 2x2/s1 SAME after the 6th conv).  It works
 module exposing the reference's DnnGraphBuilder API (dnn_hip, or the reference's own
 wrappers), taking the weight list in the pickle's format
 (proj3/yolov2tiny.py:30-77: dicts with kernel / biases / moving_mean / moving_variance /
-gamma).  The reference's `get_y2t_w` pickle loader is out of scope (its version gate
-rejects Python 3.10, proj3/yolov2tiny.py:17-22, and the pickle is not in the repo).
+gamma).  The pickle itself is read by yolo_weights.load_y2t_weights (the reference's
+get_y2t_w rejects Python 3.10, proj3/yolov2tiny.py:17-22) and the reference's model class is
+mirrored by yolov2tiny.YOLO_V2_TINY.
 """
 import numpy as np
 

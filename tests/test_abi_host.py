@@ -190,3 +190,44 @@ def test_postprocess_api_host_checks():
     # argument validation happens before any GPU call
     assert dnn_hip.mylib.dnn_yolo_postprocess_host(None, -1, None, 0, None) != 0
     assert "bad arguments" in dnn_hip.last_error()
+
+
+def test_weight_pickle_round_trip_and_safety(tmp_path):
+    import pickle
+    import yolo_weights as YW
+    ws = synth.yolo_weights()
+    p = tmp_path / "y2t_weights.pickle"
+    YW.save_y2t_weights(ws, p)
+    back = YW.load_y2t_weights(p)
+    assert len(back) == 9
+    for a, b in zip(ws, back):
+        for k in a:
+            assert b[k].dtype == np.float32 and np.array_equal(a[k], b[k])
+    # protocol 0 / 4 writers and float64 arrays load too (converted to fp32)
+    for proto in (0, 4):
+        q = tmp_path / f"w{proto}.pickle"
+        with open(q, "wb") as f:
+            pickle.dump([{k: v.astype(np.float64) for k, v in d.items()} for d in ws], f, protocol=proto)
+        assert all(np.array_equal(x["kernel"], y["kernel"]) for x, y in zip(ws, YW.load_y2t_weights(q)))
+
+    # a pickle that would run code is refused before anything executes
+    class Evil(object):
+        def __reduce__(self):
+            return (os.system, ("touch " + str(tmp_path / "pwned"),))
+    e = tmp_path / "evil.pickle"
+    with open(e, "wb") as f:
+        pickle.dump([Evil()], f, protocol=2)
+    with pytest.raises(YW.WeightFileError):
+        YW.load_y2t_weights(e)
+    assert not (tmp_path / "pwned").exists()
+    # structure checks
+    with pytest.raises(YW.WeightFileError):
+        YW.validate(ws[:8])
+    bad = [dict(d) for d in ws]
+    bad[3] = dict(bad[3], kernel=np.zeros((3, 3, 7, 256), np.float32))
+    with pytest.raises(YW.WeightFileError):
+        YW.validate(bad)
+    bad = [dict(d) for d in ws]
+    del bad[2]["gamma"]
+    with pytest.raises(YW.WeightFileError):
+        YW.validate(bad)

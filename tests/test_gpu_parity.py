@@ -515,3 +515,22 @@ def test_plan_graph_replay_matches_eager(yolo_b1):
     assert torch.equal(y_e, y2)
     with pytest.raises(dnn_hip.DnnHipError):
         plan.run_graph(1, x.data_ptr(), y_g.data_ptr(), 0)  # the NULL stream cannot be captured
+
+
+def test_yolov2tiny_front_end_from_pickle(tmp_path, yolo_weights, golden_frames, post_golden):
+    """The reference's model API (YOLO_V2_TINY(in_shape, weight_pickle, debug).inference +
+    postprocessing) on our engine, weights read from a pickle by the safe loader."""
+    import yolo_weights as YW
+    import yolov2tiny
+    p = tmp_path / "y2t_weights.pickle"
+    YW.save_y2t_weights(yolo_weights, p)
+    y2t = yolov2tiny.YOLO_V2_TINY([1, 416, 416, 3], str(p), False)
+    out = y2t.inference(synth.frame(0))
+    assert R.normwise_err(out, golden_frames[0]) < NET_TOL
+    boxes = yolov2tiny.postprocessing(np.squeeze(out))
+    import post_numpy as PN
+    assert boxes == PN.postprocessing(np.squeeze(out))  # same tensor: exact
+    # vs the reference's detections on ITS output (1e-6-level differences in the raw tensor
+    # can move a truncated corner of a huge box by one pixel)
+    gold = post_golden["net_frame0"][1]
+    assert [b[0] for b in boxes] == [g[0] for g in gold]
