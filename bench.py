@@ -39,6 +39,7 @@ ORACLE = os.path.join(REPO, "oracle")
 sys.path.insert(0, PKG)
 
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md, dense fp32 matrix (= vector) peak
+FP16_MFMA_PEAK_TFLOPS = 16 * FP32_MFMA_PEAK_TFLOPS  # dense F16 MFMA (MI355X_MICROARCH.md: fp32 = 1/16 of it)
 HBM_PEAK_GBS = 8000.0
 DOMINANT = "conv7.gemm"
 
@@ -52,6 +53,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="bound on the CPU-baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-latency", action="store_true", help="skip the batch-1 latency measurement")
+    ap.add_argument("--precision", choices=("fp32", "fp16"), default="fp32",
+                    help="conv path precision (fp16 = BASELINE config 5: fp16 MFMA, fp32 accumulate)")
+    ap.add_argument("--no-fp16", action="store_true", help="skip the embedded fp16 (config 5) measurement")
     ap.add_argument("--kernels", action="store_true", help="add the per-kernel table to the JSON")
     ap.add_argument("--gather", choices=("detections", "outputs"), default="detections",
                     help="per step, gather post-NMS detections (on-GPU postprocessing, the north star's "
@@ -199,6 +203,49 @@ def latency_b1(dnn_hip, yolo_graph, ws, dev, iters=200):
     return out
 
 
+def fp16_config(dnn_hip, yolo_graph, ws, dev, frames, out32, plan32, stream, B, steps=20):
+    """BASELINE config 5 beside the fp32 line: the same 64 frames through an fp16 plan (fp16
+    MFMA, fp32 accumulate/epilogue): forward img/s (HIP events on the run stream), per-kernel
+    times, and the normwise error of its predictions vs the fp32 plan's on the same frames."""
+    import torch
+    g, _ = yolo_graph.build_graph(dnn_hip.DnnGraphBuilder, ws, in_shape=(B, 416, 416, 3))
+    entries = dnn_hip.lower_graph(g)
+    wb, sb = dnn_hip.Plan.memory(B, (416, 416, 3), entries, precision="fp16")
+    wbuf = torch.empty(wb, dtype=torch.uint8, device=dev)
+    sbuf = torch.empty(max(sb, 1), dtype=torch.uint8, device=dev)
+    p16 = dnn_hip.Plan(B, (416, 416, 3), entries, device=dev.index, weights_ptr=wbuf.data_ptr(),
+                       workspace_ptr=sbuf.data_ptr(), precision="fp16")
+    y16 = torch.empty((B, 13, 13, 125), device=dev)
+    for _ in range(3):
+        p16.run_device(B, frames.data_ptr(), y16.data_ptr(), stream)
+    plan32.run_device(B, frames.data_ptr(), out32.data_ptr(), stream)
+    torch.cuda.synchronize()
+    err = float((y16 - out32[:B]).abs().max() / out32[:B].abs().max())
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(steps):
+        p16.run_device(B, frames.data_ptr(), y16.data_ptr(), stream)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / steps
+    p16.timing_begin(5)
+    for _ in range(5):
+        p16.run_device(B, frames.data_ptr(), y16.data_ptr(), stream)
+    kms, cnt = p16.timing_end()
+    kinfo = p16.kernels()
+    ker = {k["name"]: round(m / max(c, 1), 4) for k, m, c in zip(kinfo, kms, cnt)}
+    c7 = [(k, m / max(c, 1)) for k, m, c in zip(kinfo, kms, cnt) if k["name"] == "conv7.gemm"]
+    out = {"value": round(B / (ms / 1e3), 2), "unit": "images/s", "ms_per_forward": round(ms, 4),
+           "dtype": "fp16 (fp32 accumulate + epilogue)", "normwise_err_vs_fp32": err,
+           "net_pct_fp16_peak": round(100 * 6.971e9 * B / (ms / 1e3) / 1e12 / FP16_MFMA_PEAK_TFLOPS, 2),
+           "kernels_ms": ker, "note": "forward only (no postprocess/gather), same frames as the fp32 line"}
+    if c7:
+        k, m = c7[0]
+        out["conv7_tflops"] = round(k["flops"] / (m / 1e3) / 1e12, 1)
+    p16.close()
+    return out
+
+
 def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -225,11 +272,11 @@ def main():
     ws = synth.yolo_weights() if rank == 0 else yolo_graph.zero_weights_like(synth.yolo_weights())
     g, _ = yolo_graph.build_graph(dnn_hip.DnnGraphBuilder, ws, in_shape=(B, 416, 416, 3))
     entries = dnn_hip.lower_graph(g)
-    wbytes, sbytes = dnn_hip.Plan.memory(B, (416, 416, 3), entries)
+    wbytes, sbytes = dnn_hip.Plan.memory(B, (416, 416, 3), entries, precision=args.precision)
     wbuf = torch.empty(wbytes, dtype=torch.uint8, device=dev)
     sbuf = torch.empty(max(sbytes, 1), dtype=torch.uint8, device=dev)
     plan = dnn_hip.Plan(B, (416, 416, 3), entries, device=local_rank, weights_ptr=wbuf.data_ptr(),
-                        workspace_ptr=sbuf.data_ptr(), upload=(rank == 0))
+                        workspace_ptr=sbuf.data_ptr(), upload=(rank == 0), precision=args.precision)
     torch.cuda.synchronize()
     D.broadcast_weights(wbuf, src=0)
     torch.cuda.synchronize()
@@ -325,7 +372,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "fp32",
+            "dtype": args.precision,
             "data": "synthetic (uniform [0,1) frames, random-init weights, tiny-yolo-voc channel plan)",
             "config": {"workload": "YOLOv2-tiny forward, 416x416x3 NHWC fp32, 64 frames per GPU in HBM, "
                                    + ("on-GPU postprocessing (decode, 0.3 threshold, sort, NMS), post-NMS "
@@ -357,6 +404,8 @@ def main():
 
     if rank == 0 and world == 1 and not args.no_latency:
         res["latency_b1"] = latency_b1(dnn_hip, yolo_graph, ws, dev)
+    if rank == 0 and world == 1 and args.precision == "fp32" and not args.no_fp16:
+        res["fp16"] = fp16_config(dnn_hip, yolo_graph, ws, dev, frames, runner.out, plan, stream, B)
     if rank == 0:
         res["cpu_baseline"] = None if (world > 1 or args.no_cpu) else cpu_baseline(args.cpu_seconds)
         print(json.dumps(res), flush=True)

@@ -22,9 +22,9 @@ namespace dnnhip {
 
 constexpr int DC_T = 16;  // pooled outputs per block edge (16 x 16 threads)
 
-template <int CIN, int NOUT>
+template <int CIN, int NOUT, typename OutT>
 __global__ void __launch_bounds__(256)
-conv3x3_pool2_direct_kernel(const float* __restrict__ in, const float* __restrict__ w, float* __restrict__ out,
+conv3x3_pool2_direct_kernel(const float* __restrict__ in, const float* __restrict__ w, OutT* __restrict__ out,
                             DirectGeom g, EpiParams epi) {
   constexpr int PR = 2 * DC_T + 2, PC = 2 * DC_T + 2;  // input patch rows / cols
   constexpr int RS = PC * CIN + ((PC * CIN) % 2 == 0 ? 1 : 0);  // odd row stride: conflict-free reads
@@ -88,10 +88,21 @@ conv3x3_pool2_direct_kernel(const float* __restrict__ in, const float* __restric
     pooled[o] = pool_then_epilogue(v, pb, pm, ps, pg, epi.flags);
   }
   if (py < g.PH && px < g.PW) {
-    float* dst = out + (((size_t)b * g.PH + py) * g.PW + px) * NOUT;
+    OutT* dst = out + (((size_t)b * g.PH + py) * g.PW + px) * NOUT;
+    if constexpr (sizeof(OutT) == 4) {
 #pragma unroll
-    for (int o = 0; o < NOUT; o += 4)
-      *reinterpret_cast<float4*>(dst + o) = make_float4(pooled[o], pooled[o + 1], pooled[o + 2], pooled[o + 3]);
+      for (int o = 0; o < NOUT; o += 4)
+        *reinterpret_cast<float4*>(dst + o) = make_float4(pooled[o], pooled[o + 1], pooled[o + 2], pooled[o + 3]);
+    } else {  // fp16 activations (fp16 path): 8 channels per 16-byte store
+      typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+#pragma unroll
+      for (int o = 0; o < NOUT; o += 8) {
+        h8 v;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = (half_t)pooled[o + e];
+        *reinterpret_cast<h8*>(dst + o) = v;
+      }
+    }
   }
 }
 
@@ -99,8 +110,9 @@ bool direct_conv_pool_supported(int cin, int nout, int kh, int kw, int sh, int s
   return kh == 3 && kw == 3 && sh == 1 && sw == 1 && cin >= 1 && cin <= 4 && nout == 16;
 }
 
-int launch_conv3x3_pool2_direct(const float* in, const float* w, float* out, const DirectGeom& g, int cin, int nout,
-                                const EpiParams& epi, hipStream_t stream) {
+template <typename OutT>
+static int launch_direct(const float* in, const float* w, OutT* out, const DirectGeom& g, int cin, int nout,
+                         const EpiParams& epi, hipStream_t stream) {
   if (g.B == 0) return 0;
   if (nout != 16 || cin < 1 || cin > 4) {
     set_error("direct conv: unsupported cin=%d nout=%d", cin, nout);
@@ -109,16 +121,16 @@ int launch_conv3x3_pool2_direct(const float* in, const float* w, float* out, con
   dim3 grid((g.PW + DC_T - 1) / DC_T, (g.PH + DC_T - 1) / DC_T, g.B);
   switch (cin) {
     case 1:
-      hipLaunchKernelGGL((conv3x3_pool2_direct_kernel<1, 16>), grid, dim3(256), 0, stream, in, w, out, g, epi);
+      hipLaunchKernelGGL((conv3x3_pool2_direct_kernel<1, 16, OutT>), grid, dim3(256), 0, stream, in, w, out, g, epi);
       break;
     case 2:
-      hipLaunchKernelGGL((conv3x3_pool2_direct_kernel<2, 16>), grid, dim3(256), 0, stream, in, w, out, g, epi);
+      hipLaunchKernelGGL((conv3x3_pool2_direct_kernel<2, 16, OutT>), grid, dim3(256), 0, stream, in, w, out, g, epi);
       break;
     case 3:
-      hipLaunchKernelGGL((conv3x3_pool2_direct_kernel<3, 16>), grid, dim3(256), 0, stream, in, w, out, g, epi);
+      hipLaunchKernelGGL((conv3x3_pool2_direct_kernel<3, 16, OutT>), grid, dim3(256), 0, stream, in, w, out, g, epi);
       break;
     case 4:
-      hipLaunchKernelGGL((conv3x3_pool2_direct_kernel<4, 16>), grid, dim3(256), 0, stream, in, w, out, g, epi);
+      hipLaunchKernelGGL((conv3x3_pool2_direct_kernel<4, 16, OutT>), grid, dim3(256), 0, stream, in, w, out, g, epi);
       break;
   }
   hipError_t e = hipGetLastError();
@@ -127,6 +139,16 @@ int launch_conv3x3_pool2_direct(const float* in, const float* w, float* out, con
     return -1;
   }
   return 0;
+}
+
+int launch_conv3x3_pool2_direct(const float* in, const float* w, float* out, const DirectGeom& g, int cin, int nout,
+                                const EpiParams& epi, hipStream_t stream) {
+  return launch_direct<float>(in, w, out, g, cin, nout, epi, stream);
+}
+
+int launch_conv3x3_pool2_direct_f16out(const float* in, const float* w, half_t* out, const DirectGeom& g, int cin,
+                                       int nout, const EpiParams& epi, hipStream_t stream) {
+  return launch_direct<half_t>(in, w, out, g, cin, nout, epi, stream);
 }
 
 }  // namespace dnnhip

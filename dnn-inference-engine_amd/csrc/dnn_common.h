@@ -147,6 +147,36 @@ int patch_conv_kpad(int C);
 int launch_conv3x3_patch_pool(const float* in, const float* Bt, int ldb, float* out, const DirectGeom& g, int C,
                               int N, const float* zero, const EpiParams& epi, hipStream_t stream);
 
+// ---------------------------------------------------------------- fp16 path (kernels_f16.hip)
+// fp16 activations / weights, v_mfma_f32_32x32x16_f16 with fp32 accumulate and epilogue.
+typedef _Float16 half_t;
+enum Gemm16Cfg : int {
+  GEMM16_128x128 = 0,     // long-K wide layers with split-K (conv5-7 at batch 64)
+  GEMM16_64x128 = 1,      // other N >= 128
+  GEMM16_32x128_NS4 = 2,  // N >= 128, small M: 4-stage ring
+  GEMM16_128x64 = 3,      // N <= 64
+  GEMM16_32x64_NS4 = 4,   // N <= 64, small M
+  GEMM16_128x32 = 5,      // N <= 32
+  GEMM16_32x32_NS4 = 6,   // N <= 32, small M
+  GEMM16_NUM_CFGS = 7,
+};
+int choose_gemm16_cfg(long long M, int N, int K);
+int choose_splitk16(int N, int K);
+int gemm16_cfg_bn(int cfg);
+// mode: GEMM_DENSE (A = [M][lda] fp16), GEMM_IMPLICIT / GEMM_IMPLICIT_POOL (A = NHWC fp16 input
+// described by ic; C % 8 == 0).  Kpad % 64 == 0; C is fp16 [M][ldc]; split-K partials in slab.
+int launch_gemm16(int cfg, int mode, const half_t* A, int lda, const ImplicitConv& ic, const half_t* Bt, int ldb,
+                  half_t* C, int ldc, long long M, int N, int Kpad, const EpiParams& epi, hipStream_t stream,
+                  int splits = 1, float* slab = nullptr);
+int launch_splitk_reduce16(const float* slab, int splits, long long M, int N, half_t* C, int ldc,
+                           const EpiParams& epi, hipStream_t stream);
+int launch_f32_to_f16(const float* in, half_t* out, long long n, hipStream_t s);
+int launch_f16_to_f32(const half_t* in, float* out, long long n, hipStream_t s);
+int launch_maxpool16(const half_t* in, half_t* out, const PoolGeom& g, hipStream_t s);
+// conv0 direct kernel with an fp16 output (fp32 input frames)
+int launch_conv3x3_pool2_direct_f16out(const float* in, const float* w, half_t* out, const DirectGeom& g, int cin,
+                                       int nout, const EpiParams& epi, hipStream_t stream);
+
 // element-wise ops of the per-op ABI
 int launch_bias_add(const float* in, const float* b, float* out, long long n, int C, hipStream_t s);
 int launch_bn_mvg(const float* in, const float* mean, const float* sq, const float* gamma, float* out,

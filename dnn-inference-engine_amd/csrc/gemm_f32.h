@@ -24,6 +24,11 @@ namespace dnnhip {
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
+typedef _Float16 half_t;
+// store conversion of the fp32 epilogue result: identity, or round-to-nearest-even to fp16
+__device__ __forceinline__ void store_out(float* p, float v) { *p = v; }
+__device__ __forceinline__ void store_out(half_t* p, float v) { *p = (half_t)v; }
+
 __device__ __forceinline__ float apply_epilogue(float v, float bias, float mean, float sq, float gamma,
                                                 int flags) {
   if (flags & EPI_BIAS) v = v + bias;
@@ -82,8 +87,8 @@ __device__ __forceinline__ int xcd_tile(int bid, int nb) {
 }
 
 // Fused epilogue + store of one wave's accumulators (NHWC: row = pixel, col = channel).
-template <int MF, int TM, int TN, int WTM, int WTN>
-__device__ __forceinline__ void store_tile(const typename Mfma<MF>::acc_t (&acc)[TM][TN], float* __restrict__ C,
+template <int MF, int TM, int TN, int WTM, int WTN, typename OutT = float>
+__device__ __forceinline__ void store_tile(const typename Mfma<MF>::acc_t (&acc)[TM][TN], OutT* __restrict__ C,
                                            int ldc, int M, int N, int m0, int n0, int wm, int wn, int lane,
                                            const EpiParams& epi) {
   typedef Mfma<MF> MM;
@@ -101,7 +106,7 @@ __device__ __forceinline__ void store_tile(const typename Mfma<MF>::acc_t (&acc)
 #pragma unroll
         for (int r = 0; r < MM::REGS; ++r) {
           const int m = m0 + wm * WTM + i * MF + MM::out_row(lane, r);
-          if (m < M) C[(size_t)m * ldc + n] = apply_epilogue(acc[i][j][r], pb, pm, ps, pg, epi.flags);
+          if (m < M) store_out(C + (size_t)m * ldc + n, apply_epilogue(acc[i][j][r], pb, pm, ps, pg, epi.flags));
         }
       }
     }
@@ -268,9 +273,9 @@ __device__ __forceinline__ float pool_then_epilogue(f32x4 v, float pb, float pm,
 // lane (32x32x2: regs 4q..4q+3 = rows 8q+4h+0..3; 16x16x4: regs 0..3 = rows 4(l>>4)+0..3).
 // Window cells past the conv output (odd OH/OW: the SAME pool's padding, -FLT_MAX in the
 // reference) are left out by repeating cell (0,0), which always exists.
-template <int MF, int TM, int TN, int WTM, int WTN>
+template <int MF, int TM, int TN, int WTM, int WTN, typename OutT = float>
 __device__ __forceinline__ void store_tile_pool(const typename Mfma<MF>::acc_t (&acc)[TM][TN],
-                                                float* __restrict__ C, int ldc, int M, int N, int m0, int n0,
+                                                OutT* __restrict__ C, int ldc, int M, int N, int m0, int n0,
                                                 int wm, int wn, int lane, const EpiParams& epi,
                                                 const ImplicitConv& ic) {
   typedef Mfma<MF> MM;
@@ -299,7 +304,7 @@ __device__ __forceinline__ void store_tile_pool(const typename Mfma<MF>::acc_t (
           if (!y1) v[2] = v[0];
           if (!(x1 && y1)) v[3] = v[0];
         }
-        C[(size_t)win * ldc + n] = pool_then_epilogue(v, pb, pm, ps, pg, epi.flags);
+        store_out(C + (size_t)win * ldc + n, pool_then_epilogue(v, pb, pm, ps, pg, epi.flags));
       }
     }
   }
@@ -320,8 +325,9 @@ struct SplitK {
 // Thread layout (no per-element index division): a block row of nqb threads covers channel
 // quads q0, q0 + nqb, ... (epilogue parameters loaded once per quad); the block's rp rows
 // stride over M.
+template <typename OutT>
 static __global__ void __launch_bounds__(256) __attribute__((unused))
-splitk_reduce_kernel(const float* __restrict__ part, int splits, long long slab, float* __restrict__ C, int M,
+splitk_reduce_kernel(const float* __restrict__ part, int splits, long long slab, OutT* __restrict__ C, int M,
                      int N, int ldc, EpiParams epi, int nqb, int rp) {
   const int nq = N >> 2;  // N % 4 == 0 (checked by the launcher)
   const int q0 = threadIdx.x % nqb, r = threadIdx.x / nqb;
@@ -342,7 +348,12 @@ splitk_reduce_kernel(const float* __restrict__ part, int splits, long long slab,
       f32x4 o;
 #pragma unroll
       for (int e = 0; e < 4; ++e) o[e] = apply_epilogue(v[e], pb[e], pm[e], ps[e], pg[e], epi.flags);
-      *reinterpret_cast<f32x4*>(C + (size_t)m * ldc + n) = o;
+      if constexpr (sizeof(OutT) == 4) {
+        *reinterpret_cast<f32x4*>(C + (size_t)m * ldc + n) = o;
+      } else {  // 4 fp16 = one 8-byte store
+        typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+        *reinterpret_cast<h4*>(C + (size_t)m * ldc + n) = h4{(half_t)o[0], (half_t)o[1], (half_t)o[2], (half_t)o[3]};
+      }
     }
   }
 }

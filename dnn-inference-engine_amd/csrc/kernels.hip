@@ -306,7 +306,7 @@ int launch_splitk_reduce(const float* slab, int splits, long long M, int N, floa
   const int nq = N / 4, nqb = nq < 256 ? nq : 256, rp = 256 / nqb;
   long long blocks = (M + rp - 1) / rp;
   if (blocks > 2048) blocks = 2048;
-  hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, slab, splits,
+  hipLaunchKernelGGL(splitk_reduce_kernel<float>, dim3((unsigned)blocks), dim3(256), 0, stream, slab, splits,
                      M * (long long)N, C, (int)M, N, ldc, epi, nqb, rp);
   return check_launch("splitk_reduce");
 }

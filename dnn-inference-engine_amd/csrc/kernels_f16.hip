@@ -1,0 +1,194 @@
+// fp16 conv path (BASELINE config 5): launchers for the fp16 MFMA GEMM (gemm_f16.h) and the
+// small fp16 kernels around it (weight / activation conversion, 2x2 max pool, split-K
+// reduce).  Activations are NHWC fp16 between layers, accumulation and epilogue fp32.
+#include <hip/hip_runtime.h>
+#include <cfloat>
+#include "dnn_common.h"
+#include "gemm_f16.h"
+
+namespace dnnhip {
+
+static int check16(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    set_error("launch %s: %s", what, hipGetErrorString(e));
+    return -1;
+  }
+  return 0;
+}
+
+struct Cfg16Info {
+  int bm, bn;
+};
+static const Cfg16Info kCfg16[GEMM16_NUM_CFGS] = {{128, 128}, {64, 128}, {32, 128}, {128, 64},
+                                                  {32, 64},   {128, 32}, {32, 32}};
+int gemm16_cfg_bn(int cfg) { return kCfg16[cfg].bn; }
+
+// Same rules as the fp32 chooser (kernels.hip): every config is the 32x32x16 f16 family with
+// BK = 64, and the split depends on (N, K) only, so results do not depend on M.
+int choose_splitk16(int N, int K) {
+  if (N >= 512 && N % 4 == 0 && K >= 2048 && (K / 64) % 3 == 0) return 3;
+  return 1;
+}
+
+int choose_gemm16_cfg(long long M, int N, int K) {
+  if (N <= 32) return ((M + 127) / 128) < 256 ? GEMM16_32x32_NS4 : GEMM16_128x32;
+  if (N <= 64) return ((M + 127) / 128) < 256 ? GEMM16_32x64_NS4 : GEMM16_128x64;
+  const int s = choose_splitk16(N, K);
+  const long long t128 = ((M + 127) / 128) * ((N + 127) / 128);
+  if (K >= 2048 && t128 * s >= 512) return GEMM16_128x128;
+  const long long t64 = ((M + 63) / 64) * ((N + 127) / 128);
+  if (t64 * s < 256) return GEMM16_32x128_NS4;
+  return GEMM16_64x128;
+}
+
+template <int MODE>
+static int launch16(int cfg, const half_t* A, int lda, const half_t* Bt, int ldb, half_t* C, float* slab, int ldc,
+                    int M, int N, int Kpad, const EpiParams& epi, int tilesN, const ImplicitConv& ic,
+                    const SplitK& sk, dim3 grid, hipStream_t st) {
+#define DNN_L16(BM_, BN_, WM_, WN_, NS_)                                                                     \
+  hipLaunchKernelGGL((gemm_f16_glds_kernel<BM_, BN_, WM_, WN_, NS_, MODE, half_t>), grid, dim3(WM_ * WN_ * 64), \
+                     0, st, A, lda, Bt, ldb, C, slab, ldc, M, N, Kpad, epi, tilesN, ic, sk)
+  switch (cfg) {
+    case GEMM16_128x128: DNN_L16(128, 128, 2, 2, 2); break;
+    case GEMM16_64x128: DNN_L16(64, 128, 2, 2, 2); break;
+    case GEMM16_32x128_NS4: DNN_L16(32, 128, 1, 4, 4); break;
+    case GEMM16_128x64: DNN_L16(128, 64, 4, 1, 2); break;
+    case GEMM16_32x64_NS4: DNN_L16(32, 64, 1, 2, 4); break;
+    case GEMM16_128x32: DNN_L16(128, 32, 4, 1, 2); break;
+    case GEMM16_32x32_NS4: DNN_L16(32, 32, 1, 1, 4); break;
+    default:
+      set_error("gemm16: bad cfg %d", cfg);
+      return -2;
+  }
+#undef DNN_L16
+  return check16("gemm_f16");
+}
+
+int launch_gemm16(int cfg, int mode, const half_t* A, int lda, const ImplicitConv& ic, const half_t* Bt, int ldb,
+                  half_t* C, int ldc, long long M, int N, int Kpad, const EpiParams& epi, hipStream_t stream,
+                  int splits, float* slab) {
+  if (M == 0 || N == 0) return 0;
+  if (cfg < 0 || cfg >= GEMM16_NUM_CFGS || mode < GEMM_DENSE || mode > GEMM_IMPLICIT_POOL) {
+    set_error("gemm16: bad cfg %d / mode %d", cfg, mode);
+    return -2;
+  }
+  const Cfg16Info ci = kCfg16[cfg];
+  if (Kpad % 64 != 0 || ldb % 8 != 0 || M > 0x7fffffffLL || (mode == GEMM_DENSE && lda % 8 != 0) ||
+      (mode != GEMM_DENSE && (ic.C % 8 != 0 || ic.kh * ic.kw > 30 || !ic.zero)) ||
+      (mode == GEMM_IMPLICIT_POOL && (M % 4 != 0 || splits > 1))) {
+    set_error("gemm16: unsupported shape M=%lld N=%d Kpad=%d mode=%d C=%d splits=%d", M, N, Kpad, mode, ic.C, splits);
+    return -2;
+  }
+  const int tilesM = (int)((M + ci.bm - 1) / ci.bm), tilesN = (N + ci.bn - 1) / ci.bn;
+  int grid = tilesM * tilesN;
+  SplitK sk{0, grid, 0};
+  if (splits > 1) {
+    if (!slab || (Kpad / 64) % splits != 0 || N % 4 != 0) {
+      set_error("gemm16: split-K %d unsupported (Kpad %d, N %d)", splits, Kpad, N);
+      return -2;
+    }
+    sk = SplitK{Kpad / 64 / splits, grid, M * (long long)N};
+    grid *= splits;
+  }
+  switch (mode) {
+    case GEMM_DENSE:
+      return launch16<GEMM_DENSE>(cfg, A, lda, Bt, ldb, C, slab, ldc, (int)M, N, Kpad, epi, tilesN, ic, sk,
+                                  dim3(grid), stream);
+    case GEMM_IMPLICIT:
+      return launch16<GEMM_IMPLICIT>(cfg, A, lda, Bt, ldb, C, slab, ldc, (int)M, N, Kpad, epi, tilesN, ic, sk,
+                                     dim3(grid), stream);
+    default:
+      return launch16<GEMM_IMPLICIT_POOL>(cfg, A, lda, Bt, ldb, C, slab, ldc, (int)M, N, Kpad, epi, tilesN, ic,
+                                          sk, dim3(grid), stream);
+  }
+}
+
+int launch_splitk_reduce16(const float* slab, int splits, long long M, int N, half_t* C, int ldc,
+                           const EpiParams& epi, hipStream_t stream) {
+  if (M == 0 || N == 0) return 0;
+  if (N % 4 != 0 || ldc % 4 != 0 || M > 0x7fffffffLL) {
+    set_error("splitk_reduce16: unsupported N %d / ldc %d", N, ldc);
+    return -2;
+  }
+  const int nq = N / 4, nqb = nq < 256 ? nq : 256, rp = 256 / nqb;
+  long long blocks = (M + rp - 1) / rp;
+  if (blocks > 2048) blocks = 2048;
+  hipLaunchKernelGGL(splitk_reduce_kernel<half_t>, dim3((unsigned)blocks), dim3(256), 0, stream, slab, splits,
+                     M * (long long)N, C, (int)M, N, ldc, epi, nqb, rp);
+  return check16("splitk_reduce16");
+}
+
+// ---- element conversion
+__global__ void f32_to_f16_kernel(const float* __restrict__ in, half_t* __restrict__ out, long long n) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    out[i] = (half_t)in[i];
+}
+__global__ void f16_to_f32_kernel(const half_t* __restrict__ in, float* __restrict__ out, long long n) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    out[i] = (float)in[i];
+}
+static long long grid_for(long long n) {
+  long long b = (n + 255) / 256;
+  return b < 1 ? 1 : (b > 16384 ? 16384 : b);
+}
+int launch_f32_to_f16(const float* in, half_t* out, long long n, hipStream_t s) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(f32_to_f16_kernel, dim3((unsigned)grid_for(n)), dim3(256), 0, s, in, out, n);
+  return check16("f32_to_f16");
+}
+int launch_f16_to_f32(const half_t* in, float* out, long long n, hipStream_t s) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(f16_to_f32_kernel, dim3((unsigned)grid_for(n)), dim3(256), 0, s, in, out, n);
+  return check16("f16_to_f32");
+}
+
+// ---- max pool on fp16 NHWC (C % 8 == 0): 8 channels per thread, the reference's window
+// order and `m >= x ? m : x`, pad cells (-FLT_MAX in the reference) skipped
+__global__ void maxpool16_kernel(const half_t* __restrict__ in, half_t* __restrict__ out, PoolGeom g, long long total) {
+  typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+  const int cq = g.C / 8;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % cq) * 8;
+    long long t = i / cq;
+    const int ox = (int)(t % g.OW);
+    t /= g.OW;
+    const int oy = (int)(t % g.OH);
+    const int b = (int)(t / g.OH);
+    float m[8];
+    bool first = true;
+    for (int dy = 0; dy < g.kh; ++dy)
+      for (int dx = 0; dx < g.kw; ++dx) {
+        const int iy = oy * g.sh - g.pt + dy, ix = ox * g.sw - g.pl + dx;
+        float v[8];
+        if ((unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W) {
+          const h8 x = *reinterpret_cast<const h8*>(in + (((size_t)b * g.H + iy) * g.W + ix) * g.C + c);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = (float)x[e];
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = -FLT_MAX;
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) m[e] = first ? v[e] : (m[e] >= v[e] ? m[e] : v[e]);
+        first = false;
+      }
+    h8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = (half_t)m[e];
+    *reinterpret_cast<h8*>(out + (((size_t)b * g.OH + oy) * g.OW + ox) * g.C + c) = o;
+  }
+}
+int launch_maxpool16(const half_t* in, half_t* out, const PoolGeom& g, hipStream_t s) {
+  if (g.B == 0) return 0;
+  if (g.C % 8 != 0) {
+    set_error("maxpool16: C=%d must be a multiple of 8", g.C);
+    return -2;
+  }
+  const long long total = (long long)g.B * g.OH * g.OW * (g.C / 8);
+  hipLaunchKernelGGL(maxpool16_kernel, dim3((unsigned)grid_for(total)), dim3(256), 0, s, in, out, g, total);
+  return check16("maxpool16");
+}
+
+}  // namespace dnnhip

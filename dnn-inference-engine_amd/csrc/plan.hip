@@ -101,6 +101,7 @@ struct dnn_plan {
   int cur_h = 0, cur_w = 0, cur_c = 0;
   bool fuse = true;
   bool patch = true;
+  int fp16 = 0;  // 1: fp16 activations/weights, fp16 MFMA, fp32 accumulate + epilogue
   std::vector<PlanLayer> layers;
   std::vector<KernelDesc> kernels;
   int device = -1;
@@ -151,7 +152,9 @@ static void layout(dnn_plan* p) {
     char nm[64];
     if (L.type == 0) {
       L.w_off = off;
-      off = align_up(off + (size_t)L.Npad * L.Kpad, 64);
+      // fp16 GEMM layers hold Bt in halves (2 per float slot); conv0's direct kernel reads fp32
+      const bool half_w = p->fp16 && L.mode != MODE_DIRECT;
+      off = align_up(off + ((size_t)L.Npad * L.Kpad + (half_w ? 1 : 0)) / (half_w ? 2 : 1), 64);
       L.epi_off = off;
       off = align_up(off + 4 * (size_t)L.Npad, 64);
       const double flops = 2.0 * M * L.OC * L.K, w_b = 4.0 * L.K * L.OC;
@@ -181,8 +184,15 @@ static void layout(dnn_plan* p) {
       p->kernels.push_back({nm, (int)i, 2, 0.0, in_b + out_b});
     }
   }
+  if (p->fp16) {  // fp16 plans convert at the edges: fp32 frames in (unless conv0 is direct), fp32 out
+    if (p->layers.empty() || p->layers[0].mode != MODE_DIRECT)
+      p->kernels.insert(p->kernels.begin(), {"input.cvt", -1, 4, 0.0, 6.0 * B * p->in_h * p->in_w * p->in_c});
+    p->kernels.push_back({"output.cvt", -1, 4, 0.0, 6.0 * B * p->cur_h * p->cur_w * p->cur_c});
+    for (auto& L : p->layers) L.kernel_idx += (p->layers.empty() || p->layers[0].mode != MODE_DIRECT) ? 1 : 0;
+  }
   p->weight_floats = align_up(off, 64);
-  p->act_floats = align_up(act * (size_t)p->batch, 64);
+  // activation buffers hold fp16 elements on the fp16 path
+  p->act_floats = align_up((act * (size_t)p->batch + (p->fp16 ? 1 : 0)) / (p->fp16 ? 2 : 1), 64);
   p->col_floats = align_up(col * (size_t)p->batch, 64);
   p->slab_floats = align_up(slab * (size_t)p->batch, 64);
   p->ws_floats = 2 * p->act_floats + p->col_floats + p->slab_floats + dnn_plan::kZeroFloats;
@@ -222,10 +232,24 @@ void dnn_plan_destroy(dnn_plan* p) {
 
 static void set_cfg(dnn_plan* p, PlanLayer& L) {
   const long long M = (long long)p->batch * L.OH * L.OW;
+  if (p->fp16) {  // fp16 MFMA configs: BK = 64 halves, split rule on (N, K) only
+    L.cfg = choose_gemm16_cfg(M, L.OC, L.K);
+    L.Kpad = (int)align_up(L.K, 64);
+    L.Npad = (int)align_up(L.OC, gemm16_cfg_bn(L.cfg));
+    L.splits = (L.Kpad == L.K) ? choose_splitk16(L.OC, L.K) : 1;
+    return;
+  }
   L.cfg = L.mode == MODE_IMPLICIT ? choose_gemm_cfg_implicit(M, L.OC, L.K) : choose_gemm_cfg(M, L.OC, L.K);
   L.Kpad = (int)align_up(L.K, gemm_cfg_bk(L.cfg));
   L.Npad = (int)align_up(L.OC, gemm_cfg_bn(L.cfg));
   L.splits = (L.cfg >= GEMM_128x128_K32 && L.Kpad == L.K) ? choose_splitk(L.OC, L.K) : 1;
+}
+
+int dnn_plan_set_precision(dnn_plan* p, int precision) {
+  DNN_REQUIRE(p && !p->finalized && p->layers.empty(), "dnn_plan_set_precision: call before adding layers");
+  DNN_REQUIRE(precision == 0 || precision == 1, "dnn_plan_set_precision: precision must be 0 (fp32) or 1 (fp16)");
+  p->fp16 = precision;
+  return 0;
 }
 
 int dnn_plan_add_conv(dnn_plan* p, int kh, int kw, int od, int stride_h, int stride_w, int padding,
@@ -252,8 +276,12 @@ int dnn_plan_add_conv(dnn_plan* p, int kh, int kw, int od, int stride_h, int str
   L.OC = od;
   L.K = kh * kw * L.C;
   const bool one_by_one = kh == 1 && kw == 1 && stride_h == 1 && stride_w == 1 && L.pt == 0 && L.pl == 0 &&
-                          L.OH == L.H && L.OW == L.W && L.C % 32 == 0;
-  if (one_by_one)
+                          L.OH == L.H && L.OW == L.W && L.C % (p->fp16 ? 8 : 32) == 0;
+  if (p->fp16) {
+    // fp16 path: 1x1 on the input, implicit GEMM (C % 8 == 0), or conv0's direct kernel (set
+    // when its 2x2/s2 pool arrives); anything else is rejected at finalize
+    L.mode = one_by_one ? MODE_DIRECT_A : (L.C % 8 == 0 && kh * kw <= 30) ? MODE_IMPLICIT : MODE_GEMM;
+  } else if (one_by_one)
     L.mode = MODE_DIRECT_A;
   else if (p->fuse && implicit_conv_supported(L.C, kh, kw) &&
            choose_gemm_cfg_implicit((long long)p->batch * L.OH * L.OW, od, L.K) >= 0)
@@ -312,7 +340,7 @@ int dnn_plan_add_max_pool(dnn_plan* p, int kh, int kw, int stride_h, int stride_
       bool ok = false;
       if (prev.mode == MODE_IMPLICIT) {
         ok = true;
-        if (p->patch && patch_conv_pool_supported(prev.C, prev.OC, prev.H, prev.W, prev.OH, prev.OW, prev.kh, prev.kw,
+        if (!p->fp16 && p->patch && patch_conv_pool_supported(prev.C, prev.OC, prev.H, prev.W, prev.OH, prev.OW, prev.kh, prev.kw,
                                                   prev.sh, prev.sw, prev.pt, prev.pl) &&
             prev.Kpad == patch_conv_kpad(prev.C))
           prev.mode = MODE_PATCH;  // same packed weights (Bt[Npad][Kpad]) as the implicit GEMM
@@ -356,11 +384,15 @@ int dnn_plan_memory(const dnn_plan* pc, size_t* weight_bytes, size_t* workspace_
 }
 
 static int upload_weights(dnn_plan* p) {
-  size_t maxw = 0;
+  size_t maxw = 0, maxp = 0;
   for (auto& L : p->layers)
-    if (L.type == 0) maxw = std::max(maxw, L.w.size());
+    if (L.type == 0) {
+      maxw = std::max(maxw, L.w.size());
+      maxp = std::max(maxp, (size_t)L.Npad * L.Kpad);
+    }
   float* tmp = nullptr;
-  DNN_HIP_TRY(hipMalloc(&tmp, std::max<size_t>(maxw, 1) * sizeof(float)));
+  DNN_HIP_TRY(hipMalloc(&tmp, (std::max<size_t>(maxw, 1) + (p->fp16 ? maxp : 0)) * sizeof(float)));
+  float* packed32 = tmp + std::max<size_t>(maxw, 1);  // fp16 plans: fp32 pack, then convert
   int rc = 0;
   for (auto& L : p->layers) {
     if (L.type != 0) continue;
@@ -369,7 +401,14 @@ static int upload_weights(dnn_plan* p) {
       if (hipMemcpy(p->weights + L.w_off, L.w.data(), wb, hipMemcpyHostToDevice) != hipSuccess) rc = -1;
     } else {
       if (hipMemcpy(tmp, L.w.data(), wb, hipMemcpyHostToDevice) != hipSuccess) rc = -1;
-      if (!rc) rc = launch_pack_weights(tmp, p->weights + L.w_off, L.K, L.OC, L.Kpad, L.Npad, 0, L.kh, L.kw, L.C, 0);
+      if (p->fp16) {
+        if (!rc) rc = launch_pack_weights(tmp, packed32, L.K, L.OC, L.Kpad, L.Npad, 0, L.kh, L.kw, L.C, 0);
+        if (!rc)
+          rc = launch_f32_to_f16(packed32, reinterpret_cast<half_t*>(p->weights + L.w_off),
+                                 (long long)L.Npad * L.Kpad, 0);
+      } else if (!rc) {
+        rc = launch_pack_weights(tmp, p->weights + L.w_off, L.K, L.OC, L.Kpad, L.Npad, 0, L.kh, L.kw, L.C, 0);
+      }
     }
     float* e = p->weights + L.epi_off;
     const size_t nb = (size_t)L.Npad * sizeof(float);
@@ -393,6 +432,13 @@ static int upload_weights(dnn_plan* p) {
 int dnn_plan_finalize(dnn_plan* p, int device, void* weights, void* workspace) {
   DNN_REQUIRE(p && !p->finalized, "dnn_plan_finalize: plan is NULL or already finalized");
   DNN_REQUIRE(!p->layers.empty(), "dnn_plan_finalize: plan has no layers");
+  if (p->fp16)
+    for (auto& L : p->layers) {
+      DNN_REQUIRE(L.type != 0 || L.mode != MODE_GEMM,
+                  "dnn_plan_finalize: fp16 plan cannot run conv %dx%dx%d k%dx%d (needs C %% 8 == 0, or <= 4 "
+                  "input channels with a fused 2x2/s2 pool)", L.H, L.W, L.C, L.kh, L.kw);
+      DNN_REQUIRE(L.type != 1 || L.C % 8 == 0, "dnn_plan_finalize: fp16 pool needs C %% 8 == 0 (C=%d)", L.C);
+    }
   layout(p);
   DNN_HIP_TRY(hipSetDevice(device));
   p->device = device;
@@ -438,12 +484,75 @@ static int record(dnn_plan* p, int kernel, hipStream_t s) {
   return 0;
 }
 
+// fp16 path: fp16 activations between layers, fp32 frames in / predictions out
+static int run_fp16(dnn_plan* p, int n, const float* d_in, float* d_out, hipStream_t s) {
+  half_t* act[2] = {reinterpret_cast<half_t*>(p->ws), reinterpret_cast<half_t*>(p->ws + p->act_floats)};
+  float* slab = p->ws + 2 * p->act_floats + p->col_floats;
+  const float* zero = p->ws + p->ws_floats - dnn_plan::kZeroFloats;
+  const int nl = (int)p->layers.size();
+  const half_t* cur = nullptr;
+  int rc = 0;
+  if (p->layers[0].mode != MODE_DIRECT) {  // convert the frames once (into act[1]: layer 0 writes act[0])
+    if ((rc = record(p, 0, s))) return rc;
+    if ((rc = launch_f32_to_f16(d_in, act[1], (long long)n * p->in_h * p->in_w * p->in_c, s))) return rc;
+    cur = act[1];
+  }
+  for (int i = 0; i < nl; ++i) {
+    PlanLayer& L = p->layers[i];
+    half_t* dst = act[i & 1];
+    int k = L.kernel_idx;
+    if (L.type == 0) {
+      const float* e = p->weights + L.epi_off;
+      const EpiParams epi{e, e + L.Npad, e + 2 * L.Npad, e + 3 * L.Npad, L.epi_flags};
+      const half_t* wt = reinterpret_cast<const half_t*>(p->weights + L.w_off);
+      if ((rc = record(p, k, s))) return rc;
+      const long long Mc = (long long)n * L.OH * L.OW;
+      switch (L.mode) {
+        case MODE_DIRECT: {
+          DirectGeom g{n, L.H, L.W, L.OH, L.OW, L.PH, L.PW, L.pt, L.pl};
+          rc = launch_conv3x3_pool2_direct_f16out(d_in, p->weights + L.w_off, dst, g, L.C, L.OC, epi, s);
+          break;
+        }
+        case MODE_DIRECT_A:
+          rc = launch_gemm16(L.cfg, GEMM_DENSE, cur, L.C, ImplicitConv{}, wt, L.Kpad, dst, L.OC, Mc, L.OC, L.Kpad,
+                             epi, s, L.splits, slab);
+          break;
+        case MODE_IMPLICIT: {
+          ImplicitConv ic{zero, L.H, L.W, L.C, L.OH, L.OW, L.PH, L.PW, L.kh, L.kw, L.sh, L.sw, L.pt, L.pl,
+                          L.pool ? 1 : 0};
+          const long long M = L.pool ? 4LL * n * L.PH * L.PW : Mc;
+          rc = launch_gemm16(L.cfg, L.pool ? GEMM_IMPLICIT_POOL : GEMM_IMPLICIT, cur, 0, ic, wt, L.Kpad, dst, L.OC,
+                             M, L.OC, L.Kpad, epi, s, L.splits, slab);
+          break;
+        }
+        default:
+          set_error("dnn_plan_run: fp16 plan has an unsupported conv mode %d", L.mode);
+          return -2;
+      }
+      if (rc) return rc;
+      if (L.splits > 1) {
+        if ((rc = record(p, ++k, s))) return rc;
+        if ((rc = launch_splitk_reduce16(slab, L.splits, Mc, L.OC, dst, L.OC, epi, s))) return rc;
+      }
+    } else {
+      PoolGeom g{n, L.H, L.W, L.C, L.OH, L.OW, L.kh, L.kw, L.sh, L.sw, L.pt, L.pl, 0};
+      if ((rc = record(p, k, s))) return rc;
+      if ((rc = launch_maxpool16(cur, dst, g, s))) return rc;
+    }
+    cur = dst;
+  }
+  if ((rc = record(p, (int)p->kernels.size() - 1, s))) return rc;
+  if ((rc = launch_f16_to_f32(cur, d_out, (long long)n * p->cur_h * p->cur_w * p->cur_c, s))) return rc;
+  return record(p, -1, s);
+}
+
 int dnn_plan_run(dnn_plan* p, int n, const float* d_in, float* d_out, void* stream) {
   DNN_REQUIRE(p && p->finalized, "dnn_plan_run: plan not finalized");
   DNN_REQUIRE(n >= 0 && n <= p->batch, "dnn_plan_run: n=%d outside [0, %d]", n, p->batch);
   if (n == 0) return 0;
   DNN_REQUIRE(d_in && d_out, "dnn_plan_run: NULL tensor");
   hipStream_t s = static_cast<hipStream_t>(stream);
+  if (p->fp16) return run_fp16(p, n, d_in, d_out, s);
   float* act[2] = {p->ws, p->ws + p->act_floats};
   float* col = p->ws + 2 * p->act_floats;
   float* slab = col + p->col_floats;
@@ -582,12 +691,13 @@ int dnn_plan_describe(const dnn_plan* p, char* buf, int buf_len) {
   for (size_t i = 0; i < p->layers.size(); ++i) {
     const PlanLayer& L = p->layers[i];
     if (L.type == 0)
-      snprintf(line, sizeof(line), "conv %dx%dx%d -> %dx%dx%d k%dx%d s%d mode=%s cfg=%d K=%d Kpad=%d%s%s\n", L.H,
+      snprintf(line, sizeof(line), "conv %dx%dx%d -> %dx%dx%d k%dx%d s%d mode=%s cfg=%d K=%d Kpad=%d%s%s%s\n", L.H,
                L.W, L.C, L.out_h(), L.out_w(), L.OC, L.kh, L.kw, L.sh, kModeName[L.mode], L.cfg, L.K, L.Kpad,
-               L.pool ? " +pool2x2s2" : "", L.splits > 1 ? (L.splits == 3 ? " splitK=3" : " splitK") : "");
+               L.pool ? " +pool2x2s2" : "", L.splits > 1 ? (L.splits == 3 ? " splitK=3" : " splitK") : "",
+               p->fp16 ? " fp16" : "");
     else
-      snprintf(line, sizeof(line), "pool %dx%dx%d -> %dx%dx%d k%dx%d s%d\n", L.H, L.W, L.C, L.OH, L.OW, L.OC, L.kh,
-               L.kw, L.sh);
+      snprintf(line, sizeof(line), "pool %dx%dx%d -> %dx%dx%d k%dx%d s%d%s\n", L.H, L.W, L.C, L.OH, L.OW, L.OC, L.kh,
+               L.kw, L.sh, p->fp16 ? " fp16" : "");
     s += line;
   }
   snprintf(buf, buf_len, "%s", s.c_str());

@@ -64,6 +64,7 @@ def _bind_plan_api(lib):
         "dnn_plan_run": (i, [vp, i, vp, vp, vp]),
         "dnn_plan_run_host": (i, [vp, i, vp, vp]),
         "dnn_plan_run_graph": (i, [vp, i, vp, vp, vp]),
+        "dnn_plan_set_precision": (i, [vp, i]),
         "dnn_plan_num_kernels": (i, [vp]),
         "dnn_plan_kernel_info": (i, [vp, i, ctypes.c_char_p, i, P(ctypes.c_double), P(ctypes.c_double)]),
         "dnn_plan_timing_begin": (i, [vp, i]),
@@ -127,12 +128,25 @@ def _vp(a):
     return None if a is None else ctypes.c_void_p(a.ctypes.data)
 
 
-class DnnInferenceEngine(object):
-    """proj3/dnn_openblas.py:23-57.  `device` picks the GPU (default $DNN_HIP_DEVICE or 0)."""
+PRECISIONS = {"fp32": 0, "fp16": 1}
 
-    def __init__(self, graph, debug, device=None):
+
+def _precision(p):
+    p = (os.environ.get("DNN_HIP_PRECISION", "fp32") if p is None else p).lower()
+    if p not in PRECISIONS:
+        raise ValueError(f"precision must be one of {sorted(PRECISIONS)}, got {p!r}")
+    return p
+
+
+class DnnInferenceEngine(object):
+    """proj3/dnn_openblas.py:23-57.  `device` picks the GPU (default $DNN_HIP_DEVICE or 0);
+    `precision` "fp32" (default, the reference's arithmetic) or "fp16" (fp16 MFMA conv path,
+    BASELINE config 5; default from $DNN_HIP_PRECISION)."""
+
+    def __init__(self, graph, debug, device=None, precision=None):
         self.g = graph
         self.debug = debug
+        self.precision = _precision(precision)
         self.device = int(os.environ.get("DNN_HIP_DEVICE", "0")) if device is None else device
         self.save_dir = os.path.join(os.getcwd(), "intermediate")
         self._plan = None
@@ -142,7 +156,7 @@ class DnnInferenceEngine(object):
     def plan(self):
         """The lowered plan (built on first use; weights uploaded once)."""
         if self._plan is None:
-            self._plan = Plan.from_graph(self.g, device=self.device)
+            self._plan = Plan.from_graph(self.g, device=self.device, precision=self.precision)
         return self._plan
 
     def run(self, tin):
@@ -492,13 +506,16 @@ class Plan(object):
     """Owner of a dnn_plan handle (include/dnn_hip_plan.h)."""
 
     def __init__(self, batch, in_shape, entries, device=0, weights_ptr=None, workspace_ptr=None, upload=True,
-                 leaky_variant=1, lib=None):
+                 leaky_variant=1, lib=None, precision="fp32"):
         self.lib = lib or mylib
         self.batch = int(batch)
         self.in_shape = tuple(int(v) for v in in_shape)
+        self.precision = _precision(precision)
         h = ctypes.c_void_p()
         _check(self.lib.dnn_plan_create(self.batch, *self.in_shape, ctypes.byref(h)), "dnn_plan_create", self.lib)
         self.h = h
+        _check(self.lib.dnn_plan_set_precision(self.h, PRECISIONS[self.precision]), "dnn_plan_set_precision",
+               self.lib)
         self.entries = entries
         for e in entries:
             if isinstance(e, ConvEntry):
@@ -538,12 +555,13 @@ class Plan(object):
         return cls(g.in_node.in_shape[0], tuple(g.in_node.in_shape[1:]), entries, device=device, **kw)
 
     @staticmethod
-    def memory(batch, in_shape, entries, lib=None):
+    def memory(batch, in_shape, entries, lib=None, precision="fp32"):
         """(weight_bytes, workspace_bytes) a plan of this shape needs, without finalizing."""
         lib = lib or mylib
         h = ctypes.c_void_p()
         _check(lib.dnn_plan_create(int(batch), *in_shape, ctypes.byref(h)), "dnn_plan_create", lib)
         try:
+            _check(lib.dnn_plan_set_precision(h, PRECISIONS[_precision(precision)]), "dnn_plan_set_precision", lib)
             for e in entries:
                 if isinstance(e, ConvEntry):
                     kh, kw, _, od = e.conv.kernel.shape

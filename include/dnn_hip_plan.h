@@ -34,6 +34,13 @@ const char* dnn_last_error(void);
 int dnn_plan_create(int batch, int in_h, int in_w, int in_c, dnn_plan** out);
 void dnn_plan_destroy(dnn_plan* plan);
 
+/* Precision of the plan (call before adding layers): 0 = fp32 everywhere (default, the
+ * reference's arithmetic); 1 = fp16 conv path (BASELINE config 5): fp16 activations and
+ * weights, v_mfma_f32_32x32x16_f16 with fp32 accumulation and fp32 epilogue, fp32 frames in
+ * and fp32 predictions out.  fp16 plans need C % 8 == 0 for every conv except a <= 4-channel
+ * 3x3 first conv followed by a 2x2/s2 pool; tolerance vs fp32: DESIGN.md. */
+int dnn_plan_set_precision(dnn_plan* plan, int precision);
+
 /* Append a Conv2D (proj3/dnn_openblas.py:144-188) with its trailing BiasAdd / BatchNorm /
  * LeakyReLU fused.  kernel: [kh][kw][in_c][od] HWIO.  biases may be NULL (no BiasAdd);
  * mean/var/gamma all NULL means no BatchNorm (else all three, eps as in

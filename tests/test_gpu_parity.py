@@ -534,3 +534,56 @@ def test_yolov2tiny_front_end_from_pickle(tmp_path, yolo_weights, golden_frames,
     # can move a truncated corner of a huge box by one pixel)
     gold = post_golden["net_frame0"][1]
     assert [b[0] for b in boxes] == [g[0] for g in gold]
+
+
+# ------------------------------------------------------------------ fp16 path (BASELINE config 5)
+FP16_LAYER_TOL = 5e-3   # normwise vs the fp32 oracle: fp16 inputs/weights/outputs (2^-11 each), fp32 accumulate
+FP16_NET_TOL = 2e-2     # whole net vs the fp32 reference goldens (SURVEY.md §8d suggested bound)
+
+FP16_CASES = [
+    # B, H, W, C, kh, od, pool (2x2 s2 | s1 | None)
+    (2, 26, 22, 16, 3, 32, "s2"),     # conv1-like: 4 taps per 64-half K-step
+    (3, 20, 18, 32, 3, 64, "s2"),     # conv2-like
+    (2, 13, 13, 32, 3, 64, "s2"),     # odd 13x13 -> 7x7 pool padding
+    (4, 16, 16, 64, 3, 128, None),    # conv3-like, no pool
+    (64, 13, 13, 256, 3, 512, "s1"),  # conv5-like: split-K 3 + reduce, then the stride-1 pool
+    (3, 13, 13, 64, 1, 125, None),    # 1x1 dense, ragged N
+    (2, 40, 38, 3, 3, 16, "s2"),      # conv0-like: direct kernel, fp32 frames -> fp16 activations
+]
+
+
+@pytest.mark.parametrize("case", FP16_CASES)
+def test_fp16_layers_vs_oracle(case):
+    B, H, W, C, kh, od, pool = case
+    rng = np.random.default_rng(B * 7 + C + od)
+    x = rng.standard_normal((B, H, W, C)).astype(np.float32)
+    k = (rng.standard_normal((kh, kh, C, od)) * np.sqrt(2.0 / (kh * kh * C))).astype(np.float32)
+    bias = rng.standard_normal(od).astype(np.float32) * 0.1
+    bn = (rng.standard_normal(od).astype(np.float32) * 0.1, rng.uniform(0.5, 1.5, od).astype(np.float32),
+          rng.uniform(0.5, 1.5, od).astype(np.float32))
+    pl = {"s2": (2, 2, "SAME"), "s1": (2, 1, "SAME"), None: None}[pool]
+    kw = dict(bias=bias, bn=bn, leaky=True, pool=pl)
+    eng = dnn_hip.DnnInferenceEngine(_chain(x.shape, k, **kw), False, precision="fp16")
+    y = eng.run(x)
+    assert " fp16" in eng.plan().describe()
+    ref = _oracle_chain(x, k, **kw)
+    assert y.shape == ref.shape and y.dtype == np.float32
+    assert R.normwise_err(y, ref) < FP16_LAYER_TOL
+
+
+def test_fp16_yolo_vs_reference_golden_and_batch_invariance(yolo_weights, golden_frames):
+    """Whole YOLOv2-tiny in fp16 vs the fp32 reference goldens, and batch-64 rows == batch-1
+    runs bit for bit (the fp16 plan's summation order also depends on (N, K) only)."""
+    g1, _ = yolo_graph.build_graph(dnn_hip.DnnGraphBuilder, yolo_weights, in_shape=(1, 416, 416, 3))
+    e1 = dnn_hip.DnnInferenceEngine(g1, False, precision="fp16")
+    errs = []
+    for f in range(4):
+        y = e1.run(synth.frame(f))
+        errs.append(R.normwise_err(y, golden_frames[f]))
+    assert max(errs) < FP16_NET_TOL, errs
+    idx = [0, 1, 2, 3] + [100 + i for i in range(60)]
+    x = synth.frames(idx)
+    g64, _ = yolo_graph.build_graph(dnn_hip.DnnGraphBuilder, yolo_weights, in_shape=(64, 416, 416, 3))
+    y64 = dnn_hip.DnnInferenceEngine(g64, False, precision="fp16").run(x)
+    for pos in (0, 3, 17, 63):
+        assert np.array_equal(y64[pos:pos + 1], e1.run(x[pos:pos + 1]))
