@@ -1,0 +1,338 @@
+// MFMA kernels for the two small-channel layers of YOLOv2-tiny.
+//
+// conv0_mfma_pool_kernel<F16>: 3x3 / stride 1 / SAME conv of fp32 NHWC frames with <= 3
+//   input channels and 16 outputs + epilogue + 2x2/s2 max pool (conv0: 416x416x3 -> 16,
+//   pooled 208x208).  K = 9*cin <= 27 is padded to 32 and the conv runs on MFMAs whose A
+//   fragments each lane gathers straight from an LDS input patch (no im2col anywhere):
+//   F16 = false: v_mfma_f32_16x16x4_f32 (8 per 16-pixel tile, exact fp32 products);
+//   F16 = true : v_mfma_f32_16x16x32_f16 (1 per tile; fp16 path, fp16 output).
+//   Weights (HWIO [K][16]) live in registers.  Rows are pool-window-major (row = 4*window +
+//   2*dy + dx), so a lane's 4 accumulator registers are one pool window: pool, then the
+//   epilogue once (pool_then_epilogue, gemm_f32.h).  Replaces conv3x3_pool2_direct_kernel's
+//   fp32 FMA loop (VALU-bound at ~50 TF, SQ counters) for cin <= 3.
+//
+// conv1_patch_f16_kernel: the fp16 path's conv1 (208x208x16 -> 32, pooled): the fp32 patch
+//   kernel's structure (conv_patch.hip) in fp16 — one LDS-DMA pass stages the 18x18x16 half
+//   patch per 16x16 tile, each lane holds its weight fragments in registers, and every K-step
+//   of v_mfma_f32_16x16x32_f16 covers two taps (lane part p: tap 2s + p/2, channels
+//   8(p&1)..+7), tap 9 being zero.
+#include <hip/hip_runtime.h>
+#include <cfloat>
+#include "dnn_common.h"
+#include "gemm_f32.h"
+
+namespace dnnhip {
+
+typedef _Float16 h8_t __attribute__((ext_vector_type(8)));
+
+constexpr int SC_T = 16;        // conv outputs per tile edge (8 x 8 pool windows)
+constexpr int SC_P = SC_T + 2;  // patch edge
+
+// ------------------------------------------------------------------------------ conv0
+template <int CIN, bool F16, typename OutT>
+__global__ void __launch_bounds__(256)
+conv0_mfma_pool_kernel(const float* __restrict__ in, const float* __restrict__ w, OutT* __restrict__ out,
+                       DirectGeom g, int tilesX, int tilesY, int ntiles, int vec_ok, EpiParams epi) {
+  static_assert(CIN >= 1 && CIN <= 3, "K = 9*cin must fit 32");
+  constexpr int K = 9 * CIN;
+  // patch rows start at pixel x0 - pl - 3 (16-B aligned for any CIN when x0 % 16 == 0 and
+  // pl = 1) and hold 24 pixels: the 18 the tile needs plus alignment slack
+  constexpr int PXL = 24, RS = PXL * CIN, RQ = RS / 4;  // floats / float4s per patch row
+  constexpr int XOFF = 3;
+  constexpr int NQ = SC_P * RQ;                  // float4s per patch
+  constexpr int QPT = (NQ + 255) / 256;          // per thread
+  __shared__ __attribute__((aligned(16))) float patch[SC_P * RS];
+  __shared__ __attribute__((aligned(16))) float stage[4][2][8][16];  // per wave: 2 window rows x 8 windows x 16 ch
+
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int fr = lane & 15, fp = lane >> 4, n = lane & 15;
+
+  // weights (HWIO [K][16]) -> this lane's B fragments, once per workgroup; A offsets per k
+  auto koff = [](int k) { return (k / (3 * CIN)) * RS + ((k / CIN) % 3) * CIN + k % CIN; };
+  float wv[8];
+  int ao[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int k = F16 ? 8 * fp + j : 4 * j + fp;
+    wv[j] = k < K ? w[k * 16 + n] : 0.f;
+    ao[j] = k < K ? koff(k) : -1;
+  }
+  const float pb_ = (epi.flags & EPI_BIAS) ? epi.bias[n] : 0.f;
+  const float pm = (epi.flags & (EPI_BN | EPI_BN_AB)) ? epi.mean[n] : 0.f;
+  const float ps = (epi.flags & (EPI_BN | EPI_BN_AB)) ? epi.sq[n] : 1.f;
+  const float pg = (epi.flags & EPI_BN) ? epi.gamma[n] : 1.f;
+
+  // patch fetch of tile t into registers (float4 per chunk, zero outside the frame)
+  auto fetch = [&](int t, f32x4 (&v)[QPT]) {
+    const int tx = t % tilesX, tt = t / tilesX, ty = tt % tilesY, b = tt / tilesY;
+    const int y0 = ty * SC_T, x0 = tx * SC_T, xs = x0 - g.pl - XOFF;
+    const float* inb = in + (size_t)b * g.H * g.W * CIN;
+#pragma unroll
+    for (int u = 0; u < QPT; ++u) {
+      const int i = threadIdx.x + 256 * u;
+      v[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (i < NQ) {
+        const int r = i / RQ, q = i - r * RQ;
+        const int iy = y0 - g.pt + r;
+        if ((unsigned)iy < (unsigned)g.H) {
+          const float* row = inb + (size_t)iy * g.W * CIN;
+          const int f0 = 4 * q;
+          const int p0 = xs + f0 / CIN, p3 = xs + (f0 + 3) / CIN;
+          // vec_ok (host): every patch-row start is 16-B aligned in the tensor
+          if (vec_ok && p0 >= 0 && p3 < g.W) {
+            v[u] = *reinterpret_cast<const f32x4*>(row + (long long)xs * CIN + f0);
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const int px = xs + (f0 + e) / CIN;
+              if (px >= 0 && px < g.W) v[u][e] = row[(long long)xs * CIN + f0 + e];
+            }
+          }
+        }
+      }
+    }
+  };
+
+  f32x4 pre[QPT];
+  int t = blockIdx.x;
+  if (t < ntiles) fetch(t, pre);
+  for (; t < ntiles; t += gridDim.x) {
+    const int tx = t % tilesX, tt = t / tilesX, ty = tt % tilesY, b = tt / tilesY;
+    const int y0 = ty * SC_T, x0 = tx * SC_T, xs = x0 - g.pl - XOFF;
+    // raw barriers with LDS-only waits: __syncthreads would also drain vmcnt, i.e. wait for
+    // the previous tile's global stores
+    wait_lgkm0();
+    raw_barrier();  // every wave's reads of the previous patch are done
+#pragma unroll
+    for (int u = 0; u < QPT; ++u) {
+      const int i = threadIdx.x + 256 * u;
+      if (i < NQ) *reinterpret_cast<f32x4*>(patch + (i / RQ) * RS + 4 * (i % RQ)) = pre[u];
+    }
+    wait_lgkm0();
+    raw_barrier();
+    if (t + (int)gridDim.x < ntiles) fetch(t + gridDim.x, pre);  // in flight during the MFMAs
+
+    f32x4 acc[4];
+    float a[4][8];  // A values of the 4 M-tiles (output pixel (y0+y, x0+x) reads input pixel
+                    // x0+x-pl+kx = patch col x + kx + (x0 - pl - xs))
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const int wi = fr >> 2, pos = fr & 3;
+      const int y = 4 * wid + 2 * (i >> 1) + (pos >> 1);
+      const int x = 2 * (4 * (i & 1) + wi) + (pos & 1);
+      const int pbase = y * RS + (x + (x0 - g.pl - xs)) * CIN;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) a[i][j] = ao[j] >= 0 ? patch[pbase + ao[j]] : 0.f;
+    }
+    if constexpr (F16) {
+      h8_t bb;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) bb[j] = (half_t)wv[j];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        h8_t av;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) av[j] = (half_t)a[i][j];
+        acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av, bb, acc[i], 0, 0, 0);
+      }
+    } else {  // 4 independent accumulation chains interleaved (dependent MFMA latency 40 cycles)
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][j], wv[j], acc[i], 0, 0, 0);
+    }
+
+    // pool + epilogue into the wave's LDS stage, then 16-B coalesced stores
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int wy = (y0 >> 1) + 2 * wid + (i >> 1), wx = (x0 >> 1) + 4 * (i & 1) + fp;
+      // window cells past the conv output (odd sizes: SAME pool padding) repeat cell (0,0)
+      const bool x1 = 2 * wx + 1 < g.OW, y1 = 2 * wy + 1 < g.OH;
+      const f32x4 v = {acc[i][0], x1 ? acc[i][1] : acc[i][0], y1 ? acc[i][2] : acc[i][0],
+                       x1 && y1 ? acc[i][3] : acc[i][0]};
+      stage[wid][i >> 1][4 * (i & 1) + fp][n] = pool_then_epilogue(v, pb_, pm, ps, pg, epi.flags);
+    }
+    wait_lgkm0();  // this wave's stage writes have landed (the stage is wave-private)
+    constexpr int VEC = F16 ? 8 : 4;
+    for (int c = lane; c < 2 * 128 / VEC; c += 64) {
+      const int lr = c / (128 / VEC), f = (c % (128 / VEC)) * VEC;  // f: float index in the row's run
+      const int wy = (y0 >> 1) + 2 * wid + lr, wxs = (x0 >> 1) + f / 16;
+      if (wy >= g.PH || wxs >= g.PW) continue;
+      const float* src = &stage[wid][lr][0][0] + f;
+      OutT* dst = out + (((size_t)b * g.PH + wy) * g.PW + (x0 >> 1)) * 16 + f;
+      if constexpr (F16) {
+        h8_t o;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = (half_t)src[e];
+        *reinterpret_cast<h8_t*>(dst) = o;
+      } else {
+        *reinterpret_cast<f32x4*>(dst) = *reinterpret_cast<const f32x4*>(src);
+      }
+    }
+    wait_lgkm0();  // stage reads done before the next tile overwrites it
+  }
+}
+
+bool conv0_mfma_supported(int cin, int nout, int kh, int kw, int sh, int sw) {
+  return kh == 3 && kw == 3 && sh == 1 && sw == 1 && cin >= 1 && cin <= 3 && nout == 16;
+}
+
+template <bool F16, typename OutT>
+static int launch_conv0(const float* in, const float* w, OutT* out, const DirectGeom& g, int cin,
+                        const EpiParams& epi, hipStream_t s) {
+  if (g.B == 0) return 0;
+  const int tilesX = (g.OW + SC_T - 1) / SC_T, tilesY = (g.OH + SC_T - 1) / SC_T;
+  const long long blocks = (long long)g.B * tilesX * tilesY;
+  if (blocks > 0x7fffffffLL || cin < 1 || cin > 3 || g.PH != (g.OH + 1) / 2 || g.PW != (g.OW + 1) / 2) {
+    set_error("conv0_mfma: unsupported shape (cin=%d)", cin);
+    return -2;
+  }
+  // persistent: 8 workgroups per CU loop over the tiles (weights loaded once per workgroup,
+  // the next tile's patch prefetched into registers during the current tile's MFMAs)
+  const int nt = (int)blocks;
+  const dim3 grid((unsigned)(nt < 2048 ? nt : 2048));
+  // float4 patch rows when every row start (pixel x0 - pl - 3, x0 % 16 == 0) is 16-B aligned
+  const int vec_ok = ((g.W * cin) % 4 == 0 && ((long long)g.H * g.W * cin) % 4 == 0 && ((g.pl + 3) * cin) % 4 == 0 &&
+                      (reinterpret_cast<uintptr_t>(in) % 16) == 0)
+                         ? 1
+                         : 0;
+  switch (cin) {
+    case 1: hipLaunchKernelGGL((conv0_mfma_pool_kernel<1, F16, OutT>), grid, dim3(256), 0, s, in, w, out, g, tilesX, tilesY, nt, vec_ok, epi); break;
+    case 2: hipLaunchKernelGGL((conv0_mfma_pool_kernel<2, F16, OutT>), grid, dim3(256), 0, s, in, w, out, g, tilesX, tilesY, nt, vec_ok, epi); break;
+    default: hipLaunchKernelGGL((conv0_mfma_pool_kernel<3, F16, OutT>), grid, dim3(256), 0, s, in, w, out, g, tilesX, tilesY, nt, vec_ok, epi); break;
+  }
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    set_error("launch conv0_mfma: %s", hipGetErrorString(e));
+    return -1;
+  }
+  return 0;
+}
+
+int launch_conv0_mfma(const float* in, const float* w, float* out, const DirectGeom& g, int cin, const EpiParams& epi,
+                      hipStream_t s) {
+  return launch_conv0<false, float>(in, w, out, g, cin, epi, s);
+}
+int launch_conv0_mfma_f16(const float* in, const float* w, half_t* out, const DirectGeom& g, int cin,
+                          const EpiParams& epi, hipStream_t s) {
+  return launch_conv0<true, half_t>(in, w, out, g, cin, epi, s);
+}
+
+// ------------------------------------------------------------------------------ conv1 fp16
+// in: fp16 NHWC [B][H][W][16]; Bt: packed fp16 weights [32][ldb] (k = tap*16 + c, ldb >= 144);
+// out: fp16 pooled [B][PH][PW][32].  SAME 3x3 stride 1, even OH/OW.
+__global__ void __launch_bounds__(256)
+conv1_patch_f16_kernel(const half_t* __restrict__ in, const half_t* __restrict__ Bt, int ldb,
+                       half_t* __restrict__ out, DirectGeom g, int tilesX, int tilesY, const float* __restrict__ zero,
+                       EpiParams epi) {
+  constexpr int C = 16;
+  constexpr int PATCH = SC_P * SC_P * C;      // halves
+  constexpr int PATCH_CH = (PATCH * 2 + 1023) / 1024;  // 1-KiB DMA chunks
+  __shared__ __attribute__((aligned(1024))) float smem[PATCH_CH * 256];
+  const half_t* P = reinterpret_cast<const half_t*>(smem);
+
+  int t = xcd_tile(blockIdx.x, gridDim.x);
+  const int tx = t % tilesX;
+  t /= tilesX;
+  const int ty = t % tilesY;
+  const int b = t / tilesY;
+  const int y0 = ty * SC_T, x0 = tx * SC_T;
+  const int lane = threadIdx.x & 63;
+  const int wid = wave_uniform(threadIdx.x >> 6);
+
+  // patch: 16-B chunks = 8 channels; pixel pp = chunk / 2
+  const half_t* inb = in + (size_t)b * g.H * g.W * C;
+  for (int c = wid; c < PATCH_CH; c += 4) {
+    const int q = c * 64 + lane;  // 16-B chunk index
+    const int pp = q >> 1, half8 = (q & 1) * 8;
+    const int py = pp / SC_P, px = pp - py * SC_P;
+    const int iy = y0 - 1 + py, ix = x0 - 1 + px;
+    const bool ok = pp < SC_P * SC_P && (unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W;
+    lds_dma16(ok ? reinterpret_cast<const float*>(inb + ((size_t)iy * g.W + ix) * C + half8) : zero,
+              smem + c * 256);
+  }
+
+  // B fragments in registers: K-step s (0..4) covers taps 2s, 2s+1; lane part p -> tap 2s + p/2,
+  // channels 8(p&1)..+7; N-tile j -> output channel 16j + (lane&15)
+  const int fr = lane & 15, fp = lane >> 4;
+  h8_t bw[5][2];
+#pragma unroll
+  for (int s = 0; s < 5; ++s) {
+    const int tap = 2 * s + (fp >> 1);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      if (tap < 9)
+        bw[s][j] = *reinterpret_cast<const h8_t*>(Bt + (size_t)(16 * j + fr) * ldb + tap * C + 8 * (fp & 1));
+      else
+        bw[s][j] = h8_t{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+  }
+  wait_vmcnt<0>();
+  raw_barrier();
+
+  f32x4 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int wi = fr >> 2, pos = fr & 3;
+    const int y = 4 * wid + 2 * (i >> 1) + (pos >> 1);
+    const int x = 2 * (4 * (i & 1) + wi) + (pos & 1);
+    const int base = (y * SC_P + x) * C + 8 * (fp & 1);
+#pragma unroll
+    for (int s = 0; s < 5; ++s) {
+      const int tap = 2 * s + (fp >> 1);
+      h8_t a = h8_t{0, 0, 0, 0, 0, 0, 0, 0};
+      if (tap < 9) a = *reinterpret_cast<const h8_t*>(P + base + ((tap / 3) * SC_P + tap % 3) * C);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, bw[s][j], acc[i][j], 0, 0, 0);
+    }
+  }
+
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int n = 16 * j + fr;
+    const float pb = (epi.flags & EPI_BIAS) ? epi.bias[n] : 0.f;
+    const float pm = (epi.flags & (EPI_BN | EPI_BN_AB)) ? epi.mean[n] : 0.f;
+    const float ps = (epi.flags & (EPI_BN | EPI_BN_AB)) ? epi.sq[n] : 1.f;
+    const float pg = (epi.flags & EPI_BN) ? epi.gamma[n] : 1.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int wy = (y0 >> 1) + 2 * wid + (i >> 1), wx = (x0 >> 1) + 4 * (i & 1) + fp;
+      if (wy < g.PH && wx < g.PW)
+        store_out(out + (((size_t)b * g.PH + wy) * g.PW + wx) * 32 + n,
+                  pool_then_epilogue(acc[i][j], pb, pm, ps, pg, epi.flags));
+    }
+  }
+}
+
+bool conv1_patch_f16_supported(int C, int OC, int H, int W, int OH, int OW, int kh, int kw, int sh, int sw, int pt,
+                               int pl) {
+  return C == 16 && OC == 32 && kh == 3 && kw == 3 && sh == 1 && sw == 1 && pt == 1 && pl == 1 && OH == H &&
+         OW == W && OH % 2 == 0 && OW % 2 == 0;
+}
+
+int launch_conv1_patch_f16(const half_t* in, const half_t* Bt, int ldb, half_t* out, const DirectGeom& g,
+                           const float* zero, const EpiParams& epi, hipStream_t s) {
+  if (g.B == 0) return 0;
+  if (ldb < 144 || ldb % 8 || g.OH % 2 || g.OW % 2 || g.PH != g.OH / 2 || g.PW != g.OW / 2 || g.pt != 1 ||
+      g.pl != 1 || !zero) {
+    set_error("conv1_patch_f16: unsupported shape");
+    return -2;
+  }
+  const int tilesX = (g.OW + SC_T - 1) / SC_T, tilesY = (g.OH + SC_T - 1) / SC_T;
+  const long long blocks = (long long)g.B * tilesX * tilesY;
+  hipLaunchKernelGGL(conv1_patch_f16_kernel, dim3((unsigned)blocks), dim3(256), 0, s, in, Bt, ldb, out, g, tilesX,
+                     tilesY, zero, epi);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    set_error("launch conv1_patch_f16: %s", hipGetErrorString(e));
+    return -1;
+  }
+  return 0;
+}
+
+}  // namespace dnnhip

@@ -344,6 +344,10 @@ int dnn_plan_add_max_pool(dnn_plan* p, int kh, int kw, int stride_h, int stride_
                                                   prev.sh, prev.sw, prev.pt, prev.pl) &&
             prev.Kpad == patch_conv_kpad(prev.C))
           prev.mode = MODE_PATCH;  // same packed weights (Bt[Npad][Kpad]) as the implicit GEMM
+        if (p->fp16 && p->patch &&
+            conv1_patch_f16_supported(prev.C, prev.OC, prev.H, prev.W, prev.OH, prev.OW, prev.kh, prev.kw, prev.sh,
+                                      prev.sw, prev.pt, prev.pl))
+          prev.mode = MODE_PATCH;  // fp16 patch kernel on the same fp16 Bt
       } else if (prev.mode == MODE_GEMM && direct_conv_pool_supported(prev.C, prev.OC, prev.kh, prev.kw, prev.sh,
                                                                       prev.sw)) {
         prev.mode = MODE_DIRECT;
@@ -510,7 +514,14 @@ static int run_fp16(dnn_plan* p, int n, const float* d_in, float* d_out, hipStre
       switch (L.mode) {
         case MODE_DIRECT: {
           DirectGeom g{n, L.H, L.W, L.OH, L.OW, L.PH, L.PW, L.pt, L.pl};
-          rc = launch_conv3x3_pool2_direct_f16out(d_in, p->weights + L.w_off, dst, g, L.C, L.OC, epi, s);
+          rc = conv0_mfma_supported(L.C, L.OC, L.kh, L.kw, L.sh, L.sw)
+                   ? launch_conv0_mfma_f16(d_in, p->weights + L.w_off, dst, g, L.C, epi, s)
+                   : launch_conv3x3_pool2_direct_f16out(d_in, p->weights + L.w_off, dst, g, L.C, L.OC, epi, s);
+          break;
+        }
+        case MODE_PATCH: {
+          DirectGeom g{n, L.H, L.W, L.OH, L.OW, L.PH, L.PW, L.pt, L.pl};
+          rc = launch_conv1_patch_f16(cur, wt, L.Kpad, dst, g, zero, epi, s);
           break;
         }
         case MODE_DIRECT_A:
@@ -591,7 +602,9 @@ int dnn_plan_run(dnn_plan* p, int n, const float* d_in, float* d_out, void* stre
         }
         case MODE_DIRECT: {
           DirectGeom g{n, L.H, L.W, L.OH, L.OW, L.PH, L.PW, L.pt, L.pl};
-          rc = launch_conv3x3_pool2_direct(cur, wt, dst, g, L.C, L.OC, epi, s);
+          rc = conv0_mfma_supported(L.C, L.OC, L.kh, L.kw, L.sh, L.sw)
+                   ? launch_conv0_mfma(cur, wt, dst, g, L.C, epi, s)
+                   : launch_conv3x3_pool2_direct(cur, wt, dst, g, L.C, L.OC, epi, s);
           break;
         }
         case MODE_PATCH: {

@@ -40,7 +40,10 @@ def main():
     ap.add_argument("csv", nargs="+")
     ap.add_argument("--trace", help="kernel trace csv for durations (clk_ghz)")
     ap.add_argument("--out")
+    ap.add_argument("--fp16", action="store_true", help="fp16 plan kernel order")
     a = ap.parse_args()
+    if a.fp16:
+        P.ORDER[:] = P.ORDER_FP16
     res = table(a.csv)
     if a.trace:
         s = P.summarise(a.trace)

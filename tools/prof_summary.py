@@ -20,6 +20,9 @@ from collections import defaultdict
 # kernel order of one YOLOv2-tiny forward in the default (fused) plan
 ORDER = ["conv0.direct", "conv1.patch", "conv2.gemm", "conv3.gemm", "conv4.gemm", "conv5.gemm", "conv5.reduce", "pool5",
          "conv6.gemm", "conv6.reduce", "conv7.gemm", "conv7.reduce", "conv8.gemm"]
+# ... the fp16 plan (dnn_plan_set_precision 1): conv1 patch kernel, f16->f32 output conversion
+ORDER_FP16 = ["conv0.direct", "conv1.patch", "conv2.gemm", "conv3.gemm", "conv4.gemm", "conv5.gemm", "conv5.reduce",
+              "pool5", "conv6.gemm", "conv6.reduce", "conv7.gemm", "conv7.reduce", "conv8.gemm", "output.cvt"]
 # ... and with DNN_HIP_FUSE=0 (explicit im2col + GEMM, separate pools)
 ORDER_UNFUSED = []
 for _i in range(9):
@@ -31,12 +34,14 @@ for _i in range(9):
     if _i < 6:
         ORDER_UNFUSED.append(f"pool{_i}")
 
-OURS = ("dnnhip::im2col", "dnnhip::gemm", "dnnhip::maxpool", "dnnhip::conv3x3_pool2_direct",
-        "dnnhip::splitk_reduce", "dnnhip::conv3x3_patch_pool")
+# every kernel of the plan lives in namespace dnnhip; weight packing (finalize) and the
+# postprocessing kernels (after the forward) are not plan kernels
+_NOT_PLAN = ("pack_weights", "yolo_", "f32_to_f16_kernel")
 
 
 def _ours(name):
-    return any(t in name for t in OURS) and "pack_weights" not in name
+    # rocprofv3 leaves names with _Float16 parameters mangled (..6dnnhip..)
+    return ("dnnhip::" in name or "6dnnhip" in name) and not any(t in name for t in _NOT_PLAN)
 
 
 def dispatch_sequence(rows, key_start="Start_Timestamp", key_end="End_Timestamp"):
@@ -104,9 +109,12 @@ def main():
     ap.add_argument("--out")
     ap.add_argument("--note", default="")
     ap.add_argument("--unfused", action="store_true", help="trace of a DNN_HIP_FUSE=0 run")
+    ap.add_argument("--fp16", action="store_true", help="trace of a --precision fp16 run")
     a = ap.parse_args()
     if a.unfused:
         ORDER[:] = ORDER_UNFUSED
+    if a.fp16:
+        ORDER[:] = ORDER_FP16
     s = summarise(a.trace, a.fetch, a.write)
     doc = {"note": a.note or __doc__.strip().splitlines()[0], "kernels": s}
     text = json.dumps(doc, indent=1)
