@@ -18,8 +18,8 @@ import yolo_graph
 import ref_numpy as R
 
 HEADERS = {
-    "libdnn_hip.so": ["dnn_hip_plan.h", "dnn_hip.h", "dnn_hip_post.h"],
-    "libdnn_hip_avx.so": ["dnn_hip_plan.h", "dnn_hip_avx.h", "dnn_hip_post.h"],
+    "libdnn_hip.so": ["dnn_hip_plan.h", "dnn_hip.h", "dnn_hip_post.h", "dnn_hip_ingest.h"],
+    "libdnn_hip_avx.so": ["dnn_hip_plan.h", "dnn_hip_avx.h", "dnn_hip_post.h", "dnn_hip_ingest.h"],
 }
 
 

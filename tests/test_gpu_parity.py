@@ -587,3 +587,40 @@ def test_fp16_yolo_vs_reference_golden_and_batch_invariance(yolo_weights, golden
     y64 = dnn_hip.DnnInferenceEngine(g64, False, precision="fp16").run(x)
     for pos in (0, 3, 17, 63):
         assert np.array_equal(y64[pos:pos + 1], e1.run(x[pos:pos + 1]))
+
+
+# ------------------------------------------------------------------ frame ingest (§8f row 3)
+@pytest.mark.parametrize("hw", [(416, 416), (480, 640), (240, 320), (417, 203)])
+def test_preprocess_frames_vs_restatement(hw):
+    """dnn_preprocess_frames == __init__.py:8-12 restated (oracle/ingest_numpy.py): exact for
+    the identity size (the reference's own arithmetic), exact vs the restated fixed-point
+    INTER_LINEAR for real resizes (parity with cv2 itself unpinned: cv2 is absent)."""
+    import ingest
+    import ingest_numpy as IN
+    rng = np.random.default_rng(hw[0] + hw[1])
+    im = rng.integers(0, 256, size=hw + (3,), dtype=np.uint8)
+    got = ingest.resize_input_gpu(im)
+    assert got.shape == (416, 416, 3) and got.dtype == np.float32
+    assert np.array_equal(got, IN.resize_input(im))
+    if hw == (416, 416):  # the reference's formula with cv2.resize the identity
+        assert np.array_equal(got, np.asarray((im / 255.)[:, :, ::-1], dtype=np.float32))
+
+
+def test_frame_ingest_pipeline_double_buffer(yolo_b1):
+    """FrameIngest: two slots, uploads overlapped with compute, results per batch unchanged."""
+    import torch
+    import ingest
+    import ingest_numpy as IN
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(3)
+    batches = [rng.integers(0, 256, size=(3, 240, 320, 3), dtype=np.uint8) for _ in range(4)]
+    fi = ingest.FrameIngest(3, 240, 320, dev)
+    outs = []
+    for b in batches:
+        x = fi.submit(b)
+        outs.append(x.clone())  # the "forward" consuming the batch on the compute stream
+        fi.release()
+    torch.cuda.synchronize()
+    for b, o in zip(batches, outs):
+        ref = np.stack([IN.resize_input(f) for f in b])
+        assert np.array_equal(o.cpu().numpy(), ref)
