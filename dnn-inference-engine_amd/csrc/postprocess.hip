@@ -10,10 +10,13 @@
 //            boxes above the threshold append a sort key to LDS
 //   phase 2  bitonic sort of the keys (score descending, then box index = Python's stable
 //            sort of the (row, col, anchor)-ordered list)
-//   phase 3  one wave runs the greedy NMS: candidate i is dropped if its IoU with ANY kept box
-//            is > 0.3; lanes test the kept list in parallel.  IoU is the reference's integer
-//            formula (+1 widths, negative overlaps not clamped) in exact 128-bit integers,
-//            converted to double with correct rounding like Python's int -> float.
+//   phase 3  greedy NMS as a bitmask: every wave fills rows of S[i][j] = IoU(i, j) > 0.3 for
+//            j < i (64 pairs per wave step, ballot into one word), then one wave walks the
+//            candidates in order with the keep mask in registers (lane w holds word w):
+//            candidate i is dropped iff S[i] & keep != 0 — the reference's "IoU with ANY kept
+//            box" (yolov2tiny.py:197-226).  IoU is the reference's integer formula (+1 widths,
+//            negative overlaps not clamped) in exact 64/128-bit integers, converted to double
+//            with correct rounding like Python's int -> float.
 #include <hip/hip_runtime.h>
 #include <cstdint>
 #include "dnn_common.h"
@@ -21,7 +24,9 @@
 
 namespace dnnhip {
 
-constexpr int PP_THREADS = 256;
+constexpr int PP_THREADS = 512;
+constexpr int PP_WAVES = PP_THREADS / 64;
+constexpr int PP_WORDS = (DNN_YOLO_BOXES + 63) / 64;  // 14 keep / suppression words
 constexpr int PP_SORT = 1024;  // >= DNN_YOLO_BOXES, power of two
 
 __constant__ float kAnchorsF32[10] = {1.08f, 1.19f, 3.42f, 4.41f, 6.63f, 11.38f, 9.42f, 5.11f, 16.62f, 10.52f};
@@ -139,7 +144,8 @@ yolo_postprocess_kernel(const float* __restrict__ pred, dnn_detection* __restric
   __shared__ long long box[DNN_YOLO_BOXES][4];
   __shared__ float score_of[DNN_YOLO_BOXES];
   __shared__ int cls_of[DNN_YOLO_BOXES];
-  __shared__ int kept[DNN_YOLO_BOXES];
+  __shared__ unsigned long long sup[DNN_YOLO_BOXES][PP_WORDS];  // S[i][w]: bits j = 64w.. < i
+  __shared__ unsigned char zrow[DNN_YOLO_BOXES];               // row i has a zero IoU denominator
   __shared__ int n_cand, bad;
 
   const int img = blockIdx.x, tid = threadIdx.x;
@@ -221,28 +227,62 @@ yolo_postprocess_kernel(const float* __restrict__ pred, dnn_detection* __restric
     }
   }
 
-  // ---- phase 3: greedy NMS in wave 0 (yolov2tiny.py:197-226)
-  if (tid < 64) {
-    // lane 0 appends, every lane reads the list: volatile keeps the LDS accesses in program
-    // order (one wave: the LDS serves them in issue order)
-    volatile int* kv = kept;
-    int nk = 0;
-    bool zero_den = false;  // the reference evaluates every (candidate, kept) pair: exact flag
-    for (int i = 0; i < n; ++i) {
-      const int k = (int)(keys[i] & 0xffffffffu);
-      bool drop = false;
-      for (int j = tid; j < nk; j += 64) drop |= iou_gt(box[k], box[kv[j]], 0.3, &zero_den);
-      if (!__any(drop)) {
-        if (tid == 0) kv[nk] = k;
-        ++nk;
-      }
+  // ---- phase 3a: suppression bitmask, all waves (yolov2tiny.py:197-216 evaluates every pair
+  // (candidate i, kept j < i); here every pair j < i, the keep mask selects below)
+  const int lane = tid & 63, wid = tid >> 6;
+  for (int i = wid; i < n; i += PP_WAVES) {
+    const int ki = (int)(keys[i] & 0xffffffffu);
+    const long long bi[4] = {box[ki][0], box[ki][1], box[ki][2], box[ki][3]};
+    bool zany = false;
+    for (int w = 0; w * 64 < i; ++w) {
+      const int j = w * 64 + lane;
+      bool hit = false;
+      if (j < i) hit = iou_gt(bi, box[(int)(keys[j] & 0xffffffffu)], 0.3, &zany);
+      const unsigned long long m = __ballot(hit);
+      if (lane == 0) sup[i][w] = m;
     }
-    if (__any(zero_den)) {
-      if (tid == 0) counts[img] = -2;
+    const bool z = __any(zany);
+    if (lane == 0) zrow[i] = z ? 1 : 0;
+  }
+  __syncthreads();
+
+  // ---- phase 3b: greedy walk in wave 0, keep word w in lane w
+  if (tid < 64) {
+    unsigned long long kw = 0;
+    bool zero_hit = false;
+    for (int i = 0; i < n; ++i) {
+      const int nwi = (i + 63) >> 6;  // words holding j < i
+      const unsigned long long row = lane < nwi ? sup[i][lane] : 0ull;
+      const bool drop = __any((row & kw) != 0ull);
+      if (zrow[i]) {  // rare: a zero IoU denominator against a KEPT box raises in the reference
+        const int ki = (int)(keys[i] & 0xffffffffu);
+        bool zd = false;
+        for (unsigned long long bits = lane < nwi ? kw : 0ull; bits; bits &= bits - 1) {
+          const int j = lane * 64 + __builtin_ctzll(bits);
+          (void)iou_gt(box[ki], box[(int)(keys[j] & 0xffffffffu)], 0.3, &zd);
+        }
+        zero_hit |= zd;
+      }
+      if (!drop && lane == (i >> 6)) kw |= 1ull << (i & 63);
+    }
+    if (__any(zero_hit)) {
+      if (lane == 0) counts[img] = -2;
       return;
     }
-    for (int j = tid; j < nk && j < max_det; j += 64) {
-      const int k = kv[j];
+    // output in candidate order: exclusive prefix of the per-word popcounts
+    const int cnt = __popcll(kw);
+    int incl = cnt;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int v = __shfl_up(incl, d);
+      if (lane >= d) incl += v;
+    }
+    const int nk = __shfl(incl, 63);
+    int r = incl - cnt;
+    for (unsigned long long bits = kw; bits; bits &= bits - 1, ++r) {
+      const int i = lane * 64 + __builtin_ctzll(bits);
+      if (r >= max_det) break;
+      const int k = (int)(keys[i] & 0xffffffffu);
       dnn_detection d;
       d.cls = cls_of[k];
       d.score = score_of[k];
@@ -250,9 +290,9 @@ yolo_postprocess_kernel(const float* __restrict__ pred, dnn_detection* __restric
       d.top = box[k][1];
       d.right = box[k][2];
       d.bottom = box[k][3];
-      dets[(size_t)img * max_det + j] = d;
+      dets[(size_t)img * max_det + r] = d;
     }
-    if (tid == 0) counts[img] = nk;
+    if (lane == 0) counts[img] = nk;
   }
 }
 
