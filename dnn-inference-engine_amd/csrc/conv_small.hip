@@ -2,10 +2,10 @@
 //
 // conv0_mfma_pool_kernel<F16>: 3x3 / stride 1 / SAME conv of fp32 NHWC frames with <= 3
 //   input channels and 16 outputs + epilogue + 2x2/s2 max pool (conv0: 416x416x3 -> 16,
-//   pooled 208x208).  K = 9*cin <= 27 is padded to 32 and the conv runs on MFMAs whose A
-//   fragments each lane gathers straight from an LDS input patch (no im2col anywhere):
-//   F16 = false: v_mfma_f32_16x16x4_f32 (8 per 16-pixel tile, exact fp32 products);
-//   F16 = true : v_mfma_f32_16x16x32_f16 (1 per tile; fp16 path, fp16 output).
+//   pooled 208x208).  The input halo patch sits in LDS as 4-channel pixels, so each MFMA
+//   operand is a single LDS read at a compile-time tap offset (no im2col anywhere):
+//   F16 = false: 9 x v_mfma_f32_16x16x4_f32 per 16-pixel tile (lane part = channel, exact
+//   fp32 products); F16 = true: 3 x v_mfma_f32_16x16x16_f16 (lane part = tap; fp16 path).
 //   Weights (HWIO [K][16]) live in registers.  Rows are pool-window-major (row = 4*window +
 //   2*dy + dx), so a lane's 4 accumulator registers are one pool window: pool, then the
 //   epilogue once (pool_then_epilogue, gemm_f32.h).  Replaces conv3x3_pool2_direct_kernel's
@@ -18,6 +18,7 @@
 //   8(p&1)..+7), tap 9 being zero.
 #include <hip/hip_runtime.h>
 #include <cfloat>
+#include <type_traits>
 #include "dnn_common.h"
 #include "gemm_f32.h"
 
@@ -29,118 +30,126 @@ constexpr int SC_T = 16;        // conv outputs per tile edge (8 x 8 pool window
 constexpr int SC_P = SC_T + 2;  // patch edge
 
 // ------------------------------------------------------------------------------ conv0
+// LDS patch: 18 x 18 pixels x 4 channels (cin <= 3 zero-padded to 4; fp32 for the fp32
+// path, fp16 for the fp16 path), so every MFMA operand is one LDS read at a compile-time tap
+// offset from the lane's pixel:
+//   fp32: 9 x v_mfma_f32_16x16x4_f32 per 16-pixel tile, lane part p = channel p, one tap each
+//   fp16: 3 x v_mfma_f32_16x16x16_f16, lane part p = tap 4g + p (taps 9..11 zero), one
+//         ds_read_b64 = the pixel's 4 channels
+typedef _Float16 h4_t __attribute__((ext_vector_type(4)));
+
 template <int CIN, bool F16, typename OutT>
 __global__ void __launch_bounds__(256)
 conv0_mfma_pool_kernel(const float* __restrict__ in, const float* __restrict__ w, OutT* __restrict__ out,
-                       DirectGeom g, int tilesX, int tilesY, int ntiles, int vec_ok, EpiParams epi) {
-  static_assert(CIN >= 1 && CIN <= 3, "K = 9*cin must fit 32");
-  constexpr int K = 9 * CIN;
-  // patch rows start at pixel x0 - pl - 3 (16-B aligned for any CIN when x0 % 16 == 0 and
-  // pl = 1) and hold 24 pixels: the 18 the tile needs plus alignment slack
-  constexpr int PXL = 24, RS = PXL * CIN, RQ = RS / 4;  // floats / float4s per patch row
-  constexpr int XOFF = 3;
-  constexpr int NQ = SC_P * RQ;                  // float4s per patch
-  constexpr int QPT = (NQ + 255) / 256;          // per thread
-  __shared__ __attribute__((aligned(16))) float patch[SC_P * RS];
+                       DirectGeom g, int tilesX, int tilesY, int ntiles, EpiParams epi) {
+  static_assert(CIN >= 1 && CIN <= 3, "patch pixels hold 4 channels");
+  typedef typename std::conditional<F16, half_t, float>::type PT;
+  constexpr int NPX = SC_P * SC_P;          // 324 patch pixels
+  constexpr int PPT = (NPX + 255) / 256;    // pixels per thread
+  __shared__ __attribute__((aligned(16))) PT patch[NPX * 4];
   __shared__ __attribute__((aligned(16))) float stage[4][2][8][16];  // per wave: 2 window rows x 8 windows x 16 ch
 
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int fr = lane & 15, fp = lane >> 4, n = lane & 15;
 
-  // weights (HWIO [K][16]) -> this lane's B fragments, once per workgroup; A offsets per k
-  auto koff = [](int k) { return (k / (3 * CIN)) * RS + ((k / CIN) % 3) * CIN + k % CIN; };
-  float wv[8];
-  int ao[8];
+  // B fragments (HWIO [tap*CIN + c][16]), once per workgroup
+  float wv[9];
+  h4_t bw[3];
+  if constexpr (F16) {
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int k = F16 ? 8 * fp + j : 4 * j + fp;
-    wv[j] = k < K ? w[k * 16 + n] : 0.f;
-    ao[j] = k < K ? koff(k) : -1;
+    for (int gq = 0; gq < 3; ++gq) {
+      const int t = 4 * gq + fp;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) bw[gq][c] = (half_t)((t < 9 && c < CIN) ? w[(t * CIN + c) * 16 + n] : 0.f);
+    }
+  } else {
+#pragma unroll
+    for (int t = 0; t < 9; ++t) wv[t] = fp < CIN ? w[(t * CIN + fp) * 16 + n] : 0.f;
   }
   const float pb_ = (epi.flags & EPI_BIAS) ? epi.bias[n] : 0.f;
   const float pm = (epi.flags & (EPI_BN | EPI_BN_AB)) ? epi.mean[n] : 0.f;
   const float ps = (epi.flags & (EPI_BN | EPI_BN_AB)) ? epi.sq[n] : 1.f;
   const float pg = (epi.flags & EPI_BN) ? epi.gamma[n] : 1.f;
 
-  // patch fetch of tile t into registers (float4 per chunk, zero outside the frame)
-  auto fetch = [&](int t, f32x4 (&v)[QPT]) {
+  // this lane's pixel (patch index of its window origin) in each of its 4 M-tiles
+  int pix[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int wi = fr >> 2, pos = fr & 3;
+    const int y = 4 * wid + 2 * (i >> 1) + (pos >> 1);
+    const int x = 2 * (4 * (i & 1) + wi) + (pos & 1);
+    pix[i] = y * SC_P + x;
+  }
+
+  // prefetch of a tile's halo patch into registers: CIN floats per pixel, zero outside the frame
+  auto fetch = [&](int t, float (&v)[PPT][CIN]) {
     const int tx = t % tilesX, tt = t / tilesX, ty = tt % tilesY, b = tt / tilesY;
-    const int y0 = ty * SC_T, x0 = tx * SC_T, xs = x0 - g.pl - XOFF;
     const float* inb = in + (size_t)b * g.H * g.W * CIN;
 #pragma unroll
-    for (int u = 0; u < QPT; ++u) {
-      const int i = threadIdx.x + 256 * u;
-      v[u] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (i < NQ) {
-        const int r = i / RQ, q = i - r * RQ;
-        const int iy = y0 - g.pt + r;
-        if ((unsigned)iy < (unsigned)g.H) {
-          const float* row = inb + (size_t)iy * g.W * CIN;
-          const int f0 = 4 * q;
-          const int p0 = xs + f0 / CIN, p3 = xs + (f0 + 3) / CIN;
-          // vec_ok (host): every patch-row start is 16-B aligned in the tensor
-          if (vec_ok && p0 >= 0 && p3 < g.W) {
-            v[u] = *reinterpret_cast<const f32x4*>(row + (long long)xs * CIN + f0);
-          } else {
+    for (int u = 0; u < PPT; ++u) {
+      const int q = threadIdx.x + 256 * u;
+      const int r = q / SC_P, c = q - (q / SC_P) * SC_P;
+      const int iy = ty * SC_T - g.pt + r, ix = tx * SC_T - g.pl + c;
+      const bool ok = q < NPX && (unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W;
+      const float* src = inb + ((size_t)iy * g.W + ix) * CIN;
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const int px = xs + (f0 + e) / CIN;
-              if (px >= 0 && px < g.W) v[u][e] = row[(long long)xs * CIN + f0 + e];
-            }
-          }
-        }
-      }
+      for (int e = 0; e < CIN; ++e) v[u][e] = ok ? src[e] : 0.f;
     }
   };
 
-  f32x4 pre[QPT];
+  float pre[PPT][CIN];
   int t = blockIdx.x;
   if (t < ntiles) fetch(t, pre);
   for (; t < ntiles; t += gridDim.x) {
     const int tx = t % tilesX, tt = t / tilesX, ty = tt % tilesY, b = tt / tilesY;
-    const int y0 = ty * SC_T, x0 = tx * SC_T, xs = x0 - g.pl - XOFF;
-    // raw barriers with LDS-only waits: __syncthreads would also drain vmcnt, i.e. wait for
-    // the previous tile's global stores
+    const int y0 = ty * SC_T, x0 = tx * SC_T;
+    // raw barriers with LDS-only waits (__syncthreads would also drain the global stores)
     wait_lgkm0();
-    raw_barrier();  // every wave's reads of the previous patch are done
+    raw_barrier();
 #pragma unroll
-    for (int u = 0; u < QPT; ++u) {
-      const int i = threadIdx.x + 256 * u;
-      if (i < NQ) *reinterpret_cast<f32x4*>(patch + (i / RQ) * RS + 4 * (i % RQ)) = pre[u];
+    for (int u = 0; u < PPT; ++u) {
+      const int q = threadIdx.x + 256 * u;
+      if (q < NPX) {
+        if constexpr (F16) {
+          h4_t h;
+#pragma unroll
+          for (int c = 0; c < 4; ++c) h[c] = (half_t)(c < CIN ? pre[u][c] : 0.f);
+          *reinterpret_cast<h4_t*>(patch + 4 * q) = h;
+        } else {
+          f32x4 f;
+#pragma unroll
+          for (int c = 0; c < 4; ++c) f[c] = c < CIN ? pre[u][c] : 0.f;
+          *reinterpret_cast<f32x4*>(patch + 4 * q) = f;
+        }
+      }
     }
     wait_lgkm0();
     raw_barrier();
     if (t + (int)gridDim.x < ntiles) fetch(t + gridDim.x, pre);  // in flight during the MFMAs
 
     f32x4 acc[4];
-    float a[4][8];  // A values of the 4 M-tiles (output pixel (y0+y, x0+x) reads input pixel
-                    // x0+x-pl+kx = patch col x + kx + (x0 - pl - xs))
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-      const int wi = fr >> 2, pos = fr & 3;
-      const int y = 4 * wid + 2 * (i >> 1) + (pos >> 1);
-      const int x = 2 * (4 * (i & 1) + wi) + (pos & 1);
-      const int pbase = y * RS + (x + (x0 - g.pl - xs)) * CIN;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) a[i][j] = ao[j] >= 0 ? patch[pbase + ao[j]] : 0.f;
-    }
+    for (int i = 0; i < 4; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
     if constexpr (F16) {
-      h8_t bb;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) bb[j] = (half_t)wv[j];
+      for (int gq = 0; gq < 3; ++gq) {
+        const int tap = 4 * gq + fp;  // lane part fp
+        const int toff = tap < 9 ? (tap / 3) * SC_P + tap % 3 : 0;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        h8_t av;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) av[j] = (half_t)a[i][j];
-        acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av, bb, acc[i], 0, 0, 0);
+        for (int i = 0; i < 4; ++i) {
+          h4_t a = *reinterpret_cast<const h4_t*>(patch + 4 * (pix[i] + toff));
+          if (tap >= 9) a = h4_t{0, 0, 0, 0};
+          acc[i] = __builtin_amdgcn_mfma_f32_16x16x16f16(a, bw[gq], acc[i], 0, 0, 0);
+        }
       }
-    } else {  // 4 independent accumulation chains interleaved (dependent MFMA latency 40 cycles)
+    } else {
 #pragma unroll
-      for (int j = 0; j < 8; ++j)
+      for (int tap = 0; tap < 9; ++tap) {
+        const int toff = (tap / 3) * SC_P + tap % 3;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][j], wv[j], acc[i], 0, 0, 0);
+        for (int i = 0; i < 4; ++i)
+          acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(patch[4 * (pix[i] + toff) + fp], wv[tap], acc[i], 0, 0, 0);
+      }
     }
 
     // pool + epilogue into the wave's LDS stage, then 16-B coalesced stores
@@ -192,15 +201,10 @@ static int launch_conv0(const float* in, const float* w, OutT* out, const Direct
   // the next tile's patch prefetched into registers during the current tile's MFMAs)
   const int nt = (int)blocks;
   const dim3 grid((unsigned)(nt < 2048 ? nt : 2048));
-  // float4 patch rows when every row start (pixel x0 - pl - 3, x0 % 16 == 0) is 16-B aligned
-  const int vec_ok = ((g.W * cin) % 4 == 0 && ((long long)g.H * g.W * cin) % 4 == 0 && ((g.pl + 3) * cin) % 4 == 0 &&
-                      (reinterpret_cast<uintptr_t>(in) % 16) == 0)
-                         ? 1
-                         : 0;
   switch (cin) {
-    case 1: hipLaunchKernelGGL((conv0_mfma_pool_kernel<1, F16, OutT>), grid, dim3(256), 0, s, in, w, out, g, tilesX, tilesY, nt, vec_ok, epi); break;
-    case 2: hipLaunchKernelGGL((conv0_mfma_pool_kernel<2, F16, OutT>), grid, dim3(256), 0, s, in, w, out, g, tilesX, tilesY, nt, vec_ok, epi); break;
-    default: hipLaunchKernelGGL((conv0_mfma_pool_kernel<3, F16, OutT>), grid, dim3(256), 0, s, in, w, out, g, tilesX, tilesY, nt, vec_ok, epi); break;
+    case 1: hipLaunchKernelGGL((conv0_mfma_pool_kernel<1, F16, OutT>), grid, dim3(256), 0, s, in, w, out, g, tilesX, tilesY, nt, epi); break;
+    case 2: hipLaunchKernelGGL((conv0_mfma_pool_kernel<2, F16, OutT>), grid, dim3(256), 0, s, in, w, out, g, tilesX, tilesY, nt, epi); break;
+    default: hipLaunchKernelGGL((conv0_mfma_pool_kernel<3, F16, OutT>), grid, dim3(256), 0, s, in, w, out, g, tilesX, tilesY, nt, epi); break;
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
