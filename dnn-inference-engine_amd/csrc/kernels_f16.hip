@@ -20,8 +20,8 @@ static int check16(const char* what) {
 struct Cfg16Info {
   int bm, bn;
 };
-static const Cfg16Info kCfg16[GEMM16_NUM_CFGS] = {{128, 128}, {64, 128}, {32, 128}, {128, 64},
-                                                  {32, 64},   {128, 32}, {32, 32}};
+static const Cfg16Info kCfg16[GEMM16_NUM_CFGS] = {{128, 128}, {64, 128}, {32, 128}, {128, 64}, {32, 64},
+                                                  {128, 32},  {32, 32}};
 int gemm16_cfg_bn(int cfg) { return kCfg16[cfg].bn; }
 
 // Same rules as the fp32 chooser (kernels.hip): every config is the 32x32x16 f16 family with
@@ -46,14 +46,17 @@ template <int MODE>
 static int launch16(int cfg, const half_t* A, int lda, const half_t* Bt, int ldb, half_t* C, float* slab, int ldc,
                     int M, int N, int Kpad, const EpiParams& epi, int tilesN, const ImplicitConv& ic,
                     const SplitK& sk, dim3 grid, hipStream_t st) {
+  // 8 waves (two workgroups -> 4 waves per SIMD) on the 128- and 64-row tiles: the f16 GEMM
+  // is LDS/L2-latency bound, and 8 waves of 32x64 / 32x32 beat 4 of 64x64 / 32x64 by 13-15%
+  // on conv2-7 (MI355X, batch 64).  The wave layout does not change any summation order.
 #define DNN_L16(BM_, BN_, WM_, WN_, NS_)                                                                     \
   hipLaunchKernelGGL((gemm_f16_glds_kernel<BM_, BN_, WM_, WN_, NS_, MODE, half_t>), grid, dim3(WM_ * WN_ * 64), \
                      0, st, A, lda, Bt, ldb, C, slab, ldc, M, N, Kpad, epi, tilesN, ic, sk)
   switch (cfg) {
-    case GEMM16_128x128: DNN_L16(128, 128, 2, 2, 2); break;
-    case GEMM16_64x128: DNN_L16(64, 128, 2, 2, 2); break;
+    case GEMM16_128x128: DNN_L16(128, 128, 4, 2, 2); break;
+    case GEMM16_64x128: DNN_L16(64, 128, 2, 4, 2); break;
     case GEMM16_32x128_NS4: DNN_L16(32, 128, 1, 4, 4); break;
-    case GEMM16_128x64: DNN_L16(128, 64, 4, 1, 2); break;
+    case GEMM16_128x64: DNN_L16(128, 64, 4, 2, 2); break;
     case GEMM16_32x64_NS4: DNN_L16(32, 64, 1, 2, 4); break;
     case GEMM16_128x32: DNN_L16(128, 32, 4, 1, 2); break;
     case GEMM16_32x32_NS4: DNN_L16(32, 32, 1, 1, 4); break;
