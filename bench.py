@@ -57,6 +57,7 @@ def parse():
                     help="conv path precision (fp16 = BASELINE config 5: fp16 MFMA, fp32 accumulate)")
     ap.add_argument("--no-fp16", action="store_true", help="skip the embedded fp16 (config 5) measurement")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-frames end-to-end measurement")
+    ap.add_argument("--no-unfused", action="store_true", help="skip the explicit-im2col (unfused) plan measurement")
     ap.add_argument("--kernels", action="store_true", help="add the per-kernel table to the JSON")
     ap.add_argument("--gather", choices=("detections", "outputs"), default="detections",
                     help="per step, gather post-NMS detections (on-GPU postprocessing, the north star's "
@@ -249,6 +250,55 @@ def end_to_end(plan, B, dev, stream, steps=10, hw=(480, 640)):
             "ms_per_batch": round(dt / steps * 1e3, 3), "detections_last_batch": int(np.clip(r[1], 0, None).sum()),
             "note": "pinned host frames -> 8-bit upload (overlapped with the previous batch) -> GPU preprocess -> "
                     "forward -> postprocess -> detections on the host; PCIe-inclusive, not `value`"}
+
+
+def unfused_im2col(dnn_hip, yolo_graph, ws, dev, frames, stream, B, steps=5):
+    """The reference's structure (explicit im2col into a col buffer, GEMM, separate pools;
+    DNN_HIP_FUSE=0 at plan creation) on the same frames: per-kernel HBM GB/s of the im2col
+    kernels against the 8 TB/s peak (algorithmic bytes 4*(M*K written + B*H*W*C read),
+    SURVEY.md §8d) and the unfused forward rate beside the fused `value`."""
+    import torch
+    g, _ = yolo_graph.build_graph(dnn_hip.DnnGraphBuilder, ws, in_shape=(B, 416, 416, 3))
+    entries = dnn_hip.lower_graph(g)
+    old = os.environ.get("DNN_HIP_FUSE")
+    os.environ["DNN_HIP_FUSE"] = "0"
+    try:
+        wb, sb = dnn_hip.Plan.memory(B, (416, 416, 3), entries)
+        wbuf = torch.empty(wb, dtype=torch.uint8, device=dev)
+        sbuf = torch.empty(max(sb, 1), dtype=torch.uint8, device=dev)
+        pu = dnn_hip.Plan(B, (416, 416, 3), entries, device=dev.index, weights_ptr=wbuf.data_ptr(),
+                          workspace_ptr=sbuf.data_ptr())
+    finally:
+        if old is None:
+            del os.environ["DNN_HIP_FUSE"]
+        else:
+            os.environ["DNN_HIP_FUSE"] = old
+    y = torch.empty((B, 13, 13, 125), device=dev)
+    for _ in range(2):
+        pu.run_device(B, frames.data_ptr(), y.data_ptr(), stream)
+    torch.cuda.synchronize()
+    pu.timing_begin(steps)
+    for _ in range(steps):
+        pu.run_device(B, frames.data_ptr(), y.data_ptr(), stream)
+    ms, cnt = pu.timing_end()
+    kinfo = pu.kernels()
+    im2col, tot_b, tot_s = {}, 0.0, 0.0
+    for k, m, c in zip(kinfo, ms, cnt):
+        if not k["name"].endswith(".im2col"):
+            continue
+        sec = m / max(c, 1) / 1e3
+        gbs = k["bytes"] / sec / 1e9
+        im2col[k["name"]] = {"ms": round(sec * 1e3, 4), "gbs": round(gbs, 1),
+                             "frac_hbm_peak": round(gbs / HBM_PEAK_GBS, 4), "bytes": int(k["bytes"])}
+        tot_b += k["bytes"]
+        tot_s += sec
+    fwd_ms = sum(m / max(c, 1) for m, c in zip(ms, cnt))
+    pu.close()
+    return {"im2col": im2col, "im2col_total": {"ms": round(tot_s * 1e3, 4), "gbs": round(tot_b / tot_s / 1e9, 1),
+                                               "frac_hbm_peak": round(tot_b / tot_s / 1e9 / HBM_PEAK_GBS, 4)},
+            "unfused_forward_ms": round(fwd_ms, 4), "unfused_images_per_s": round(B / (fwd_ms / 1e3), 1),
+            "note": "DNN_HIP_FUSE=0 plan (explicit im2col + GEMM + separate pools, the reference's "
+                    "structure), kernel time sum; the default plan uses implicit GEMM (no col buffer)"}
 
 
 def fp16_config(dnn_hip, yolo_graph, ws, dev, frames, out32, plan32, stream, B, steps=20):
@@ -454,6 +504,8 @@ def main():
         res["latency_b1"] = latency_b1(dnn_hip, yolo_graph, ws, dev)
     if rank == 0 and world == 1 and not args.no_e2e:
         res["end_to_end_host_frames"] = end_to_end(plan, B, dev, stream)
+    if rank == 0 and world == 1 and args.precision == "fp32" and not args.no_unfused:
+        res["unfused"] = unfused_im2col(dnn_hip, yolo_graph, ws, dev, frames, stream, B)
     if rank == 0 and world == 1 and args.precision == "fp32" and not args.no_fp16:
         res["fp16"] = fp16_config(dnn_hip, yolo_graph, ws, dev, frames, runner.out, plan, stream, B)
     if rank == 0:

@@ -32,86 +32,116 @@ static int check_launch(const char* what) {
 }
 
 // ============================================================================ im2col
-// One block = IM2COL_ROWS consecutive output pixels (rows of col). Per-row window origins
-// and per-K-column tap offsets are tabulated in LDS once per block, so the streaming loop
-// does no integer division by layer constants. Writes are fully coalesced (a block writes
-// IM2COL_ROWS*Kpad contiguous floats); reads are contiguous runs of ic floats per tap.
-constexpr int IM2COL_ROWS = 32;
+// 2-D grid: blockIdx.y = a chunk of <= IM2COL_KCH K columns, blockIdx.x = `rows` consecutive
+// output pixels (rows of col), sized so one block moves ~16 KB.  Per-column tap offsets and
+// per-row window origins are tabulated in LDS once per block, so the streaming loop does no
+// integer division by layer constants.  Every thread stores float4s (coalesced row segments of
+// the col matrix); when C % 4 == 0 a float4 is one vector load of 4 channels of one tap, else
+// (conv0, C = 3) four scalar gathers.  Pure HBM stream: 4*(M*K) B written + the input read.
 constexpr int IM2COL_THREADS = 256;
-constexpr int IM2COL_MAX_KQ = 2560;  // Kpad/VEC entries of the tap table (Kpad <= 10240)
+constexpr int IM2COL_KCH = 1024;      // K columns per block
+constexpr int IM2COL_MAX_ROWS = 256;  // rows per block
+constexpr int IM2COL_BLOCK_FLOATS = 4096 * 4;
+constexpr int IM2COL_ILP = 4;
 
-template <int VEC>
+template <bool VEC>
 __global__ void __launch_bounds__(IM2COL_THREADS)
-im2col_nhwc_kernel(const float* __restrict__ in, float* __restrict__ col, ConvGeom g, long long M) {
-  __shared__ int s_off[IM2COL_MAX_KQ];   // (dy*W + dx)*C + c relative to the window origin
-  __shared__ int s_dydx[IM2COL_MAX_KQ];  // (dy << 16) | dx, or -1 for K padding columns
-  __shared__ long long s_base[IM2COL_ROWS];
-  __shared__ int s_iy[IM2COL_ROWS];
-  __shared__ int s_ix[IM2COL_ROWS];
+im2col_nhwc_kernel(const float* __restrict__ in, float* __restrict__ col, ConvGeom g, long long M, int rows) {
+  __shared__ int s_off[IM2COL_KCH];   // (dy*W + dx)*C + c relative to the window origin
+  __shared__ int s_dydx[IM2COL_KCH];  // (dy << 16) | dx, or -1 for K padding columns
+  __shared__ long long s_base[IM2COL_MAX_ROWS];
+  __shared__ int s_iy[IM2COL_MAX_ROWS];
+  __shared__ int s_ix[IM2COL_MAX_ROWS];
 
-  const int kq = g.Kpad / VEC;
-  for (int k4 = threadIdx.x; k4 < kq; k4 += IM2COL_THREADS) {
-    int k = k4 * VEC;
+  const int k0 = blockIdx.y * IM2COL_KCH;
+  const int kn = g.Kpad - k0 < IM2COL_KCH ? g.Kpad - k0 : IM2COL_KCH;  // multiple of 4
+  const int kq = kn >> 2;
+  const int nent = VEC ? kq : kn;  // table entries: per float4 (VEC) or per column
+  for (int e = threadIdx.x; e < nent; e += IM2COL_THREADS) {
+    const int k = k0 + (VEC ? 4 * e : e);
     if (k < g.K) {
-      int tap = k / g.C, c = k - tap * g.C;
-      int dy = tap / g.kw, dx = tap - dy * g.kw;
-      s_off[k4] = (dy * g.W + dx) * g.C + c;
-      s_dydx[k4] = (dy << 16) | dx;
+      const int tap = k / g.C, c = k - tap * g.C;
+      const int dy = tap / g.kw, dx = tap - dy * g.kw;
+      s_off[e] = (dy * g.W + dx) * g.C + c;
+      s_dydx[e] = (dy << 16) | dx;
     } else {
-      s_off[k4] = 0;
-      s_dydx[k4] = -1;
+      s_off[e] = 0;
+      s_dydx[e] = -1;
     }
   }
-  const long long m0 = (long long)blockIdx.x * IM2COL_ROWS;
-  if (threadIdx.x < IM2COL_ROWS) {
-    long long m = m0 + threadIdx.x;
+  const long long m0 = (long long)blockIdx.x * rows;
+  for (int r = threadIdx.x; r < rows; r += IM2COL_THREADS) {
+    long long m = m0 + r;
     if (m >= M) m = M - 1;
-    int ox = (int)(m % g.OW);
-    long long t = m / g.OW;
-    int oy = (int)(t % g.OH);
-    int b = (int)(t / g.OH);
-    int iy0 = oy * g.sh - g.pt, ix0 = ox * g.sw - g.pl;
-    s_iy[threadIdx.x] = iy0;
-    s_ix[threadIdx.x] = ix0;
-    s_base[threadIdx.x] = (((long long)b * g.H + iy0) * g.W + ix0) * g.C;
+    const int ox = (int)(m % g.OW);
+    const long long t = m / g.OW;
+    const int oy = (int)(t % g.OH);
+    const int b = (int)(t / g.OH);
+    const int iy0 = oy * g.sh - g.pt, ix0 = ox * g.sw - g.pl;
+    s_iy[r] = iy0;
+    s_ix[r] = ix0;
+    s_base[r] = (((long long)b * g.H + iy0) * g.W + ix0) * g.C;
   }
   __syncthreads();
 
-  const int rows = (int)((M - m0) < IM2COL_ROWS ? (M - m0) : IM2COL_ROWS);
-  const int total = rows * kq;
-  float* dst = col + m0 * g.Kpad;
-  for (int idx = threadIdx.x; idx < total; idx += IM2COL_THREADS) {
-    int r = idx / kq;
-    int k4 = idx - r * kq;
-    int dd = s_dydx[k4];
-    int iy = s_iy[r] + (dd >> 16);
-    int ix = s_ix[r] + (dd & 0xffff);
-    bool ok = dd >= 0 && (unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W;
-    const float* src = in + s_base[r] + s_off[k4];
-    if constexpr (VEC == 4) {
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (ok) v = *reinterpret_cast<const float4*>(src);
-      reinterpret_cast<float4*>(dst)[idx] = v;
-    } else {
-      dst[idx] = ok ? *src : 0.f;
+  const int nrows = (int)((M - m0) < rows ? (M - m0) : rows);
+  const int total = nrows * kq;
+  // IM2COL_ILP independent gathers in flight per thread before their stores
+  for (int base = threadIdx.x; base < total; base += IM2COL_ILP * IM2COL_THREADS) {
+    float4 v[IM2COL_ILP];
+    int dsto[IM2COL_ILP];
+#pragma unroll
+    for (int u = 0; u < IM2COL_ILP; ++u) {
+      const int idx = base + u * IM2COL_THREADS;
+      v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+      dsto[u] = -1;
+      if (idx < total) {
+        const int r = idx / kq;
+        const int j = idx - r * kq;
+        const int iy0 = s_iy[r], ix0 = s_ix[r];
+        const float* src = in + s_base[r];
+        dsto[u] = r * g.Kpad + 4 * j;
+        if constexpr (VEC) {
+          const int dd = s_dydx[j];
+          const int iy = iy0 + (dd >> 16), ix = ix0 + (dd & 0xffff);
+          if (dd >= 0 && (unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W)
+            v[u] = *reinterpret_cast<const float4*>(src + s_off[j]);
+        } else {
+          float x[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int dd = s_dydx[4 * j + q];
+            const int iy = iy0 + (dd >> 16), ix = ix0 + (dd & 0xffff);
+            const bool ok = dd >= 0 && (unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W;
+            x[q] = ok ? src[s_off[4 * j + q]] : 0.f;
+          }
+          v[u] = make_float4(x[0], x[1], x[2], x[3]);
+        }
+      }
     }
+    float* dst = col + m0 * g.Kpad + k0;
+#pragma unroll
+    for (int u = 0; u < IM2COL_ILP; ++u)
+      if (dsto[u] >= 0) *reinterpret_cast<float4*>(dst + dsto[u]) = v[u];
   }
 }
 
 int launch_im2col(const float* in, float* col, const ConvGeom& g, hipStream_t stream) {
   long long M = (long long)g.B * g.OH * g.OW;
   if (M == 0) return 0;
-  const bool vec = (g.C % 4) == 0 && (g.Kpad % 4) == 0;
-  const int kq = vec ? g.Kpad / 4 : g.Kpad;
-  if (kq > IM2COL_MAX_KQ) {
-    set_error("im2col: Kpad=%d exceeds the tap table (%d)", g.Kpad, IM2COL_MAX_KQ * (vec ? 4 : 1));
+  if (g.Kpad % 4 != 0 || g.Kpad < g.K) {
+    set_error("im2col: Kpad=%d must be a multiple of 4 and >= K=%d", g.Kpad, g.K);
     return -2;
   }
-  dim3 grid(ceil_div_i(M, IM2COL_ROWS));
+  const bool vec = (g.C % 4) == 0;
+  const int kch = g.Kpad < IM2COL_KCH ? g.Kpad : IM2COL_KCH;
+  int rows = IM2COL_BLOCK_FLOATS / kch;
+  rows = rows < 1 ? 1 : (rows > IM2COL_MAX_ROWS ? IM2COL_MAX_ROWS : rows);
+  dim3 grid(ceil_div_i(M, rows), ceil_div_i(g.Kpad, IM2COL_KCH));
   if (vec)
-    hipLaunchKernelGGL(im2col_nhwc_kernel<4>, grid, dim3(IM2COL_THREADS), 0, stream, in, col, g, M);
+    hipLaunchKernelGGL(im2col_nhwc_kernel<true>, grid, dim3(IM2COL_THREADS), 0, stream, in, col, g, M, rows);
   else
-    hipLaunchKernelGGL(im2col_nhwc_kernel<1>, grid, dim3(IM2COL_THREADS), 0, stream, in, col, g, M);
+    hipLaunchKernelGGL(im2col_nhwc_kernel<false>, grid, dim3(IM2COL_THREADS), 0, stream, in, col, g, M, rows);
   return check_launch("im2col");
 }
 

@@ -1,6 +1,6 @@
 export TMPDIR=/tmp; R=$GRAFT_REPO_ROOT; mkdir -p $R/gpurun_out
 cd /tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_r1c -o trace --output-format csv -- python3 $R/bench.py --steps 10 --warmup 3 --no-cpu --no-latency --no-fp16 > $R/gpurun_out/prof_bench.log 2>&1 || exit 1
-timeout -k 10 240 rocprofv3 --pmc FETCH_SIZE -d $R/gpurun_out/pmc_fetch_c -o fetch --output-format csv -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu --no-latency --no-fp16 > $R/gpurun_out/pmc_fetch.log 2>&1 || exit 1
-timeout -k 10 240 rocprofv3 --pmc WRITE_SIZE -d $R/gpurun_out/pmc_write_c -o write --output-format csv -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu --no-latency --no-fp16 > $R/gpurun_out/pmc_write.log 2>&1 || exit 1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_r1c -o trace --output-format csv -- python3 $R/bench.py --steps 10 --warmup 3 --no-cpu --no-latency --no-fp16 --no-unfused > $R/gpurun_out/prof_bench.log 2>&1 || exit 1
+timeout -k 10 240 rocprofv3 --pmc FETCH_SIZE -d $R/gpurun_out/pmc_fetch_c -o fetch --output-format csv -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu --no-latency --no-fp16 --no-unfused > $R/gpurun_out/pmc_fetch.log 2>&1 || exit 1
+timeout -k 10 240 rocprofv3 --pmc WRITE_SIZE -d $R/gpurun_out/pmc_write_c -o write --output-format csv -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu --no-latency --no-fp16 --no-unfused > $R/gpurun_out/pmc_write.log 2>&1 || exit 1
 echo ALLOK
