@@ -359,10 +359,15 @@ def main():
     import yolo_graph
 
     rank, local_rank, world = D.env_rank()
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    # rehearsal switches for a one-GPU box (never set by the driver): every rank on cuda:0
+    # and gloo (host-staged collectives) instead of RCCL, so --gpus 2 exercises the relaunch,
+    # weight broadcast, sharding, detection gather and max-over-ranks timing end to end
+    gpu = 0 if os.environ.get("DNN_BENCH_SHARED_GPU") == "1" else local_rank
+    backend = os.environ.get("DNN_BENCH_BACKEND", "nccl")
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
     if world > 1:
-        D.init("nccl", device=dev)
+        D.init(backend, device=dev)
 
     B = args.batch
     # rank 0 holds the weights; the other ranks only lay the plan out and receive the
@@ -373,7 +378,7 @@ def main():
     wbytes, sbytes = dnn_hip.Plan.memory(B, (416, 416, 3), entries, precision=args.precision)
     wbuf = torch.empty(wbytes, dtype=torch.uint8, device=dev)
     sbuf = torch.empty(max(sbytes, 1), dtype=torch.uint8, device=dev)
-    plan = dnn_hip.Plan(B, (416, 416, 3), entries, device=local_rank, weights_ptr=wbuf.data_ptr(),
+    plan = dnn_hip.Plan(B, (416, 416, 3), entries, device=gpu, weights_ptr=wbuf.data_ptr(),
                         workspace_ptr=sbuf.data_ptr(), upload=(rank == 0), precision=args.precision)
     torch.cuda.synchronize()
     D.broadcast_weights(wbuf, src=0)
@@ -489,6 +494,7 @@ def main():
                           "net_pct_fp32_peak": round(100 * 6.971e9 * value / world / 1e12 / FP32_MFMA_PEAK_TFLOPS,
                                                      2)},
             "kernel_ms_per_step": round(total_kernel_ms, 4),
+            "dist_backend": ("rccl" if backend == "nccl" else backend) if world > 1 else None,
         }
         if args.gather == "detections":
             res["postprocess"] = {"ms": round(post_ms, 4), "detections_last_step": n_det,

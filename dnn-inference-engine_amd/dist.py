@@ -49,11 +49,44 @@ def init(backend, device=None):
     return dist.get_rank(), dist.get_world_size()
 
 
+def _host_staged(t):
+    """gloo runs collectives on host memory: with device tensors (the one-GPU multi-rank
+    rehearsal, DNN_BENCH_BACKEND=gloo) each collective goes through a CPU copy.  RCCL
+    ("nccl") works on the device tensors directly."""
+    return t.is_cuda and dist.get_backend() == "gloo"
+
+
 def broadcast_weights(buf, src=0):
     """Broadcast a flat weight tensor in place from `src` (once, at start-up)."""
     if dist.is_initialized() and dist.get_world_size() > 1:
-        dist.broadcast(buf, src=src)
+        if _host_staged(buf):
+            h = buf.cpu()
+            dist.broadcast(h, src=src)
+            buf.copy_(h)
+        else:
+            dist.broadcast(buf, src=src)
     return buf
+
+
+def _gather(t, parts, dst):
+    if _host_staged(t):
+        hp = [torch.empty(p.shape, dtype=p.dtype) for p in parts] if parts is not None else None
+        dist.gather(t.cpu(), hp, dst=dst)
+        if parts is not None:
+            for p, h in zip(parts, hp):
+                p.copy_(h)
+    else:
+        dist.gather(t, parts, dst=dst)
+
+
+def _all_gather(parts, t):
+    if _host_staged(t):
+        hp = [torch.empty(p.shape, dtype=p.dtype) for p in parts]
+        dist.all_gather(hp, t.cpu())
+        for p, h in zip(parts, hp):
+            p.copy_(h)
+    else:
+        dist.all_gather(parts, t)
 
 
 def gather_outputs(local, dst=0):
@@ -64,7 +97,7 @@ def gather_outputs(local, dst=0):
         return local
     rank, world = dist.get_rank(), dist.get_world_size()
     parts = [torch.empty_like(local) for _ in range(world)] if rank == dst else None
-    dist.gather(local, parts, dst=dst)
+    _gather(local, parts, dst)
     return torch.cat(parts, 0) if rank == dst else None
 
 
@@ -85,7 +118,7 @@ def gather_detections(packed, total, counts, n, dst=0):
     rank, world = dist.get_rank(), dist.get_world_size()
     dev = packed.device
     sizes = [torch.zeros(2, dtype=torch.int64, device=dev) for _ in range(world)]
-    dist.all_gather(sizes, torch.tensor([p, n], dtype=torch.int64, device=dev))
+    _all_gather(sizes, torch.tensor([p, n], dtype=torch.int64, device=dev))
     sizes = [tuple(int(v) for v in t.cpu()) for t in sizes]
     pmax, nmax = max(max(sz[0] for sz in sizes), 1), max(max(sz[1] for sz in sizes), 1)
     if packed.shape[0] >= pmax:
@@ -97,8 +130,8 @@ def gather_detections(packed, total, counts, n, dst=0):
     cbuf[:n] = counts[:n]
     pparts = [torch.empty_like(pbuf) for _ in range(world)] if rank == dst else None
     cparts = [torch.empty_like(cbuf) for _ in range(world)] if rank == dst else None
-    dist.gather(pbuf, pparts, dst=dst)
-    dist.gather(cbuf, cparts, dst=dst)
+    _gather(pbuf, pparts, dst)
+    _gather(cbuf, cparts, dst)
     if rank != dst:
         return None
     d = torch.cat([pparts[r][:sizes[r][0]] for r in range(world)], 0).cpu().numpy()
