@@ -395,20 +395,40 @@ def main():
     runner = D.ShardedRunner(compute, B * world, (416, 416, 3), (13, 13, 125), dev)
     if args.gather == "detections":
         import yolo_post
-        dbuf = yolo_post.DetectionBuffers(runner.shard_cap, dev)
+        dbufs = [yolo_post.DetectionBuffers(runner.shard_cap, dev) for _ in range(2)]
+        dbuf = dbufs[0]
 
-        def post(out, n):
-            dbuf.run(out.data_ptr(), n, stream)
-            return dbuf.pack(n, stream)
+        def post(out, n, slot):
+            dbufs[slot].run(out.data_ptr(), n, stream)
+            return dbufs[slot].pack(n, stream)
+
+        # two steps in flight: step k+1's forward is enqueued before step k's detections are
+        # collected (side stream), so the host sync, D2H and gathers overlap the GPU's work;
+        # the last step is collected before the clock stops
+        pending = []
 
         def one_step():
-            return runner.step_detections(frames, post)
+            pending.append(runner.launch_detections(frames, post, one_step.k & 1))
+            one_step.k += 1
+            return runner.finish_detections(pending.pop(0)) if len(pending) == 2 else None
+
+        one_step.k = 0
+
+        def drain():
+            r = None
+            while pending:
+                r = runner.finish_detections(pending.pop(0))
+            return r
     else:
         def one_step():
             return runner.step(frames)
 
+        def drain():
+            return None
+
     for _ in range(args.warmup):
         one_step()
+    drain()
     torch.cuda.synchronize()
     if world > 1:
         tdist.barrier()
@@ -418,8 +438,12 @@ def main():
     if world > 1:
         tdist.barrier()
     t0 = time.perf_counter()
+    full = None
     for _ in range(args.steps):
-        full = one_step()
+        r = one_step()
+        full = r if r is not None else full
+    r = drain()
+    full = r if r is not None else full
     torch.cuda.synchronize()
     if world > 1:
         tdist.barrier()

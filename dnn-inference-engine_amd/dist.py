@@ -191,6 +191,38 @@ class ShardedRunner(object):
             rows.append(full[r * self.shard_cap:r * self.shard_cap + c])
         return torch.cat(rows, 0)
 
+    def launch_detections(self, local_in, post, slot):
+        """Pipelined form of step_detections, first half: enqueue the forward, `post(out, n,
+        slot)` and the pack for this rank's shard into output slot `slot` (0/1) on the current
+        stream without waiting; returns a handle for finish_detections.  The slot's previous
+        gather must have been finished (its reads are ordered before this launch)."""
+        if not hasattr(self, "_outs"):
+            self._outs = [self.out, torch.zeros_like(self.out)]
+            self._side = torch.cuda.Stream(self.out.device)
+            self._freed = [None, None]
+        cur = torch.cuda.current_stream(self.out.device)
+        if self._freed[slot] is not None:
+            cur.wait_event(self._freed[slot])
+        out = self._outs[slot]
+        self.compute(local_in, out, self.count)
+        packed, total, counts = post(out, self.count, slot)
+        ready = torch.cuda.Event()
+        ready.record(cur)
+        return slot, packed, total, counts, ready
+
+    def finish_detections(self, handle):
+        """Second half: on a side stream that waits only for that step's pack (so later steps
+        already enqueued keep the GPU busy), read the row count and gather the packed
+        detections (as gather_detections).  Returns what step_detections returns."""
+        slot, packed, total, counts, ready = handle
+        with torch.cuda.stream(self._side):
+            self._side.wait_event(ready)
+            r = gather_detections(packed, total, counts, self.count)
+            freed = torch.cuda.Event()
+            freed.record(self._side)
+        self._freed[slot] = freed
+        return r
+
     def step_detections(self, local_in, post):
         """One batch ending in detections: local compute, then `post(out, n)` -> (packed
         [rows, 40] uint8, total [1] int32, counts [cap] int32) on this rank's device (the
