@@ -36,7 +36,7 @@ for _i in range(9):
 
 # every kernel of the plan lives in namespace dnnhip; weight packing (finalize) and the
 # postprocessing kernels (after the forward) are not plan kernels
-_NOT_PLAN = ("pack_weights", "yolo_", "f32_to_f16_kernel")
+_NOT_PLAN = ("pack_weights", "yolo_", "f32_to_f16_kernel", "preprocess_kernel")
 
 
 def _ours(name):
@@ -63,7 +63,9 @@ def dispatch_sequence(rows, key_start="Start_Timestamp", key_end="End_Timestamp"
     return out
 
 
-def summarise(trace=None, fetch=None, write=None):
+def summarise(trace=None, fetch=None, write=None, skip=0):
+    """skip: leading (warm-up) dispatches per plan kernel left out of avg_us / median_us
+    (bench.py's roofline averages only its timed steps); avg_all_us keeps every call."""
     res = defaultdict(lambda: {"calls": 0})
     if trace:
         rows = list(csv.DictReader(open(trace)))
@@ -88,9 +90,12 @@ def summarise(trace=None, fetch=None, write=None):
             continue
         d = dict(res[pk])
         if "_ns" in d:
-            ns = sorted(d.pop("_ns"))
+            allns = d.pop("_ns")
+            ns = sorted(allns[skip:] if len(allns) > skip else allns)
             d["avg_us"] = round(sum(ns) / len(ns) / 1e3, 2)
             d["median_us"] = round(ns[len(ns) // 2] / 1e3, 2)
+            d["avg_all_us"] = round(sum(allns) / len(allns) / 1e3, 2)
+            d["timed_calls"] = len(ns)
         for key in ("FETCH_SIZE", "WRITE_SIZE"):
             v = d.pop("_" + key, None)
             if v:
@@ -108,6 +113,7 @@ def main():
     ap.add_argument("--write")
     ap.add_argument("--out")
     ap.add_argument("--note", default="")
+    ap.add_argument("--skip", type=int, default=0, help="warm-up dispatches per kernel to leave out of avg_us")
     ap.add_argument("--unfused", action="store_true", help="trace of a DNN_HIP_FUSE=0 run")
     ap.add_argument("--fp16", action="store_true", help="trace of a --precision fp16 run")
     a = ap.parse_args()
@@ -115,7 +121,7 @@ def main():
         ORDER[:] = ORDER_UNFUSED
     if a.fp16:
         ORDER[:] = ORDER_FP16
-    s = summarise(a.trace, a.fetch, a.write)
+    s = summarise(a.trace, a.fetch, a.write, a.skip)
     doc = {"note": a.note or __doc__.strip().splitlines()[0], "kernels": s}
     text = json.dumps(doc, indent=1)
     if a.out:
