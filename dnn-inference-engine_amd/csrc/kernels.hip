@@ -167,12 +167,13 @@ int choose_gemm_cfg(long long M, int N, int K) {
   if (N <= 32) return GEMM_256x32_K16;
   if (N <= 64) return GEMM_128x64_K32;
   // 128x128 tiles (2 per CU) when the long K split into choose_splitk(N, K) parts still gives
-  // at least 512 work units; else 64x128 (3 per CU).  Both are the 32x32x2 family with the same
+  // at least 512 work units; else 64x128 (3 per CU).  (K >= 1024: conv4 at batch 64 measured
+  // 0.252 -> 0.240 ms with 128x128; conv3, K = 576, is faster on 64x128.)  Both are the 32x32x2 family with the same
   // K permutation, and the split itself depends on (N, K) only, so the summation order of an
   // output element never depends on M.
   long long t128 = ((M + 127) / 128) * ((N + 127) / 128);
   const int s = choose_splitk(N, K);
-  if (K >= 2048 && t128 * s >= 512) return GEMM_128x128_K32;
+  if (K >= 1024 && t128 * s >= 512) return GEMM_128x128_K32;
   // small M (batch 1 and the like): 64x128 would leave most CUs idle and each workgroup
   // waiting on a 2-stage ring; 32-row tiles with a 4-stage ring (same family, same K order)
   long long t64 = ((M + 63) / 64) * ((N + 127) / 128);

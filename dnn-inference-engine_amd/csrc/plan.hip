@@ -240,6 +240,15 @@ static void set_cfg(dnn_plan* p, PlanLayer& L) {
     return;
   }
   L.cfg = L.mode == MODE_IMPLICIT ? choose_gemm_cfg_implicit(M, L.OC, L.K) : choose_gemm_cfg(M, L.OC, L.K);
+  if (const char* e = getenv("DNN_HIP_CFG")) {  // tuning experiments: "K:cfg,K:cfg,..."
+    for (const char* q = e; *q;) {
+      int k = 0, c = 0, n = 0;
+      if (sscanf(q, "%d:%d%n", &k, &c, &n) != 2) break;
+      if (k == L.K && c >= GEMM_128x128_K32 && c < GEMM_NUM_CFGS && c != GEMM_G64x32_K32) L.cfg = c;
+      q += n;
+      if (*q == ',') ++q;
+    }
+  }
   L.Kpad = (int)align_up(L.K, gemm_cfg_bk(L.cfg));
   L.Npad = (int)align_up(L.OC, gemm_cfg_bn(L.cfg));
   L.splits = (L.cfg >= GEMM_128x128_K32 && L.Kpad == L.K) ? choose_splitk(L.OC, L.K) : 1;
