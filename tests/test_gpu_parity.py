@@ -239,6 +239,7 @@ IMPLICIT_CASES = [
     (4, 16, 16, 64, 128, True),    # conv3-like
     (2, 13, 11, 128, 256, False),  # conv5-like, no pool
     (1, 9, 9, 16, 125, False),     # ragged N
+    (64, 26, 26, 128, 256, True),  # conv4 at batch 64: K = 1152 -> 128x128 tile with the fused pool
 ]
 
 
@@ -265,6 +266,21 @@ def test_implicit_gemm_and_fused_pool_vs_explicit_bit_exact(monkeypatch, case):
         assert ("+pool2x2s2" in desc) == (fuse == "1" and pool)
     assert np.array_equal(outs["1"], outs["0"])
     assert R.normwise_err(outs["1"], _oracle_chain(x, k, **kw)) < LAYER_TOL
+
+
+@pytest.mark.parametrize("fuse", ["1", "0"])
+def test_empty_batch(monkeypatch, fuse):
+    """A batch of 0 frames runs (no launches) and returns an empty [0, oh, ow, od] array, as the
+    reference's numpy engines do."""
+    monkeypatch.setenv("DNN_HIP_FUSE", fuse)
+    rng = np.random.default_rng(5)
+    k = rng.standard_normal((3, 3, 16, 32)).astype(np.float32)
+    x = np.zeros((0, 12, 10, 16), dtype=np.float32)
+    bn = (np.zeros(32, np.float32), np.ones(32, np.float32), np.ones(32, np.float32))
+    eng = dnn_hip.DnnInferenceEngine(_chain(x.shape, k, bias=np.zeros(32, np.float32), bn=bn, leaky=True,
+                                            pool=(2, 2, "SAME")), False)
+    out = eng.run(x)
+    assert out.shape == (0, 6, 5, 32) and out.dtype == np.float32
 
 
 PATCH_CASES = [
