@@ -81,7 +81,9 @@ enum GemmCfg : int {
   GEMM_G256x64_K32 = 6,  // N <= 64 implicit conv: LDS-DMA 2-stage ring, 256x64 tile, 8 waves, MFMA 32x32x2
   GEMM_G32x128_NS4 = 7,  // N >= 128, small M (batch 1): LDS-DMA 4-stage ring, 32x128 tile, MFMA 32x32x2
   GEMM_G32x64_NS4 = 8,   // N <= 64 implicit conv, small M: LDS-DMA 4-stage ring, 32x64 tile, 2 waves
-  GEMM_NUM_CFGS = 9,
+  GEMM_128x256_W8 = 9,   // split-K layers, N % 256 == 0: 128x256, 8 waves of 64x64, one workgroup per CU
+  GEMM_128x512_W16 = 10, // split-K layers, N % 512 == 0 (conv5-7): 128x512, 16 waves of 64x64, 160 KB LDS
+  GEMM_NUM_CFGS = 11,
 };
 int gemm_cfg_bm(int cfg);
 int gemm_cfg_bn(int cfg);

@@ -150,7 +150,7 @@ struct CfgInfo {
 };
 static const CfgInfo kCfgs[GEMM_NUM_CFGS] = {{256, 16, 32}, {256, 32, 16}, {128, 64, 32}, {128, 128, 32},
                                              {64, 128, 32},  {64, 32, 32},  {256, 64, 32}, {32, 128, 32},
-                                             {32, 64, 32}};
+                                             {32, 64, 32},   {128, 256, 32}, {128, 512, 32}};
 
 int gemm_cfg_bm(int cfg) { return kCfgs[cfg].bm; }
 int gemm_cfg_bn(int cfg) { return kCfgs[cfg].bn; }
@@ -173,7 +173,15 @@ int choose_gemm_cfg(long long M, int N, int K) {
   // output element never depends on M.
   long long t128 = ((M + 127) / 128) * ((N + 127) / 128);
   const int s = choose_splitk(N, K);
-  if (K >= 1024 && t128 * s >= 512) return GEMM_128x128_K32;
+  if (K >= 1024 && t128 * s >= 512) {
+    // split-K layers (conv5-7): one wide workgroup per CU with 16 / 8 waves of 64x64 stages
+    // 80 / 96 B per MFMA instead of 128 (128x128): less LDS-DMA and L2 traffic per flop, which
+    // keeps the power-limited clock up (batch 64: conv5 0.239 -> 0.216, conv6 0.855 -> 0.812,
+    // conv7 1.632 -> 1.59 ms).  Same MFMA family and K order: results are unchanged bit for bit.
+    if (s > 1 && N % 512 == 0) return GEMM_128x512_W16;
+    if (s > 1 && N % 256 == 0) return GEMM_128x256_W8;
+    return GEMM_128x128_K32;
+  }
   // small M (batch 1 and the like): 64x128 would leave most CUs idle and each workgroup
   // waiting on a 2-stage ring; 32-row tiles with a 4-stage ring (same family, same K order)
   long long t64 = ((M + 63) / 64) * ((N + 127) / 128);
@@ -232,6 +240,14 @@ static int launch_glds(int cfg, const float* A, int lda, const float* Bt, int ld
       break;
     case GEMM_G32x64_NS4:
       hipLaunchKernelGGL((gemm_f32_glds_kernel<32, 64, 1, 2, 32, 4, MODE>), grid, dim3(128), 0, stream, A, lda,
+                         Bt, ldb, C, ldc, m, N, Kpad, epi, tilesN, ic, sk);
+      break;
+    case GEMM_128x256_W8:
+      hipLaunchKernelGGL((gemm_f32_glds_kernel<128, 256, 2, 4, 32, 2, MODE>), grid, dim3(512), 0, stream, A, lda,
+                         Bt, ldb, C, ldc, m, N, Kpad, epi, tilesN, ic, sk);
+      break;
+    case GEMM_128x512_W16:
+      hipLaunchKernelGGL((gemm_f32_glds_kernel<128, 512, 2, 8, 32, 2, MODE>), grid, dim3(1024), 0, stream, A, lda,
                          Bt, ldb, C, ldc, m, N, Kpad, epi, tilesN, ic, sk);
       break;
     default:
