@@ -457,13 +457,19 @@ gemm_f32_glds_kernel(const float* __restrict__ A, int lda, const float* __restri
   }
   const long long rowstride = (long long)ic.W * ic.C;
 
+  const bool aligned = MODE != 0 && (ic.C % BK) == 0;  // wave-uniform
   auto issue = [&](int stage, int k0) {
     float* base = smem + stage * STAGE;
+    const long long tap_off = MODE != 0 ? (long long)dyb * rowstride + (long long)dxb * ic.C + cb : 0;
 #pragma unroll
     for (int i = 0; i < LPSA; ++i) {
       const float* s;
       if constexpr (MODE == 0) {
         s = srcA[i] + k0;
+      } else if (aligned) {
+        // C % 32 == 0: the K-step is 32 channels of ONE tap, so the source is the lane's
+        // pixel + a wave-uniform offset, gated by one bit of the lane's tap mask
+        s = ((maskA[i] >> tapb) & 1) ? srcA[i] + tap_off + lsA[i] : ic.zero;
       } else {
         const int e = cb + lsA[i];
         const bool nx = e >= ic.C;
