@@ -398,9 +398,9 @@ def main():
         dbufs = [yolo_post.DetectionBuffers(runner.shard_cap, dev) for _ in range(2)]
         dbuf = dbufs[0]
 
-        def post(out, n, slot):
-            dbufs[slot].run(out.data_ptr(), n, stream)
-            return dbufs[slot].pack(n, stream)
+        def post(out, n, slot, post_stream):
+            dbufs[slot].run(out.data_ptr(), n, post_stream)
+            return dbufs[slot].pack(n, post_stream)
 
         # two steps in flight: step k+1's forward is enqueued before step k's detections are
         # collected (side stream), so the host sync, D2H and gathers overlap the GPU's work;

@@ -192,22 +192,32 @@ class ShardedRunner(object):
         return torch.cat(rows, 0)
 
     def launch_detections(self, local_in, post, slot):
-        """Pipelined form of step_detections, first half: enqueue the forward, `post(out, n,
-        slot)` and the pack for this rank's shard into output slot `slot` (0/1) on the current
-        stream without waiting; returns a handle for finish_detections.  The slot's previous
-        gather must have been finished (its reads are ordered before this launch)."""
+        """Pipelined form of step_detections, first half: enqueue the forward for this rank's
+        shard into output slot `slot` (0/1) on the current stream, and `post(out, n, slot,
+        stream_ptr)` (postprocess + pack) on a post stream that waits only for that forward,
+        without waiting; returns a handle for finish_detections.  The postprocessing of step
+        k (one workgroup per image: a quarter of the CUs) thus runs beside step k+1's first
+        layers instead of between the two forwards.  The slot's previous gather must have
+        been finished (its reads are ordered before this launch, and through the forward's
+        event before this post)."""
+        dev = self.out.device
         if not hasattr(self, "_outs"):
             self._outs = [self.out, torch.zeros_like(self.out)]
-            self._side = torch.cuda.Stream(self.out.device)
+            self._side = torch.cuda.Stream(dev)
+            self._post = torch.cuda.Stream(dev)
             self._freed = [None, None]
-        cur = torch.cuda.current_stream(self.out.device)
+        cur = torch.cuda.current_stream(dev)
         if self._freed[slot] is not None:
             cur.wait_event(self._freed[slot])
         out = self._outs[slot]
         self.compute(local_in, out, self.count)
-        packed, total, counts = post(out, self.count, slot)
+        done = torch.cuda.Event()
+        done.record(cur)
+        self._post.wait_event(done)
+        with torch.cuda.stream(self._post):
+            packed, total, counts = post(out, self.count, slot, self._post.cuda_stream)
         ready = torch.cuda.Event()
-        ready.record(cur)
+        ready.record(self._post)
         return slot, packed, total, counts, ready
 
     def finish_detections(self, handle):
