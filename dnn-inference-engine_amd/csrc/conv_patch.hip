@@ -128,6 +128,121 @@ conv3x3_patch_pool_kernel(const float* __restrict__ in, const float* __restrict_
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Persistent form for C = 16 (YOLOv2-tiny conv1), same MFMA sequence per accumulator as the
+// kernel above (so the same bits):
+//   * each lane keeps its weight fragments for all 9 taps and both 16-channel N-tiles in
+//     registers (18 x f32x4), loaded once per workgroup: no weight staging per tile, no B reads
+//     from LDS (those were 4-way bank conflicts at the 640-B weight row pitch);
+//   * the input patch is double-buffered in LDS: tile k+1's patch is DMA'd while tile k's MFMAs
+//     run, so the load latency is hidden inside the workgroup, not only by other workgroups;
+//   * the 4 16-B channel quads of a patch pixel are stored XOR-swizzled by the patch row's
+//     parity (quad q at q ^ 2(y&1)), which makes every ds_read_b128 of the A fragments
+//     conflict-free for all 9 taps (the plain layout is 2-way: two pixels of a 16-lane group
+//     share each 64-B bank quarter); the DMA applies the swizzle on the source side.
+constexpr int PP_C = 16;
+constexpr int PP_PIX = PT_PATCH * PT_PATCH;             // 324 patch pixels
+constexpr int PP_CH = (PP_PIX * PP_C + 255) / 256;      // 1-KiB DMA chunks per patch (21)
+constexpr int PP_WG_PER_CU = 3;                         // 2 x 21 KiB of LDS per workgroup
+
+__global__ void __launch_bounds__(256, PP_WG_PER_CU)  // 3 waves per SIMD: <= 168 registers
+conv3x3_patch_pool_c16_persistent(const float* __restrict__ in, const float* __restrict__ Bt, int ldb,
+                                  float* __restrict__ out, DirectGeom g, int tilesX, int tilesY, int ntiles,
+                                  const float* __restrict__ zero, EpiParams epi) {
+  typedef Mfma<16> MM;
+  constexpr int C = PP_C;
+  __shared__ __attribute__((aligned(1024))) float smem[2 * PP_CH * 256];
+  const int lane = threadIdx.x & 63;
+  const int wid = wave_uniform(threadIdx.x >> 6);
+  const int fr = lane & 15, fp = lane >> 4;
+
+  // weight fragments: tap, N-tile j -> Bt[16j + fr][tap*16 + 4fp .. +3]
+  f32x4 bw[9][2];
+#pragma unroll
+  for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      bw[tap][j] = *reinterpret_cast<const f32x4*>(Bt + (size_t)(16 * j + fr) * ldb + tap * C + 4 * fp);
+  float pb[2], pm[2], ps[2], pg[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int n = 16 * j + fr;
+    pb[j] = (epi.flags & EPI_BIAS) ? epi.bias[n] : 0.f;
+    pm[j] = (epi.flags & (EPI_BN | EPI_BN_AB)) ? epi.mean[n] : 0.f;
+    ps[j] = (epi.flags & (EPI_BN | EPI_BN_AB)) ? epi.sq[n] : 1.f;
+    pg[j] = (epi.flags & EPI_BN) ? epi.gamma[n] : 1.f;
+  }
+
+  // A fragment bases (floats) for even / odd tap rows dy: the lane's pixel in M-tile i, its
+  // channel quad fp swizzled by the parity of the patch row it lands on
+  int abase[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int wi = fr >> 2, pos = fr & 3;
+    const int y = 4 * wid + 2 * (i >> 1) + (pos >> 1);
+    const int x = 2 * (4 * (i & 1) + wi) + (pos & 1);
+#pragma unroll
+    for (int d = 0; d < 2; ++d) abase[i][d] = (y * PT_PATCH + x) * C + 4 * (fp ^ (2 * ((y + d) & 1)));
+  }
+
+  // DMA of tile t's patch into buffer `buf`: physical quad ps of pixel pp holds channel quad
+  // ps ^ 2(py & 1)
+  auto issue_patch = [&](int t, int buf) {
+    const int tx = t % tilesX, tt = t / tilesX, ty = tt % tilesY, b = tt / tilesY;
+    const float* inb = in + (size_t)b * g.H * g.W * C;
+    for (int c = wid; c < PP_CH; c += 4) {
+      const int f = c * 256 + 4 * lane;
+      const int pp = f / C, q = (f - pp * C) >> 2;
+      const int py = pp / PT_PATCH, px = pp - py * PT_PATCH;
+      const int iy = ty * PT_EDGE - 1 + py, ix = tx * PT_EDGE - 1 + px;
+      const bool ok = pp < PP_PIX && (unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W;
+      lds_dma16(ok ? inb + ((size_t)iy * g.W + ix) * C + 4 * (q ^ (2 * (py & 1))) : zero,
+                smem + (buf * PP_CH + c) * 256);
+    }
+  };
+
+  int t = blockIdx.x, buf = 0;
+  if (t < ntiles) issue_patch(t, 0);
+  for (; t < ntiles; t += gridDim.x) {
+    wait_vmcnt<0>();  // this wave's DMAs of `buf` landed (and the previous tile's stores)
+    raw_barrier();    // everyone's landed; everyone finished reading buf ^ 1
+    if (t + (int)gridDim.x < ntiles) issue_patch(t + gridDim.x, buf ^ 1);
+    const float* P = smem + buf * PP_CH * 256;
+
+    MM::acc_t acc[4][2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      const int dy = tap / 3, aoff = (dy * PT_PATCH + tap % 3) * C;
+      f32x4 af[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = *reinterpret_cast<const f32x4*>(P + abase[i][dy & 1] + aoff);
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[i][j] = MM::op(af[i][s], bw[tap][j][s], acc[i][j]);
+    }
+
+    const int tx = t % tilesX, tt = t / tilesX, ty = tt % tilesY, b = tt / tilesY;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int n = 16 * j + fr;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int wy = ty * (PT_EDGE / 2) + 2 * wid + (i >> 1), wx = tx * (PT_EDGE / 2) + 4 * (i & 1) + fp;
+        const float v = pool_then_epilogue(acc[i][j], pb[j], pm[j], ps[j], pg[j], epi.flags);
+        if (wy < g.PH && wx < g.PW) out[(((size_t)b * g.PH + wy) * g.PW + wx) * 32 + n] = v;
+      }
+    }
+    buf ^= 1;
+  }
+}
+
 // OC == 32 only: the implicit/explicit GEMMs use the 16x16x4 family for N <= 32 and 32x32x2
 // above, and the plan keeps one MFMA family per layer shape so every path of a layer gives the
 // same bits (the kernel itself handles any OC % 32 == 0).
@@ -154,7 +269,13 @@ int launch_conv3x3_patch_pool(const float* in, const float* Bt, int ldb, float* 
     set_error("patch conv: grid too large");
     return -2;
   }
-  if (C == 16)
+  if (C == 16 && N == 32 && !getenv_flag_off("DNN_HIP_PATCH_PERSIST")) {
+    // persistent: as many workgroups as fit resident (3 per CU by LDS), each looping over tiles
+    const long long slots = (long long)device_cu_count() * PP_WG_PER_CU;
+    const unsigned grid = (unsigned)(blocks < slots ? blocks : slots);
+    hipLaunchKernelGGL(conv3x3_patch_pool_c16_persistent, dim3(grid), dim3(256), 0, stream, in, Bt, ldb, out, g,
+                       tilesX, tilesY, (int)blocks, zero, epi);
+  } else if (C == 16)
     hipLaunchKernelGGL((conv3x3_patch_pool_kernel<16>), dim3((unsigned)blocks), dim3(256), 0, stream, in, Bt, out, g,
                        N, tilesX, tilesY, nblkN, zero, epi);
   else

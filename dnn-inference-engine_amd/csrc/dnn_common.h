@@ -12,6 +12,10 @@ namespace dnnhip {
 // ---------------------------------------------------------------- errors
 void set_error(const char* fmt, ...);
 const char* last_error();
+// true when environment variable `name` is set and starts with '0' (experiment switches)
+bool getenv_flag_off(const char* name);
+// compute units of the current HIP device (persistent-kernel grids)
+int device_cu_count();
 
 #define DNN_HIP_TRY(x)                                                             \
   do {                                                                             \

@@ -46,6 +46,24 @@ void set_error(const char* fmt, ...) {
 }
 const char* last_error() { return g_last_error.c_str(); }
 
+bool getenv_flag_off(const char* name) {
+  const char* e = getenv(name);
+  return e && e[0] == '0';
+}
+
+int device_cu_count() {
+  // compute units of the current device (256 on MI355X), cached per device
+  static int cache[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (!cache[dev]) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cache[dev] = n;
+  }
+  return cache[dev];
+}
+
 void out_pads(int in, int k, int s, int same, int* out, int* pad_front) {
   // proj3/dnn_openblas.py:127-142 (TensorFlow SAME / VALID)
   if (same) {
