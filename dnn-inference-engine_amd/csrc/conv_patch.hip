@@ -201,10 +201,16 @@ conv3x3_patch_pool_c16_persistent(const float* __restrict__ in, const float* __r
     }
   };
 
+  const auto orsrc = out_rsrc(out, (unsigned)((size_t)g.B * g.PH * g.PW * 32 * sizeof(float)));
   int t = blockIdx.x, buf = 0;
   if (t < ntiles) issue_patch(t, 0);
   for (; t < ntiles; t += gridDim.x) {
-    wait_vmcnt<0>();  // this wave's DMAs of `buf` landed (and the previous tile's stores)
+    // this wave's DMAs of `buf` landed: all but the previous tile's 8 stores (issued after
+    // them, never branched around: store4) have completed
+    if (buf == 0 && t == (int)blockIdx.x)
+      wait_vmcnt<0>();
+    else
+      wait_vmcnt<8>();
     raw_barrier();    // everyone's landed; everyone finished reading buf ^ 1
     if (t + (int)gridDim.x < ntiles) issue_patch(t + gridDim.x, buf ^ 1);
     const float* P = smem + buf * PP_CH * 256;
@@ -236,7 +242,7 @@ conv3x3_patch_pool_c16_persistent(const float* __restrict__ in, const float* __r
       for (int i = 0; i < 4; ++i) {
         const int wy = ty * (PT_EDGE / 2) + 2 * wid + (i >> 1), wx = tx * (PT_EDGE / 2) + 4 * (i & 1) + fp;
         const float v = pool_then_epilogue(acc[i][j], pb[j], pm[j], ps[j], pg[j], epi.flags);
-        if (wy < g.PH && wx < g.PW) out[(((size_t)b * g.PH + wy) * g.PW + wx) * 32 + n] = v;
+        store4(orsrc, (wy < g.PH && wx < g.PW) ? (unsigned)(((((size_t)b * g.PH + wy) * g.PW + wx) * 32 + n) * 4) : OOB_OFF, v);
       }
     }
     buf ^= 1;
@@ -269,7 +275,8 @@ int launch_conv3x3_patch_pool(const float* in, const float* Bt, int ldb, float* 
     set_error("patch conv: grid too large");
     return -2;
   }
-  if (C == 16 && N == 32 && !getenv_flag_off("DNN_HIP_PATCH_PERSIST")) {
+  if (C == 16 && N == 32 && (size_t)g.B * g.PH * g.PW * 32 * sizeof(float) < OOB_OFF &&
+      !getenv_flag_off("DNN_HIP_PATCH_PERSIST")) {
     // persistent: as many workgroups as fit resident (3 per CU by LDS), each looping over tiles
     const long long slots = (long long)device_cu_count() * PP_WG_PER_CU;
     const unsigned grid = (unsigned)(blocks < slots ? blocks : slots);

@@ -183,6 +183,133 @@ conv0_mfma_pool_kernel(const float* __restrict__ in, const float* __restrict__ w
   }
 }
 
+// conv0_packed_pool_kernel<CIN>: the fp32 conv0 with K = 9*CIN packed densely into
+// ceil(K/4) v_mfma_f32_16x16x4_f32 steps (CIN = 3: 7 MFMAs per 16-pixel tile instead of the 9
+// one-tap-per-MFMA steps above, k = 27 multiplying a zero weight).  K order is the
+// reference's im2col order (tap-major, channel-minor, dnn_openblas.c:135-158), so every
+// accumulator is the same fmaf chain over k = 0..26 as the explicit im2col + GEMM path: same
+// bits.  The halo patch is DMA'd straight from the NHWC frame rows (one 4-B LDS-DMA lane per
+// float of the 18 x CIN floats of a patch row: no register staging, no channel padding) into
+// a double buffer, the next tile's rows in flight during this tile's MFMAs; lane part p of
+// step s reads k = 4s + p at a per-lane LDS offset koff[s] (dy*RS + dx*CIN + c) from its
+// pixel, the M-tile offset being an immediate.  (RS = 56: every ds_read_b32 is exactly
+// 2-way; no row stride makes the two pixel rows of an M-tile conflict-free.)
+constexpr int C0_RS = 56;  // patch row stride (floats) >= 18 * CIN
+
+template <int CIN>
+__global__ void __launch_bounds__(256)
+conv0_packed_pool_kernel(const float* __restrict__ in, const float* __restrict__ w, float* __restrict__ out,
+                         DirectGeom g, int tilesX, int tilesY, int ntiles, const float* __restrict__ zero,
+                         EpiParams epi) {
+  constexpr int K = 9 * CIN, KS = (K + 3) / 4, RW = SC_P * CIN, RS = C0_RS;
+  static_assert(RW <= RS && RW <= 64, "patch row");
+  __shared__ __attribute__((aligned(16))) float patch[2][SC_P * RS];
+  __shared__ __attribute__((aligned(16))) float stage[4][2][8][16];  // per wave: 2 window rows x 8 windows x 16 ch
+
+  const int lane = threadIdx.x & 63;
+  const int wid = wave_uniform(threadIdx.x >> 6);
+  const int fr = lane & 15, fp = lane >> 4, n = lane & 15;
+
+  // B fragments (HWIO [k = tap*CIN + c][16]) and the A offsets of k = 4s + fp
+  float wv[KS];
+  int koff[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    const int k = 4 * s + fp;
+    const int tap = k / CIN, c = k - (k / CIN) * CIN, dy = tap / 3, dx = tap - (tap / 3) * 3;
+    wv[s] = k < K ? w[k * 16 + n] : 0.f;
+    koff[s] = k < K ? dy * RS + dx * CIN + c : 0;
+  }
+  const float pb_ = (epi.flags & EPI_BIAS) ? epi.bias[n] : 0.f;
+  const float pm = (epi.flags & (EPI_BN | EPI_BN_AB)) ? epi.mean[n] : 0.f;
+  const float ps = (epi.flags & (EPI_BN | EPI_BN_AB)) ? epi.sq[n] : 1.f;
+  const float pg = (epi.flags & EPI_BN) ? epi.gamma[n] : 1.f;
+
+  // the lane's pixel in M-tile 0 (rows pool-window-major: row = 4*window + 2*dy + dx); M-tile
+  // i adds the constant 2*(i>>1) rows and 8*(i&1) pixels
+  const int pix0 = (4 * wid + ((fr & 3) >> 1)) * RS + (2 * (fr >> 2) + (fr & 1)) * CIN;
+
+  // tile coordinates: one set of divisions per tile, shared by its DMA issue and its stores
+  struct Tile {
+    int b, ty, tx;
+  };
+  auto coords = [&](int t) {
+    const int tt = t / tilesX, b = tt / tilesY;
+    return Tile{b, tt - b * tilesY, t - tt * tilesX};
+  };
+  // lane l of a patch row DMA copies float l of the row's 18 * CIN (the row is contiguous in
+  // the NHWC frame); lanes past the frame's edges read the zero page
+  auto issue = [&](const Tile& c, int buf) {
+    const int x0 = c.tx * SC_T - g.pl, y0 = c.ty * SC_T - g.pt;
+    const int px = x0 + lane / CIN;
+    const bool xok = (unsigned)px < (unsigned)g.W;
+    const float* rowp = in + (((size_t)c.b * g.H + y0) * g.W + x0) * CIN + lane;
+    const size_t rstride = (size_t)g.W * CIN;
+#pragma unroll
+    for (int u = 0; u < (SC_P + 3) / 4; ++u) {
+      const int r = wid + 4 * u;
+      if (r < SC_P && lane < RW) {
+        const bool ok = xok && (unsigned)(y0 + r) < (unsigned)g.H;
+        lds_dma4_opaque(ok ? rowp + r * rstride : zero, &patch[buf][r * RS]);
+      }
+    }
+  };
+
+  const auto orsrc = out_rsrc(out, (unsigned)((size_t)g.B * g.PH * g.PW * 16 * sizeof(float)));
+  int t = blockIdx.x, buf = 0;
+  Tile cur = coords(t < ntiles ? t : 0);
+  if (t < ntiles) issue(cur, 0);
+  for (; t < ntiles; t += gridDim.x) {
+    // this wave's rows of `buf` landed: everything but the previous tile's one store (issued
+    // after those DMAs; always issued, see store16) has completed
+    if (buf == 0 && t == (int)blockIdx.x)
+      wait_vmcnt<0>();
+    else
+      wait_vmcnt<1>();
+    raw_barrier();    // all rows landed; every wave finished reading buf ^ 1
+    Tile nxt = cur;
+    if (t + (int)gridDim.x < ntiles) {
+      nxt = coords(t + gridDim.x);
+      issue(nxt, buf ^ 1);
+    }
+    const float* P = patch[buf];
+
+    f32x4 acc[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const float* a = P + pix0 + koff[s];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[2 * (i >> 1) * RS + 8 * (i & 1) * CIN], wv[s], acc[i], 0, 0, 0);
+    }
+
+    const int b = cur.b, y0 = cur.ty * SC_T, x0 = cur.tx * SC_T;
+    cur = nxt;
+    // pool + epilogue into the wave's LDS stage, then 16-B coalesced stores
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int wy = (y0 >> 1) + 2 * wid + (i >> 1), wx = (x0 >> 1) + 4 * (i & 1) + fp;
+      const bool x1 = 2 * wx + 1 < g.OW, y1 = 2 * wy + 1 < g.OH;
+      const f32x4 v = {acc[i][0], x1 ? acc[i][1] : acc[i][0], y1 ? acc[i][2] : acc[i][0],
+                       x1 && y1 ? acc[i][3] : acc[i][0]};
+      stage[wid][i >> 1][4 * (i & 1) + fp][n] = pool_then_epilogue(v, pb_, pm, ps, pg, epi.flags);
+    }
+    wait_lgkm0();  // the stage is wave-private
+    {  // one 16-B store per lane (2 window rows x 8 windows x 16 channels per wave)
+      const int lr = lane >> 5, f = (lane & 31) * 4;
+      const int wy = (y0 >> 1) + 2 * wid + lr, wxs = (x0 >> 1) + f / 16;
+      const unsigned off = (wy < g.PH && wxs < g.PW)
+                               ? (unsigned)(((((size_t)b * g.PH + wy) * g.PW + (x0 >> 1)) * 16 + f) * sizeof(float))
+                               : OOB_OFF;
+      store16(orsrc, off, *reinterpret_cast<const f32x4*>(&stage[wid][lr][0][0] + f));
+    }
+    wait_lgkm0();
+    buf ^= 1;
+  }
+}
+
 bool conv0_mfma_supported(int cin, int nout, int kh, int kw, int sh, int sw) {
   return kh == 3 && kw == 3 && sh == 1 && sw == 1 && cin >= 1 && cin <= 3 && nout == 16;
 }
@@ -214,9 +341,30 @@ static int launch_conv0(const float* in, const float* w, OutT* out, const Direct
   return 0;
 }
 
-int launch_conv0_mfma(const float* in, const float* w, float* out, const DirectGeom& g, int cin, const EpiParams& epi,
-                      hipStream_t s) {
-  return launch_conv0<false, float>(in, w, out, g, cin, epi, s);
+int launch_conv0_mfma(const float* in, const float* w, float* out, const DirectGeom& g, int cin, const float* zero,
+                      const EpiParams& epi, hipStream_t s) {
+  if (cin != 3 || !zero || getenv_flag_off("DNN_HIP_CONV0_PACKED"))
+    return launch_conv0<false, float>(in, w, out, g, cin, epi, s);
+  if (g.B == 0) return 0;
+  const int tilesX = (g.OW + SC_T - 1) / SC_T, tilesY = (g.OH + SC_T - 1) / SC_T;
+  const long long blocks = (long long)g.B * tilesX * tilesY;
+  if ((size_t)g.B * g.PH * g.PW * 16 * sizeof(float) >= OOB_OFF)  // 32-bit store offsets
+    return launch_conv0<false, float>(in, w, out, g, cin, epi, s);
+  if (blocks > 0x7fffffffLL || g.PH != (g.OH + 1) / 2 || g.PW != (g.OW + 1) / 2) {
+    set_error("conv0_packed: unsupported shape");
+    return -2;
+  }
+  // persistent: 8 workgroups per CU loop over the tiles
+  const long long slots = 8LL * device_cu_count();
+  const unsigned grid = (unsigned)(blocks < slots ? blocks : slots);
+  hipLaunchKernelGGL((conv0_packed_pool_kernel<3>), dim3(grid), dim3(256), 0, s, in, w, out, g, tilesX, tilesY,
+                     (int)blocks, zero, epi);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    set_error("launch conv0_packed: %s", hipGetErrorString(e));
+    return -1;
+  }
+  return 0;
 }
 int launch_conv0_mfma_f16(const float* in, const float* w, half_t* out, const DirectGeom& g, int cin,
                           const EpiParams& epi, hipStream_t s) {

@@ -186,8 +186,8 @@ int launch_conv3x3_pool2_direct_f16out(const float* in, const float* w, half_t* 
 // conv_small.hip: conv0 on MFMA (cin <= 3, 16 outputs, fp32 frames in, pool fused) and the
 // fp16 path's conv1 patch kernel (C = 16 -> 32, pool fused)
 bool conv0_mfma_supported(int cin, int nout, int kh, int kw, int sh, int sw);
-int launch_conv0_mfma(const float* in, const float* w, float* out, const DirectGeom& g, int cin, const EpiParams& epi,
-                      hipStream_t s);
+int launch_conv0_mfma(const float* in, const float* w, float* out, const DirectGeom& g, int cin, const float* zero,
+                      const EpiParams& epi, hipStream_t s);
 int launch_conv0_mfma_f16(const float* in, const float* w, half_t* out, const DirectGeom& g, int cin,
                           const EpiParams& epi, hipStream_t s);
 bool conv1_patch_f16_supported(int C, int OC, int H, int W, int OH, int OW, int kh, int kw, int sh, int sw, int pt,

@@ -255,6 +255,36 @@ __device__ __forceinline__ void lds_dma16(const float* src, float* dst) {
   __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
 }
 
+// Stores whose instruction count per wave is fixed (persistent kernels that wait for their
+// next tile's LDS-DMA with a counted vmcnt while their own stores are still in flight: the
+// count is only exact if no store is ever branched around).  A buffer resource over the
+// output drops a lane whose byte offset is out of range (OOB_OFF) instead of faulting, so
+// the store is always issued.  Offsets are 32-bit: the launcher checks the output size.
+constexpr unsigned OOB_OFF = 0x80000000u;
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t out_rsrc(void* base, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(base, 0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ void store16(__amdgpu_buffer_rsrc_t r, unsigned off, f32x4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, off, 0, 0);
+}
+__device__ __forceinline__ void store4(__amdgpu_buffer_rsrc_t r, unsigned off, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, off, 0, 0);
+}
+
+// 4-B LDS-DMA (global_load_lds_dword) issued from inline asm: the compiler's wait pass does
+// not see it, so it does not put a conservative vmcnt(0) before every later LDS read (it
+// cannot tell a double buffer's halves apart).  The caller orders it with its own counted
+// vmcnt + barrier.  `dst` must be wave-uniform; lane l writes dst + 4*l.
+__device__ __forceinline__ void lds_dma4_opaque(const float* src, const float* dst) {
+  const unsigned m0v = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) float*)dst;
+  unsigned saved;  // M0 is a reserved register: restore it rather than clobber it
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(saved)
+               : "v"(src), "s"(m0v)
+               : "memory");
+}
+
 // max (or min, for a channel whose epilogue is non-increasing) of a pool window's raw conv
 // outputs, then the epilogue once.  The epilogue f = leaky(((v + b) - mean) / sq * gamma) is a
 // chain of IEEE-rounded monotone steps (sq > 0): non-decreasing for gamma >= 0, non-increasing

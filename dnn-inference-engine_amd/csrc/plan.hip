@@ -639,7 +639,7 @@ int dnn_plan_run(dnn_plan* p, int n, const float* d_in, float* d_out, void* stre
         case MODE_DIRECT: {
           DirectGeom g{n, L.H, L.W, L.OH, L.OW, L.PH, L.PW, L.pt, L.pl};
           rc = conv0_mfma_supported(L.C, L.OC, L.kh, L.kw, L.sh, L.sw)
-                   ? launch_conv0_mfma(cur, wt, dst, g, L.C, epi, s)
+                   ? launch_conv0_mfma(cur, wt, dst, g, L.C, zero, epi, s)
                    : launch_conv3x3_pool2_direct(cur, wt, dst, g, L.C, L.OC, epi, s);
           break;
         }
