@@ -117,14 +117,21 @@ int launch_im2col(const float* in, float* col, const ConvGeom& g, hipStream_t st
 // [splits][M][N] to `slab` and NO epilogue; launch_splitk_reduce then sums them in split order
 // and applies the epilogue into C.  choose_splitk depends on (N, K) only.
 int choose_splitk(int N, int K);
+// With `tickets` (>= the cfg's tile count of unsigned, zero before the first launch and left
+// zero by every launch) the split-K GEMM finishes itself: the last-arriving split of each tile
+// sums the partials in split order and writes C with the epilogue (splitk_combine, gemm_f32.h),
+// so no reduce kernel follows; `slab` must then hold splitk_fused_slab_floats() floats.
 int launch_gemm(int cfg, const float* A, int lda, const float* Bt, int ldb, float* C, int ldc,
                 long long M, int N, int Kpad, const EpiParams& epi, hipStream_t stream, int splits = 1,
-                float* slab = nullptr);
+                float* slab = nullptr, unsigned* tickets = nullptr);
 // implicit conv (mode GEMM_IMPLICIT / GEMM_IMPLICIT_POOL) on the LDS-DMA configs 3..6;
 // `in` is the NHWC input, M = B*OH*OW (or B*PH*PW*4 with pool; no split-K with pool)
 int launch_gemm_implicit(int cfg, int mode, const float* in, const ImplicitConv& ic, const float* Bt, int ldb,
                          float* C, int ldc, long long M, int N, int Kpad, const EpiParams& epi, hipStream_t stream,
-                         int splits = 1, float* slab = nullptr);
+                         int splits = 1, float* slab = nullptr, unsigned* tickets = nullptr);
+// slab floats and tickets a fused split-K launch of (cfg, M, N, splits) needs
+long long splitk_fused_slab_floats(int cfg, long long M, int N, int splits);
+long long splitk_tiles(int cfg, long long M, int N);
 int launch_splitk_reduce(const float* slab, int splits, long long M, int N, float* C, int ldc,
                          const EpiParams& epi, hipStream_t stream);
 int launch_maxpool(const float* in, float* out, const PoolGeom& g, hipStream_t stream);

@@ -348,6 +348,14 @@ struct SplitK {
   int steps;         // K-steps (of 32) per split; 0 = no split
   int ntile;         // tilesM * tilesN
   long long slab;    // floats between consecutive split partials
+  // fused combine (tickets != nullptr, fp32 LDS-DMA kernel): every split stores its raw tile
+  // in the accumulator-native layout, the LAST split of a tile to arrive (agent-scope ticket)
+  // sums all partials in split order and runs the epilogue into `out` (splitk_combine)
+  unsigned* tickets = nullptr;
+  float* out = nullptr;
+  int ldo = 0;
+  int flags = 0;     // epilogue of the final output
+  int splits = 1;
 };
 
 // Sum of the split-K partials in split order, ((p0 + p1) + p2) ..., then the fused epilogue.
@@ -388,6 +396,90 @@ splitk_reduce_kernel(const float* __restrict__ part, int splits, long long slab,
   }
 }
 
+// Fused split-K combine (Guideline 16 R1 hand-off, cdna_hip_programming.md §6): each split's
+// workgroup stores its raw partial tile write-through (sc1, 16-B stores in the accumulator-native
+// layout: lane-contiguous f32x4 of 4 consecutive rows, so no bounds checks and full 1-KiB wave
+// stores), every wave drains (vmcnt 0), the workgroup barrier, then ONE lane adds to the tile's
+// agent-scope ticket.  The workgroup whose add returns splits-1 is the last: one agent acquire
+// (+ vmcnt 0 + barrier), then plain loads of the other partials, summed in split order
+// ((p0 + p1) + p2 ..., the separate reduce kernel's order, so the same bits) with its own
+// partial taken from registers, the epilogue, and the row-major store.  It re-arms the ticket
+// (0) for the next launch.  Partial tile (split s, tile t) starts at slab + (s*ntile + t)*BM*BN.
+template <int SPL, int MF, int TM, int TN, int WTM, int WTN, int NW>
+__device__ __forceinline__ void splitk_combine(typename Mfma<MF>::acc_t (&acc)[TM][TN], float* __restrict__ slab,
+                                               const SplitK& sk, int s, int tile, int M, int N, int m0, int n0,
+                                               int wm, int wn, int wid, int lane, const EpiParams& epi0,
+                                               unsigned* lds_word) {
+  typedef Mfma<MF> MM;
+  constexpr int Q = MM::REGS / 4;
+  constexpr long long TILE_F = (long long)NW * TM * TN * Q * 256;  // = BM * BN
+  const unsigned slab_bytes = (unsigned)((long long)SPL * sk.ntile * TILE_F * 4);
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(slab, 0, (int)slab_bytes, 0x00020000);
+  auto idx = [&](int i, int j, int q) { return ((((wid * TM + i) * TN + j) * Q + q) * 64 + lane) * 4; };
+  const long long own = ((long long)s * sk.ntile + tile) * TILE_F;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        const f32x4 v = {acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]};
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs,
+                                               (unsigned)((own + idx(i, j, q)) * 4), 0, 16 /* sc1 */);
+      }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // EVERY storing wave drains
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned t = __hip_atomic_fetch_add(sk.tickets + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned last = t == (unsigned)(SPL - 1) ? 1u : 0u;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      __hip_atomic_store(sk.tickets + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    *lds_word = last;
+  }
+  __syncthreads();
+  if (!*lds_word) return;
+
+  EpiParams epi = epi0;
+  epi.flags = sk.flags;
+  const int oc = MM::out_col(lane);
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int n = n0 + wn * WTN + j * MF + oc;
+    const bool nok = n < N;
+    const float pb = (nok && (epi.flags & EPI_BIAS)) ? epi.bias[n] : 0.f;
+    const float pm = (nok && (epi.flags & (EPI_BN | EPI_BN_AB))) ? epi.mean[n] : 0.f;
+    const float ps = (nok && (epi.flags & (EPI_BN | EPI_BN_AB))) ? epi.sq[n] : 1.f;
+    const float pg = (nok && (epi.flags & EPI_BN)) ? epi.gamma[n] : 1.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      // all partials of this (i, j) in flight at once, then the ordered sums
+      f32x4 part[SPL][Q];
+#pragma unroll
+      for (int ss = 0; ss < SPL; ++ss)
+#pragma unroll
+        for (int q = 0; q < Q; ++q)
+          part[ss][q] = ss == s ? f32x4{acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]}
+                                : *reinterpret_cast<const f32x4*>(slab + ((long long)ss * sk.ntile + tile) * TILE_F +
+                                                                  idx(i, j, q));
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        f32x4 v = part[0][q];
+#pragma unroll
+        for (int ss = 1; ss < SPL; ++ss) v = v + part[ss][q];
+        if (!nok) continue;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int m = m0 + wm * WTM + i * MF + MM::out_row(lane, 4 * q + e);
+          if (m < M) sk.out[(size_t)m * sk.ldo + n] = apply_epilogue(v[e], pb, pm, ps, pg, epi.flags);
+        }
+      }
+    }
+  }
+}
+
 // MODE 0: dense A (col buffer or 1x1 input), MODE 1: implicit conv, MODE 2: implicit + pool.
 template <int BM, int BN, int WM, int WN, int MF, int NS, int MODE>
 __global__ void __launch_bounds__(WM* WN * 64)
@@ -411,13 +503,14 @@ gemm_f32_glds_kernel(const float* __restrict__ A, int lda, const float* __restri
 
   int tile = xcd_tile(blockIdx.x, gridDim.x);
   int kbeg = 0;  // first k of this workgroup's K range
+  int split = 0;
   if (sk.steps > 0) {
-    const int s = tile / sk.ntile;
-    tile -= s * sk.ntile;
-    kbeg = s * sk.steps * BK;
+    split = tile / sk.ntile;
+    tile -= split * sk.ntile;
+    kbeg = split * sk.steps * BK;
     K = sk.steps * BK;
-    C += s * sk.slab;
-    epi.flags = 0;  // raw partial sums; the reduce kernel applies the epilogue
+    if (!sk.tickets) C += split * sk.slab;
+    epi.flags = 0;  // raw partial sums; the reduce kernel / the combine applies the epilogue
   }
   const int tm_ = tile / tilesN, tn_ = tile - tm_ * tilesN;
   const int m0 = tm_ * BM, n0 = tn_ * BN;
@@ -587,10 +680,21 @@ gemm_f32_glds_kernel(const float* __restrict__ A, int lda, const float* __restri
     wait_lgkm0();
     stage = stage + 1 == NS ? 0 : stage + 1;
   }
-  if constexpr (MODE == 2)
+  if constexpr (MODE == 2) {
     store_tile_pool<MF, TM, TN, WTM, WTN>(acc, C, ldc, M, N, m0, n0, wm, wn, lane, epi, ic);
-  else
+  } else {
+    if (sk.steps > 0 && sk.tickets) {
+      // the launcher admits splits 2..3 only (choose_splitk gives 3)
+      if (sk.splits == 3)
+        splitk_combine<3, MF, TM, TN, WTM, WTN, NW>(acc, C, sk, split, tile, M, N, m0, n0, wm, wn, wid, lane, epi,
+                                                    reinterpret_cast<unsigned*>(smem));
+      else
+        splitk_combine<2, MF, TM, TN, WTM, WTN, NW>(acc, C, sk, split, tile, M, N, m0, n0, wm, wn, wid, lane, epi,
+                                                    reinterpret_cast<unsigned*>(smem));
+      return;
+    }
     store_tile<MF, TM, TN, WTM, WTN>(acc, C, ldc, M, N, m0, n0, wm, wn, lane, epi);
+  }
 }
 
 }  // namespace dnnhip

@@ -257,9 +257,17 @@ static int launch_glds(int cfg, const float* A, int lda, const float* Bt, int ld
   return check_launch("gemm_glds");
 }
 
-// grid and SplitK descriptor for `splits` (> 1: the kernel writes raw partials to `slab`)
-static int split_setup(int cfg, long long M, int N, int Kpad, int splits, float* slab, SplitK* sk, int* grid,
-                       int* tilesN) {
+long long splitk_tiles(int cfg, long long M, int N) {
+  return ((M + kCfgs[cfg].bm - 1) / kCfgs[cfg].bm) * ((N + kCfgs[cfg].bn - 1) / kCfgs[cfg].bn);
+}
+long long splitk_fused_slab_floats(int cfg, long long M, int N, int splits) {
+  return splitk_tiles(cfg, M, N) * kCfgs[cfg].bm * kCfgs[cfg].bn * splits;
+}
+
+// grid and SplitK descriptor for `splits` (> 1: the kernel writes raw partials to `slab`;
+// with `tickets` it also combines them itself into C)
+static int split_setup(int cfg, long long M, int N, int Kpad, int splits, float* slab, unsigned* tickets, float* C,
+                       int ldc, int flags, SplitK* sk, int* grid, int* tilesN) {
   const CfgInfo ci = kCfgs[cfg];
   const int tilesM = ceil_div_i(M, ci.bm);
   *tilesN = ceil_div_i(N, ci.bn);
@@ -271,13 +279,29 @@ static int split_setup(int cfg, long long M, int N, int Kpad, int splits, float*
       return -2;
     }
     *sk = SplitK{Kpad / 32 / splits, *grid, M * (long long)N};
+    if (tickets) {
+      if (splits > 3) {
+        set_error("gemm: fused split-K combine supports 2 or 3 splits (got %d)", splits);
+        return -2;
+      }
+      if (splitk_fused_slab_floats(cfg, M, N, splits) * 4 >= 0x80000000LL) {
+        set_error("gemm: fused split-K slab over 2 GiB (M=%lld N=%d)", M, N);
+        return -2;
+      }
+      sk->tickets = tickets;
+      sk->out = C;
+      sk->ldo = ldc;
+      sk->flags = flags;
+      sk->splits = splits;
+    }
     *grid *= splits;
   }
   return 0;
 }
 
 int launch_gemm(int cfg, const float* A, int lda, const float* Bt, int ldb, float* C, int ldc,
-                long long M, int N, int Kpad, const EpiParams& epi, hipStream_t stream, int splits, float* slab) {
+                long long M, int N, int Kpad, const EpiParams& epi, hipStream_t stream, int splits, float* slab,
+                unsigned* tickets) {
   if (M == 0 || N == 0) return 0;
   if (cfg < 0 || cfg >= GEMM_NUM_CFGS) {
     set_error("gemm: bad cfg %d", cfg);
@@ -290,7 +314,7 @@ int launch_gemm(int cfg, const float* A, int lda, const float* Bt, int ldb, floa
   }
   SplitK sk;
   int g = 0, tilesN = 0;
-  if (int rc = split_setup(cfg, M, N, Kpad, splits, slab, &sk, &g, &tilesN)) return rc;
+  if (int rc = split_setup(cfg, M, N, Kpad, splits, slab, tickets, C, ldc, epi.flags, &sk, &g, &tilesN)) return rc;
   dim3 grid(g);
   const int m = (int)M;
   switch (cfg) {
@@ -315,7 +339,7 @@ int launch_gemm(int cfg, const float* A, int lda, const float* Bt, int ldb, floa
 
 int launch_gemm_implicit(int cfg, int mode, const float* in, const ImplicitConv& ic, const float* Bt, int ldb,
                          float* C, int ldc, long long M, int N, int Kpad, const EpiParams& epi, hipStream_t stream,
-                         int splits, float* slab) {
+                         int splits, float* slab, unsigned* tickets) {
   if (M == 0 || N == 0) return 0;
   if (cfg < GEMM_128x128_K32 || cfg >= GEMM_NUM_CFGS || (mode != GEMM_IMPLICIT && mode != GEMM_IMPLICIT_POOL)) {
     set_error("gemm_implicit: bad cfg %d / mode %d", cfg, mode);
@@ -329,7 +353,7 @@ int launch_gemm_implicit(int cfg, int mode, const float* in, const ImplicitConv&
   }
   SplitK sk;
   int g = 0, tilesN = 0;
-  if (int rc = split_setup(cfg, M, N, Kpad, splits, slab, &sk, &g, &tilesN)) return rc;
+  if (int rc = split_setup(cfg, M, N, Kpad, splits, slab, tickets, C, ldc, epi.flags, &sk, &g, &tilesN)) return rc;
   float* out = sk.steps ? slab : C;
   const int ldo = sk.steps ? N : ldc;
   if (mode == GEMM_IMPLICIT)

@@ -119,6 +119,7 @@ struct dnn_plan {
   int cur_h = 0, cur_w = 0, cur_c = 0;
   bool fuse = true;
   bool patch = true;
+  bool splitk_fused = true;  // fp32 split-K layers combine in the GEMM (no reduce kernel)
   int fp16 = 0;  // 1: fp16 activations/weights, fp16 MFMA, fp32 accumulate + epilogue
   std::vector<PlanLayer> layers;
   std::vector<KernelDesc> kernels;
@@ -130,7 +131,7 @@ struct dnn_plan {
   float* ws = nullptr;
   size_t ws_floats = 0;
   bool own_ws = false;
-  size_t act_floats = 0, col_floats = 0, slab_floats = 0;
+  size_t act_floats = 0, col_floats = 0, slab_floats = 0, ticket_floats = 0;
   static constexpr size_t kZeroFloats = 64;  // zero page: source of padding taps (implicit GEMM)
   // staging for dnn_plan_run_host
   float* h_in_dev = nullptr;
@@ -156,8 +157,10 @@ static void drop_graph(dnn_plan* p) {
   p->g_n = -1;
 }
 
+static bool fused_splitk(const dnn_plan* p) { return p->splitk_fused && !p->fp16; }
+
 static void layout(dnn_plan* p) {
-  size_t off = 0, act = (size_t)p->in_h * p->in_w * p->in_c, col = 0, slab = 0;
+  size_t off = 0, act = (size_t)p->in_h * p->in_w * p->in_c, col = 0, slab = 0, slab_fused = 0, tickets = 0;
   int nconv = 0, npool = 0;  // kernel names use conv / pool ordinals: "conv7.gemm" is YOLO's conv7
   p->kernels.clear();
   const double B = p->batch;
@@ -191,7 +194,10 @@ static void layout(dnn_plan* p) {
         p->kernels.push_back({nm, (int)i, 1, flops, in_b + w_b + out_b});
         ++nconv;
       }
-      if (L.splits > 1) {  // partials written by the GEMM, summed + epilogue by the reduce kernel
+      if (L.splits > 1 && fused_splitk(p)) {  // partials combined by the GEMM's last-arriving split
+        slab_fused = std::max(slab_fused, (size_t)splitk_fused_slab_floats(L.cfg, (long long)M, L.OC, L.splits));
+        tickets = std::max(tickets, (size_t)splitk_tiles(L.cfg, (long long)M, L.OC));
+      } else if (L.splits > 1) {  // partials written by the GEMM, summed + epilogue by the reduce kernel
         slab = std::max(slab, (size_t)L.splits * L.OH * L.OW * L.OC);
         snprintf(nm, sizeof(nm), "conv%d.reduce", nconv - 1);
         p->kernels.push_back({nm, (int)i, 3, (L.splits - 1) * M * L.OC, 4.0 * (L.splits + 1) * M * L.OC});
@@ -212,8 +218,9 @@ static void layout(dnn_plan* p) {
   // activation buffers hold fp16 elements on the fp16 path
   p->act_floats = align_up((act * (size_t)p->batch + (p->fp16 ? 1 : 0)) / (p->fp16 ? 2 : 1), 64);
   p->col_floats = align_up(col * (size_t)p->batch, 64);
-  p->slab_floats = align_up(slab * (size_t)p->batch, 64);
-  p->ws_floats = 2 * p->act_floats + p->col_floats + p->slab_floats + dnn_plan::kZeroFloats;
+  p->slab_floats = align_up(std::max(slab * (size_t)p->batch, slab_fused), 64);
+  p->ticket_floats = align_up(tickets, 64);  // unsigned tickets of the fused split-K layers
+  p->ws_floats = 2 * p->act_floats + p->col_floats + p->slab_floats + p->ticket_floats + dnn_plan::kZeroFloats;
 }
 
 extern "C" {
@@ -233,6 +240,7 @@ int dnn_plan_create(int batch, int in_h, int in_w, int in_c, dnn_plan** out) {
   p->fuse = !(f && f[0] == '0');
   const char* pe = getenv("DNN_HIP_PATCH");
   p->patch = !(pe && pe[0] == '0');
+  p->splitk_fused = !getenv_flag_off("DNN_HIP_SPLITK_FUSED");
   *out = p;
   return 0;
 }
@@ -496,6 +504,9 @@ int dnn_plan_finalize(dnn_plan* p, int device, void* weights, void* workspace) {
   }
   // zero page at the end of the workspace (padding taps of the implicit GEMM read it)
   DNN_HIP_TRY(hipMemset(p->ws + p->ws_floats - dnn_plan::kZeroFloats, 0, dnn_plan::kZeroFloats * sizeof(float)));
+  if (p->ticket_floats)  // fused split-K tickets start at zero; every launch leaves them zero
+    DNN_HIP_TRY(hipMemset(p->ws + 2 * p->act_floats + p->col_floats + p->slab_floats, 0,
+                          p->ticket_floats * sizeof(float)));
   bool all_host = true;
   for (auto& L : p->layers)
     if (L.type == 0 && !L.have_host) all_host = false;
@@ -603,6 +614,7 @@ int dnn_plan_run(dnn_plan* p, int n, const float* d_in, float* d_out, void* stre
   float* act[2] = {p->ws, p->ws + p->act_floats};
   float* col = p->ws + 2 * p->act_floats;
   float* slab = col + p->col_floats;
+  unsigned* tickets = fused_splitk(p) ? reinterpret_cast<unsigned*>(slab + p->slab_floats) : nullptr;
   const float* zero = p->ws + p->ws_floats - dnn_plan::kZeroFloats;
   const float* cur = d_in;
   const int nl = (int)p->layers.size();
@@ -622,18 +634,20 @@ int dnn_plan_run(dnn_plan* p, int n, const float* d_in, float* d_out, void* stre
           ConvGeom g{n, L.H, L.W, L.C, L.OH, L.OW, L.kh, L.kw, L.sh, L.sw, L.pt, L.pl, L.K, L.Kpad};
           if ((rc = launch_im2col(cur, col, g, s))) return rc;
           if ((rc = record(p, ++k, s))) return rc;
-          rc = launch_gemm(L.cfg, col, L.Kpad, wt, L.Kpad, dst, L.OC, Mc, L.OC, L.Kpad, epi, s, L.splits, slab);
+          rc = launch_gemm(L.cfg, col, L.Kpad, wt, L.Kpad, dst, L.OC, Mc, L.OC, L.Kpad, epi, s, L.splits, slab,
+                           tickets);
           break;
         }
         case MODE_DIRECT_A:
-          rc = launch_gemm(L.cfg, cur, L.C, wt, L.Kpad, dst, L.OC, Mc, L.OC, L.Kpad, epi, s, L.splits, slab);
+          rc = launch_gemm(L.cfg, cur, L.C, wt, L.Kpad, dst, L.OC, Mc, L.OC, L.Kpad, epi, s, L.splits, slab,
+                           tickets);
           break;
         case MODE_IMPLICIT: {
           ImplicitConv ic{zero, L.H, L.W, L.C, L.OH, L.OW, L.PH, L.PW, L.kh, L.kw, L.sh, L.sw, L.pt, L.pl,
                           L.pool ? 1 : 0};
           const long long M = L.pool ? 4LL * n * L.PH * L.PW : Mc;
           rc = launch_gemm_implicit(L.cfg, L.pool ? GEMM_IMPLICIT_POOL : GEMM_IMPLICIT, cur, ic, wt, L.Kpad, dst,
-                                    L.OC, M, L.OC, L.Kpad, epi, s, L.splits, slab);
+                                    L.OC, M, L.OC, L.Kpad, epi, s, L.splits, slab, tickets);
           break;
         }
         case MODE_DIRECT: {
@@ -650,7 +664,7 @@ int dnn_plan_run(dnn_plan* p, int n, const float* d_in, float* d_out, void* stre
         }
       }
       if (rc) return rc;
-      if (L.splits > 1) {
+      if (L.splits > 1 && !tickets) {
         if ((rc = record(p, ++k, s))) return rc;
         if ((rc = launch_splitk_reduce(slab, L.splits, Mc, L.OC, dst, L.OC, epi, s))) return rc;
       }
@@ -740,10 +754,10 @@ int dnn_plan_describe(const dnn_plan* p, char* buf, int buf_len) {
   for (size_t i = 0; i < p->layers.size(); ++i) {
     const PlanLayer& L = p->layers[i];
     if (L.type == 0)
-      snprintf(line, sizeof(line), "conv %dx%dx%d -> %dx%dx%d k%dx%d s%d mode=%s cfg=%d K=%d Kpad=%d%s%s%s\n", L.H,
+      snprintf(line, sizeof(line), "conv %dx%dx%d -> %dx%dx%d k%dx%d s%d mode=%s cfg=%d K=%d Kpad=%d%s%s%s%s\n", L.H,
                L.W, L.C, L.out_h(), L.out_w(), L.OC, L.kh, L.kw, L.sh, kModeName[L.mode], L.cfg, L.K, L.Kpad,
                L.pool ? " +pool2x2s2" : "", L.splits > 1 ? (L.splits == 3 ? " splitK=3" : " splitK") : "",
-               p->fp16 ? " fp16" : "");
+               L.splits > 1 && fused_splitk(p) ? " combine" : "", p->fp16 ? " fp16" : "");
     else
       snprintf(line, sizeof(line), "pool %dx%dx%d -> %dx%dx%d k%dx%d s%d%s\n", L.H, L.W, L.C, L.OH, L.OW, L.OC, L.kh,
                L.kw, L.sh, p->fp16 ? " fp16" : "");

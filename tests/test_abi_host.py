@@ -105,16 +105,22 @@ def test_lowering_rejects_unfusable_graph():
     assert dnn_hip.lower_graph(g) is None
 
 
-@pytest.mark.parametrize("fuse", ["1", "0"])
-def test_plan_shape_memory_and_flops_host_only(monkeypatch, fuse):
+@pytest.mark.parametrize("fuse,splitk", [("1", "1"), ("0", "1"), ("1", "0")])
+def test_plan_shape_memory_and_flops_host_only(monkeypatch, fuse, splitk):
     monkeypatch.setenv("DNN_HIP_FUSE", fuse)
+    monkeypatch.setenv("DNN_HIP_SPLITK_FUSED", splitk)
     ws = synth.yolo_weights()
     g, _ = yolo_graph.build_graph(dnn_hip.DnnGraphBuilder, ws, in_shape=(64, 416, 416, 3))
     entries = dnn_hip.lower_graph(g)
     wb, sb = dnn_hip.Plan.memory(64, (416, 416, 3), entries)
     nparams = sum(w["kernel"].size for w in ws)
     assert wb >= 4 * nparams and wb < 4 * nparams * 1.2
-    slab = 3 * 64 * 13 * 13 * 1024 * 4  # split-K partials of conv5/conv6/conv7 (3 splits)
+    if splitk == "1":
+        # fused combine: partial tiles in the accumulator-native layout, 85 x 2 tiles of 128 x 512
+        # (conv6/conv7 at M = 64*169 = 10,816), + one ticket per tile
+        slab = 85 * 2 * 128 * 512 * 3 * 4 + 192 * 4
+    else:
+        slab = 3 * 64 * 13 * 13 * 1024 * 4  # split-K partials of conv5/conv6/conv7 (3 splits)
     if fuse == "0":
         # two activation buffers (conv0 output, 64x416x416x16) + the largest col buffer
         assert sb >= 2 * 64 * 416 * 416 * 16 * 4 + slab
@@ -146,20 +152,26 @@ def test_plan_shape_memory_and_flops_host_only(monkeypatch, fuse):
         assert flops == pytest.approx(64 * 6.971e9, rel=1e-3)
         # the 1x1 conv8 reads its input directly (no im2col)
         assert "conv8.im2col" not in names and "conv8.gemm" in names and "conv7.gemm" in names
-        # conv5-7 (N >= 512, K >= 2048) run split-K = 3 + an ordered reduce kernel
-        assert "conv5.reduce" in names and "conv6.reduce" in names and "conv7.reduce" in names
+        # conv5-7 (N >= 512, K >= 2048) run split-K = 3: combined inside the GEMM by the last
+        # split of each tile, or (DNN_HIP_SPLITK_FUSED=0) by an ordered reduce kernel
+        nred = 0 if splitk == "1" else 3
+        assert sum(n.endswith(".reduce") for n in names) == nred
+        if splitk == "0":
+            assert "conv5.reduce" in names and "conv6.reduce" in names and "conv7.reduce" in names
         if fuse == "0":  # explicit im2col for every 3x3 conv, every pool separate
-            assert len(names) == 26
+            assert len(names) == 23 + nred
             assert sum(n.endswith(".im2col") for n in names) == 8
             assert sum(n.startswith("pool") for n in names) == 6
         else:  # conv0 direct + pool, conv1 patch + pool, conv2-7 implicit GEMM (2-5 with the pool), pool5 (s1)
-            assert names == ["conv0.direct", "conv1.patch", "conv2.gemm", "conv3.gemm", "conv4.gemm", "conv5.gemm",
-                             "conv5.reduce", "pool5", "conv6.gemm", "conv6.reduce", "conv7.gemm", "conv7.reduce", "conv8.gemm"]
+            want = ["conv0.direct", "conv1.patch", "conv2.gemm", "conv3.gemm", "conv4.gemm", "conv5.gemm",
+                    "conv5.reduce", "pool5", "conv6.gemm", "conv6.reduce", "conv7.gemm", "conv7.reduce", "conv8.gemm"]
+            assert names == [n for n in want if splitk == "0" or not n.endswith(".reduce")]
         buf = ctypes.create_string_buffer(8192)
         assert lib.dnn_plan_describe(h, buf, 8192) == 0
         desc = buf.value.decode()
-        assert desc.count("\n") == len(names) - 3 - (8 if fuse == "0" else 0)
+        assert desc.count("\n") == len(names) - nred - (8 if fuse == "0" else 0)
         assert desc.count("splitK=3") == 3
+        assert desc.count(" combine") == (3 if splitk == "1" else 0)
     finally:
         lib.dnn_plan_destroy(h)
 

@@ -432,7 +432,7 @@ def test_plan_timing_api(yolo_b1):
         plan.run_host(x)
     ms, cnt = plan.timing_end()
     ks = plan.kernels()
-    assert len(ms) == len(ks) == 13  # 10 layers + the conv5/6/7 split-K reduces
+    assert len(ms) == len(ks) == 10  # 10 plan kernels: conv5/6/7 combine their split-K partials in the GEMM
     assert all(c == 3 for c in cnt)
     assert all(m > 0 for m in ms)
 
@@ -551,6 +551,56 @@ def test_yolov2tiny_front_end_from_pickle(tmp_path, yolo_weights, golden_frames,
     # can move a truncated corner of a huge box by one pixel)
     gold = post_golden["net_frame0"][1]
     assert [b[0] for b in boxes] == [g[0] for g in gold]
+
+
+# ------------------------------------------------------------------ fused split-K combine
+SPLITK_CASES = [
+    # B, H, W, C, od, pool: K = 9*C >= 2048 and od >= 512 -> split-K 3 (128x512 / 128x256 tiles)
+    (64, 13, 13, 256, 512, (2, 1, "SAME")),  # conv5: 85 x 1 tiles, then the stride-1 pool
+    (64, 13, 13, 512, 1024, None),           # conv6: 85 x 2 tiles
+    (5, 13, 13, 512, 1024, None),            # ragged M = 845 (not a multiple of 128), few tiles
+    (3, 9, 7, 256, 768, None),               # N = 768 -> 128x256 tiles, M = 189
+]
+
+
+@pytest.mark.parametrize("case", SPLITK_CASES)
+def test_splitk_combine_in_gemm_equals_reduce_kernel(monkeypatch, case):
+    """The last-arriving split of each tile sums the partials in split order inside the GEMM
+    (agent-scope ticket, sc1 partials, gemm_f32.h splitk_combine): bit-identical to the
+    separate ordered reduce kernel (DNN_HIP_SPLITK_FUSED=0), within the layer tolerance of
+    the float64 oracle, and the same again on repeated runs and HIP-graph replays (the
+    tickets re-arm themselves)."""
+    B, H, W, C, od, pool = case
+    rng = np.random.default_rng(B + C + od)
+    x = rng.standard_normal((B, H, W, C)).astype(np.float32)
+    k = (rng.standard_normal((3, 3, C, od)) * np.sqrt(2.0 / (9 * C))).astype(np.float32)
+    bias = rng.standard_normal(od).astype(np.float32) * 0.1
+    gam = rng.uniform(0.5, 1.5, od).astype(np.float32)
+    gam[::7] *= -1  # negative gamma: the epilogue's decreasing branch
+    bn = (rng.standard_normal(od).astype(np.float32) * 0.1, rng.uniform(0.5, 1.5, od).astype(np.float32), gam)
+    kw = dict(bias=bias, bn=bn, leaky=True, pool=pool)
+    monkeypatch.setenv("DNN_HIP_SPLITK_FUSED", "0")
+    e_red = dnn_hip.DnnInferenceEngine(_chain(x.shape, k, **kw), False)
+    y_red = e_red.run(x)
+    assert "combine" not in e_red.plan().describe()
+    monkeypatch.setenv("DNN_HIP_SPLITK_FUSED", "1")
+    e_fus = dnn_hip.DnnInferenceEngine(_chain(x.shape, k, **kw), False)
+    assert "splitK=3 combine" in e_fus.plan().describe()
+    y1 = e_fus.run(x)
+    y2 = e_fus.run(x)
+    assert np.array_equal(y1, y_red) and np.array_equal(y2, y_red)
+    assert R.normwise_err(y1, _oracle_chain(x, k, **kw)) < LAYER_TOL
+    # device-resident runs and graph replays, with another layer's launch in between
+    import torch
+    plan = e_fus.plan()
+    xd = torch.from_numpy(x).cuda()
+    yd = torch.empty((B,) + plan.out_shape, device="cuda")
+    st = torch.cuda.Stream()
+    for it in range(3):
+        plan.run_graph(B, xd.data_ptr(), yd.data_ptr(), st.cuda_stream)
+        e_red.plan().run_host(x[:1])  # interleave other work
+    st.synchronize()
+    assert np.array_equal(yd.cpu().numpy(), y_red)
 
 
 # ------------------------------------------------------------------ fp16 path (BASELINE config 5)

@@ -17,9 +17,11 @@ import csv
 import json
 from collections import defaultdict
 
-# kernel order of one YOLOv2-tiny forward in the default (fused) plan
-ORDER = ["conv0.direct", "conv1.patch", "conv2.gemm", "conv3.gemm", "conv4.gemm", "conv5.gemm", "conv5.reduce", "pool5",
-         "conv6.gemm", "conv6.reduce", "conv7.gemm", "conv7.reduce", "conv8.gemm"]
+# kernel order of one YOLOv2-tiny forward in the default (fused) plan: conv5-7's split-K
+# partials are combined inside their GEMMs (DNN_HIP_SPLITK_FUSED=0 / --reduce: a separate
+# convN.reduce kernel after each)
+ORDER = ["conv0.direct", "conv1.patch", "conv2.gemm", "conv3.gemm", "conv4.gemm", "conv5.gemm", "pool5",
+         "conv6.gemm", "conv7.gemm", "conv8.gemm"]
 # ... the fp16 plan (dnn_plan_set_precision 1): conv1 patch kernel, f16->f32 output conversion
 ORDER_FP16 = ["conv0.direct", "conv1.patch", "conv2.gemm", "conv3.gemm", "conv4.gemm", "conv5.gemm", "conv5.reduce",
               "pool5", "conv6.gemm", "conv6.reduce", "conv7.gemm", "conv7.reduce", "conv8.gemm", "output.cvt"]
@@ -29,10 +31,18 @@ for _i in range(9):
     if _i < 8:
         ORDER_UNFUSED.append(f"conv{_i}.im2col")
     ORDER_UNFUSED.append(f"conv{_i}.gemm")
-    if _i in (5, 6, 7):
-        ORDER_UNFUSED.append(f"conv{_i}.reduce")
     if _i < 6:
         ORDER_UNFUSED.append(f"pool{_i}")
+
+def with_reduces(order):
+    """the same plan with a separate split-K reduce kernel after conv5/6/7's GEMM"""
+    out = []
+    for n in order:
+        out.append(n)
+        if n in ("conv5.gemm", "conv6.gemm", "conv7.gemm"):
+            out.append(n.replace(".gemm", ".reduce"))
+    return out
+
 
 # every kernel of the plan lives in namespace dnnhip; weight packing (finalize) and the
 # postprocessing kernels (after the forward) are not plan kernels
@@ -116,9 +126,12 @@ def main():
     ap.add_argument("--skip", type=int, default=0, help="warm-up dispatches per kernel to leave out of avg_us")
     ap.add_argument("--unfused", action="store_true", help="trace of a DNN_HIP_FUSE=0 run")
     ap.add_argument("--fp16", action="store_true", help="trace of a --precision fp16 run")
+    ap.add_argument("--reduce", action="store_true", help="trace of a DNN_HIP_SPLITK_FUSED=0 run (fp32)")
     a = ap.parse_args()
     if a.unfused:
         ORDER[:] = ORDER_UNFUSED
+    if a.reduce:
+        ORDER[:] = with_reduces(ORDER)
     if a.fp16:
         ORDER[:] = ORDER_FP16
     s = summarise(a.trace, a.fetch, a.write, a.skip)
