@@ -441,10 +441,46 @@ static dim3 stream_grid(long long total, int threads = 256) {
   return dim3((unsigned)(b < cap ? (b > 0 ? b : 1) : cap));
 }
 
+// Row form for C % 4 == 0: blockIdx.y = output row (b, oy), threads over (ox, channel quad) of
+// that row: one 32-bit division per output quad instead of four 64-bit ones (pool5 of the
+// plan: 0.019 -> see DESIGN.md).  Same comparisons as maxpool_nhwc_kernel.
+__global__ void __launch_bounds__(256)
+maxpool_rows_kernel(const float* __restrict__ in, float* __restrict__ out, PoolGeom g) {
+  const int cq = g.C >> 2;
+  const int idx = blockIdx.x * 256 + threadIdx.x;
+  if (idx >= g.OW * cq) return;
+  const int row = blockIdx.y, ox = idx / cq, c = (idx - ox * cq) * 4;
+  const int oy = row % g.OH, b = row / g.OH;
+  const int iy0 = oy * g.sh - g.pt, ix0 = ox * g.sw - g.pl;
+  const float* base = in + (size_t)b * g.H * g.W * g.C + c;
+  auto fetch = [&](int iy, int ix) {
+    if ((unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W)
+      return *reinterpret_cast<const f32x4*>(base + ((size_t)iy * g.W + ix) * g.C);
+    return f32x4{-FLT_MAX, -FLT_MAX, -FLT_MAX, -FLT_MAX};
+  };
+  f32x4 m = fetch(iy0, ix0);
+  for (int di = 0; di < g.kh; ++di)
+    for (int dj = 0; dj < g.kw; ++dj) {
+      const f32x4 x = fetch(iy0 + di, ix0 + dj);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        if (c + e < g.gt_below)
+          m[e] = m[e] > x[e] ? m[e] : x[e];
+        else
+          m[e] = m[e] >= x[e] ? m[e] : x[e];
+      }
+    }
+  *reinterpret_cast<f32x4*>(out + ((size_t)row * g.OW + ox) * g.C + c) = m;
+}
+
 int launch_maxpool(const float* in, float* out, const PoolGeom& g, hipStream_t stream) {
   long long outs = (long long)g.B * g.OH * g.OW;
   if (outs == 0 || g.C == 0) return 0;
-  if (g.C % 4 == 0) {
+  const long long rows = (long long)g.B * g.OH, per_row = (long long)g.OW * (g.C / 4);
+  if (g.C % 4 == 0 && rows <= 0x7fffffffLL && per_row <= 0x7fffffffLL && rows <= 65535) {
+    hipLaunchKernelGGL(maxpool_rows_kernel, dim3((unsigned)((per_row + 255) / 256), (unsigned)rows), dim3(256), 0,
+                       stream, in, out, g);
+  } else if (g.C % 4 == 0) {
     long long total = outs * (g.C / 4);
     hipLaunchKernelGGL(maxpool_nhwc_kernel<4>, stream_grid(total), dim3(256), 0, stream, in, out, g, total);
   } else {
