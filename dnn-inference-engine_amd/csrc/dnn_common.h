@@ -116,7 +116,7 @@ int launch_im2col(const float* in, float* col, const ConvGeom& g, hipStream_t st
 // With splits > 1 (LDS-DMA configs only) the GEMM writes `splits` raw fp32 partials
 // [splits][M][N] to `slab` and NO epilogue; launch_splitk_reduce then sums them in split order
 // and applies the epilogue into C.  choose_splitk depends on (N, K) only.
-int choose_splitk(int N, int K);
+int choose_splitk(int N, int K, bool combine = false);
 // With `tickets` (>= the cfg's tile count of unsigned, zero before the first launch and left
 // zero by every launch) the split-K GEMM finishes itself: the last-arriving split of each tile
 // sums the partials in split order and writes C with the epilogue (splitk_combine, gemm_f32.h),

@@ -172,7 +172,7 @@ int choose_gemm_cfg(long long M, int N, int K) {
   // K permutation, and the split itself depends on (N, K) only, so the summation order of an
   // output element never depends on M.
   long long t128 = ((M + 127) / 128) * ((N + 127) / 128);
-  const int s = choose_splitk(N, K);
+  const int s = choose_splitk(N, K, false);
   if (K >= 1024 && t128 * s >= 512) {
     // split-K layers (conv5-7): one wide workgroup per CU with 16 / 8 waves of 64x64 stages
     // 80 / 96 B per MFMA instead of 128 (128x128): less LDS-DMA and L2 traffic per flop, which
@@ -207,8 +207,12 @@ bool implicit_conv_supported(int C, int kh, int kw) {
 // including the reduce, tools/gemm_bench.hip, profiles/r01_gemm_bench_v2.txt); conv5's 340
 // tiles become 1020 units (1.99 rounds).  Chosen from (N, K) only so every batch size sums in
 // the same order.
-int choose_splitk(int N, int K) {
+int choose_splitk(int N, int K, bool combine) {
   if (N >= 512 && N % 4 == 0 && K >= 2048 && (K / 32) % 3 == 0) return 3;
+  // (measured: splitting conv8 (N = 125, K = 1024) in two K halves with the in-GEMM combine
+  // made it slower, 0.047 -> 0.050 ms at batch 64: the combine's acquire + partial round trip
+  // costs more than the extra units gain.  `combine` keeps the option for shapes where it pays.)
+  (void)combine;
   return 1;
 }
 
@@ -274,7 +278,7 @@ static int split_setup(int cfg, long long M, int N, int Kpad, int splits, float*
   *grid = tilesM * *tilesN;
   *sk = SplitK{0, *grid, 0};
   if (splits > 1) {
-    if (cfg < GEMM_128x128_K32 || !slab || (Kpad / 32) % splits != 0 || N % 4 != 0) {
+    if (cfg < GEMM_128x128_K32 || !slab || (Kpad / 32) % splits != 0 || (!tickets && N % 4 != 0)) {
       set_error("gemm: split-K %d unsupported for cfg %d Kpad %d N %d", splits, cfg, Kpad, N);
       return -2;
     }

@@ -286,7 +286,7 @@ static void set_cfg(dnn_plan* p, PlanLayer& L) {
   }
   L.Kpad = (int)align_up(L.K, gemm_cfg_bk(L.cfg));
   L.Npad = (int)align_up(L.OC, gemm_cfg_bn(L.cfg));
-  L.splits = (L.cfg >= GEMM_128x128_K32 && L.Kpad == L.K) ? choose_splitk(L.OC, L.K) : 1;
+  L.splits = (L.cfg >= GEMM_128x128_K32 && L.Kpad == L.K) ? choose_splitk(L.OC, L.K, fused_splitk(p)) : 1;
 }
 
 int dnn_plan_set_precision(dnn_plan* p, int precision) {

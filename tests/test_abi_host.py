@@ -117,7 +117,7 @@ def test_plan_shape_memory_and_flops_host_only(monkeypatch, fuse, splitk):
     assert wb >= 4 * nparams and wb < 4 * nparams * 1.2
     if splitk == "1":
         # fused combine: partial tiles in the accumulator-native layout, 85 x 2 tiles of 128 x 512
-        # (conv6/conv7 at M = 64*169 = 10,816), + one ticket per tile
+        # (conv6/conv7 at M = 64*169 = 10,816), + one ticket per tile (170 -> 192 words)
         slab = 85 * 2 * 128 * 512 * 3 * 4 + 192 * 4
     else:
         slab = 3 * 64 * 13 * 13 * 1024 * 4  # split-K partials of conv5/conv6/conv7 (3 splits)

@@ -205,6 +205,7 @@ FUSED_CASES = [
     (64, 13, 13, 96, 3, 1024, 1, "SAME", None),           # M=10816, N=1024 -> cfg 128x128 (conv7-like)
     (64, 13, 13, 256, 3, 1024, 1, "SAME", (2, 1, "SAME")),  # K=2304 -> split-K 3 on the 128x512 tile + reduce, s1 pool
     (3, 13, 13, 64, 1, 125, 1, "SAME", None),             # 1x1 direct path, ragged N=125
+    (4, 13, 13, 1024, 1, 125, 1, "SAME", None),           # conv8: 1x1, K=1024, N=125 (32x128 tiles)
     (2, 9, 11, 5, 3, 48, 2, "SAME", None),                # stride 2, K=45 not a multiple of BK
     (1, 10, 9, 8, 3, 24, 1, "VALID", None),               # VALID
 ]
