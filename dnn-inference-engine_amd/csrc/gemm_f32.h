@@ -480,12 +480,29 @@ __device__ __forceinline__ void splitk_combine(typename Mfma<MF>::acc_t (&acc)[T
   }
 }
 
+// Buffer-resource addressing of the LDS-DMA sources (ABUF kernels): A and Bt are read by
+// buffer_load ... lds with a per-lane 32-bit byte offset fixed for the whole tile (voffset) and
+// the K-step's position as a wave-uniform soffset, so a DMA costs no 64-bit address arithmetic;
+// a padding tap is a voffset past the descriptor's range (OOB_OFF), which the hardware turns
+// into zeros in LDS (no zero page).  For the implicit modes the A descriptor starts (W+1)*C
+// floats BEFORE the input, so every in-frame (pixel, tap) offset is non-negative.  The
+// launcher picks ABUF only when both descriptors fit 2^31 bytes.
+struct BufDesc {
+  const float* a;   // descriptor base of A (implicit: input - (W+1)*C)
+  unsigned a_bytes;
+  unsigned b_bytes; // Bt: Npad * ldb * 4
+};
+__device__ __forceinline__ void lds_dma16_buf(__amdgpu_buffer_rsrc_t r, unsigned voff, unsigned soff, float* dst) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)dst, 16, (int)voff, (int)soff,
+                                           0, 0);
+}
+
 // MODE 0: dense A (col buffer or 1x1 input), MODE 1: implicit conv, MODE 2: implicit + pool.
-template <int BM, int BN, int WM, int WN, int MF, int NS, int MODE>
+template <int BM, int BN, int WM, int WN, int MF, int NS, int MODE, bool ABUF = false>
 __global__ void __launch_bounds__(WM* WN * 64)
 gemm_f32_glds_kernel(const float* __restrict__ A, int lda, const float* __restrict__ Bt, int ldb,
                      float* __restrict__ C, int ldc, int M, int N, int K, EpiParams epi, int tilesN,
-                     ImplicitConv ic, SplitK sk) {
+                     ImplicitConv ic, SplitK sk, BufDesc bd) {
   typedef Mfma<MF> MM;
   typedef typename MM::acc_t acc_t;
   constexpr int BK = 32;
@@ -521,6 +538,7 @@ gemm_f32_glds_kernel(const float* __restrict__ A, int lda, const float* __restri
   // ---- A sources.  Chunk c (8 rows) of this wave: c = wid + i*NW; lane -> row 8c + lane/8,
   // logical 16-B slot ls = (lane&7) ^ ((row>>1)&7) (the source side of the LDS swizzle).
   const float* srcA[LPSA];  // dense: row pointer + slot (advanced by k0); implicit: pixel base
+  unsigned voA[LPSA];       // ABUF: byte offset of the same (dense: + slot; implicit: + slot, shifted base)
   int maskA[LPSA], lsA[LPSA];
 #pragma unroll
   for (int i = 0; i < LPSA; ++i) {
@@ -530,7 +548,10 @@ gemm_f32_glds_kernel(const float* __restrict__ A, int lda, const float* __restri
     const int m = m0 + r;
     if constexpr (MODE == 0) {
       const int gm = m < M ? m : M - 1;
-      srcA[i] = A + (size_t)gm * lda + kbeg + 4 * ls;
+      if constexpr (ABUF)
+        voA[i] = (unsigned)(((size_t)gm * lda + 4 * ls) * 4);
+      else
+        srcA[i] = A + (size_t)gm * lda + kbeg + 4 * ls;
       maskA[i] = 0;
     } else {
       int b = 0, oy = 0, ox = 0;
@@ -549,7 +570,10 @@ gemm_f32_glds_kernel(const float* __restrict__ A, int lda, const float* __restri
         b = t / ic.OH;
       }
       const int iy0 = oy * ic.sh - ic.pt, ix0 = ox * ic.sw - ic.pl;
-      srcA[i] = A + (((long long)b * ic.H + iy0) * ic.W + ix0) * (long long)ic.C;
+      if constexpr (ABUF)
+        voA[i] = (unsigned)(((((long long)b * ic.H + iy0) * ic.W + ix0 + ic.W + 1) * ic.C + 4 * ls) * 4);
+      else
+        srcA[i] = A + (((long long)b * ic.H + iy0) * ic.W + ix0) * (long long)ic.C;
       int mk = 0;
       if (rv) {
         for (int dy = 0; dy < ic.kh; ++dy)
@@ -561,12 +585,19 @@ gemm_f32_glds_kernel(const float* __restrict__ A, int lda, const float* __restri
     }
   }
   const float* srcB[LPSB];
+  unsigned voB[LPSB];
 #pragma unroll
   for (int j = 0; j < LPSB; ++j) {
     const int r = 8 * (wid + j * NW) + (lane >> 3);
     const int ls = (lane & 7) ^ ((r >> 1) & 7);
-    srcB[j] = Bt + (size_t)(n0 + r) * ldb + kbeg + 4 * ls;
+    if constexpr (ABUF)
+      voB[j] = (unsigned)(((size_t)(n0 + r) * ldb + 4 * ls) * 4);
+    else
+      srcB[j] = Bt + (size_t)(n0 + r) * ldb + kbeg + 4 * ls;
   }
+  // (built unconditionally: unused, and dropped, in the flat-address instantiation)
+  const auto rsA = __builtin_amdgcn_make_buffer_rsrc((void*)bd.a, 0, (int)bd.a_bytes, 0x00020000);
+  const auto rsB = __builtin_amdgcn_make_buffer_rsrc((void*)Bt, 0, (int)bd.b_bytes, 0x00020000);
 
   // implicit mode: wave-uniform position of the next K-step to issue, k = tap*C + c
   int cb = 0, tapb = 0, dyb = 0, dxb = 0, dyn = 0, dxn = 1;
@@ -583,6 +614,36 @@ gemm_f32_glds_kernel(const float* __restrict__ A, int lda, const float* __restri
   const bool aligned = MODE != 0 && (ic.C % BK) == 0;  // wave-uniform
   auto issue = [&](int stage, int k0) {
     float* base = smem + stage * STAGE;
+    if constexpr (ABUF) {
+      // MODE 0: every lane at its row's k0; implicit (C % 32 == 0 only): one tap per K-step, the
+      // tap + channel offset uniform in soffset, the tap mask choosing voffset or OOB
+      const unsigned koff = (unsigned)((kbeg + k0) * 4);
+      const unsigned soffA =
+          MODE == 0 ? koff : (unsigned)((((long long)dyb * ic.W + dxb) * ic.C + cb) * 4);
+#pragma unroll
+      for (int i = 0; i < LPSA; ++i) {
+        const unsigned vo = (MODE == 0 || ((maskA[i] >> tapb) & 1)) ? voA[i] : OOB_OFF;
+        lds_dma16_buf(rsA, vo, soffA, base + (wid + i * NW) * 256);
+      }
+#pragma unroll
+      for (int j = 0; j < LPSB; ++j) lds_dma16_buf(rsB, voB[j], koff, base + (A_CH + wid + j * NW) * 256);
+      if constexpr (MODE != 0) {  // one tap per K-step: C % 32 == 0
+        cb += BK;
+        if (cb >= ic.C) {
+          cb = 0;
+          ++tapb;
+          dyb = dyn;
+          dxb = dxn;
+          if (dxn + 1 == ic.kw) {
+            dxn = 0;
+            ++dyn;
+          } else {
+            ++dxn;
+          }
+        }
+      }
+      return;
+    }
     const long long tap_off = MODE != 0 ? (long long)dyb * rowstride + (long long)dxb * ic.C + cb : 0;
 #pragma unroll
     for (int i = 0; i < LPSA; ++i) {

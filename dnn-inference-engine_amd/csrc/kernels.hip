@@ -180,7 +180,9 @@ int choose_gemm_cfg(long long M, int N, int K) {
     // conv7 1.632 -> 1.59 ms).  Same MFMA family and K order: results are unchanged bit for bit.
     if (s > 1 && N % 512 == 0) return GEMM_128x512_W16;
     if (s > 1 && N % 256 == 0) return GEMM_128x256_W8;
-    return GEMM_128x128_K32;
+    // unsplit long-K layers (conv4: N = 256, K = 1152): with buffer-addressed DMA the 64x128
+    // ring (3 per CU) beats 128x128 (2 per CU, 1.3 rounds at batch 64): 0.273 -> 0.224 ms
+    if (s > 1) return GEMM_128x128_K32;
   }
   // small M (batch 1 and the like): 64x128 would leave most CUs idle and each workgroup
   // waiting on a 2-stage ring; 32-row tiles with a 4-stage ring (same family, same K order)
@@ -216,48 +218,29 @@ int choose_splitk(int N, int K, bool combine) {
   return 1;
 }
 
-// LDS-DMA configs 3..6 for one A mode (dense / implicit / implicit + pool)
-template <int MODE>
-static int launch_glds(int cfg, const float* A, int lda, const float* Bt, int ldb, float* C, int ldc, int m, int N,
-                       int Kpad, const EpiParams& epi, int tilesN, const ImplicitConv& ic, const SplitK& sk,
-                       dim3 grid, hipStream_t stream) {
+// LDS-DMA configs for one A mode (dense / implicit / implicit + pool); `abuf`: buffer-resource
+// addressed DMA (BufDesc, gemm_f32.h), else flat 64-bit addresses
+template <int MODE, bool ABUF>
+static int launch_glds_t(int cfg, const float* A, int lda, const float* Bt, int ldb, float* C, int ldc, int m, int N,
+                         int Kpad, const EpiParams& epi, int tilesN, const ImplicitConv& ic, const SplitK& sk,
+                         const BufDesc& bd, dim3 grid, hipStream_t stream) {
+#define DNN_GLDS(BM_, BN_, WM_, WN_, MF_, NS_)                                                                      \
+  hipLaunchKernelGGL((gemm_f32_glds_kernel<BM_, BN_, WM_, WN_, MF_, NS_, MODE, ABUF>), grid, dim3(WM_ * WN_ * 64), 0, \
+                     stream, A, lda, Bt, ldb, C, ldc, m, N, Kpad, epi, tilesN, ic, sk, bd)
   switch (cfg) {
-    case GEMM_128x128_K32:
-      hipLaunchKernelGGL((gemm_f32_glds_kernel<128, 128, 2, 2, 32, 2, MODE>), grid, dim3(256), 0, stream, A, lda,
-                         Bt, ldb, C, ldc, m, N, Kpad, epi, tilesN, ic, sk);
-      break;
-    case GEMM_64x128_K32:
-      hipLaunchKernelGGL((gemm_f32_glds_kernel<64, 128, 2, 2, 32, 2, MODE>), grid, dim3(256), 0, stream, A, lda,
-                         Bt, ldb, C, ldc, m, N, Kpad, epi, tilesN, ic, sk);
-      break;
-    case GEMM_G64x32_K32:
-      hipLaunchKernelGGL((gemm_f32_glds_kernel<64, 32, 4, 1, 16, 2, MODE>), grid, dim3(256), 0, stream, A, lda,
-                         Bt, ldb, C, ldc, m, N, Kpad, epi, tilesN, ic, sk);
-      break;
-    case GEMM_G256x64_K32:
-      hipLaunchKernelGGL((gemm_f32_glds_kernel<256, 64, 4, 2, 32, 2, MODE>), grid, dim3(512), 0, stream, A, lda,
-                         Bt, ldb, C, ldc, m, N, Kpad, epi, tilesN, ic, sk);
-      break;
-    case GEMM_G32x128_NS4:
-      hipLaunchKernelGGL((gemm_f32_glds_kernel<32, 128, 1, 4, 32, 4, MODE>), grid, dim3(256), 0, stream, A, lda,
-                         Bt, ldb, C, ldc, m, N, Kpad, epi, tilesN, ic, sk);
-      break;
-    case GEMM_G32x64_NS4:
-      hipLaunchKernelGGL((gemm_f32_glds_kernel<32, 64, 1, 2, 32, 4, MODE>), grid, dim3(128), 0, stream, A, lda,
-                         Bt, ldb, C, ldc, m, N, Kpad, epi, tilesN, ic, sk);
-      break;
-    case GEMM_128x256_W8:
-      hipLaunchKernelGGL((gemm_f32_glds_kernel<128, 256, 2, 4, 32, 2, MODE>), grid, dim3(512), 0, stream, A, lda,
-                         Bt, ldb, C, ldc, m, N, Kpad, epi, tilesN, ic, sk);
-      break;
-    case GEMM_128x512_W16:
-      hipLaunchKernelGGL((gemm_f32_glds_kernel<128, 512, 2, 8, 32, 2, MODE>), grid, dim3(1024), 0, stream, A, lda,
-                         Bt, ldb, C, ldc, m, N, Kpad, epi, tilesN, ic, sk);
-      break;
+    case GEMM_128x128_K32: DNN_GLDS(128, 128, 2, 2, 32, 2); break;
+    case GEMM_64x128_K32: DNN_GLDS(64, 128, 2, 2, 32, 2); break;
+    case GEMM_G64x32_K32: DNN_GLDS(64, 32, 4, 1, 16, 2); break;
+    case GEMM_G256x64_K32: DNN_GLDS(256, 64, 4, 2, 32, 2); break;
+    case GEMM_G32x128_NS4: DNN_GLDS(32, 128, 1, 4, 32, 4); break;
+    case GEMM_G32x64_NS4: DNN_GLDS(32, 64, 1, 2, 32, 4); break;
+    case GEMM_128x256_W8: DNN_GLDS(128, 256, 2, 4, 32, 2); break;
+    case GEMM_128x512_W16: DNN_GLDS(128, 512, 2, 8, 32, 2); break;
     default:
       set_error("gemm: cfg %d is not an LDS-DMA config", cfg);
       return -2;
   }
+#undef DNN_GLDS
   return check_launch("gemm_glds");
 }
 
@@ -266,6 +249,27 @@ long long splitk_tiles(int cfg, long long M, int N) {
 }
 long long splitk_fused_slab_floats(int cfg, long long M, int N, int splits) {
   return splitk_tiles(cfg, M, N) * kCfgs[cfg].bm * kCfgs[cfg].bn * splits;
+}
+
+template <int MODE>
+static int launch_glds(int cfg, const float* A, int lda, const float* Bt, int ldb, float* C, int ldc, int m, int N,
+                       int Kpad, const EpiParams& epi, int tilesN, const ImplicitConv& ic, const SplitK& sk,
+                       const BufDesc* bd, dim3 grid, hipStream_t stream) {
+  if (bd)
+    return launch_glds_t<MODE, true>(cfg, A, lda, Bt, ldb, C, ldc, m, N, Kpad, epi, tilesN, ic, sk, *bd, grid, stream);
+  return launch_glds_t<MODE, false>(cfg, A, lda, Bt, ldb, C, ldc, m, N, Kpad, epi, tilesN, ic, sk, BufDesc{}, grid,
+                                    stream);
+}
+
+// buffer descriptors fit (offsets are 32-bit, OOB_OFF = 2^31 marks padding taps)?
+static bool fits_buf(long long bytes) { return bytes > 0 && bytes < 0x80000000LL; }
+static bool g_abuf_checked = false, g_abuf_on = true;
+static bool abuf_enabled() {
+  if (!g_abuf_checked) {
+    g_abuf_on = !getenv_flag_off("DNN_HIP_GEMM_BUF");
+    g_abuf_checked = true;
+  }
+  return g_abuf_on;
 }
 
 // grid and SplitK descriptor for `splits` (> 1: the kernel writes raw partials to `slab`;
@@ -334,9 +338,13 @@ int launch_gemm(int cfg, const float* A, int lda, const float* Bt, int ldb, floa
       hipLaunchKernelGGL((gemm_f32_mfma_kernel<128, 64, 32, 2, 2, 32>), grid, dim3(256), 0, stream, A, lda,
                          Bt, ldb, C, ldc, m, N, Kpad, epi, tilesN);
       break;
-    default:
+    default: {
+      const long long a_bytes = (M * (long long)lda) * 4, b_bytes = (long long)tilesN * ci.bn * ldb * 4;
+      BufDesc bd{A, (unsigned)a_bytes, (unsigned)b_bytes};
+      const bool abuf = abuf_enabled() && fits_buf(a_bytes) && fits_buf(b_bytes);
       return launch_glds<GEMM_DENSE>(cfg, A, lda, Bt, ldb, sk.steps ? slab : C, sk.steps ? N : ldc, m, N, Kpad,
-                                     epi, tilesN, ImplicitConv{}, sk, grid, stream);
+                                     epi, tilesN, ImplicitConv{}, sk, abuf ? &bd : nullptr, grid, stream);
+    }
   }
   return check_launch("gemm");
 }
@@ -360,10 +368,18 @@ int launch_gemm_implicit(int cfg, int mode, const float* in, const ImplicitConv&
   if (int rc = split_setup(cfg, M, N, Kpad, splits, slab, tickets, C, ldc, epi.flags, &sk, &g, &tilesN)) return rc;
   float* out = sk.steps ? slab : C;
   const int ldo = sk.steps ? N : ldc;
+  // buffer-addressed DMA when each K-step is one tap (C % 32 == 0) and the descriptors fit
+  const long long per_img = mode == GEMM_IMPLICIT_POOL ? 4LL * ic.PH * ic.PW : (long long)ic.OH * ic.OW;
+  const long long nimg = per_img > 0 ? M / per_img : 0;
+  const long long a_bytes = ((nimg * ic.H * ic.W + ic.W + 1) * (long long)ic.C) * 4;
+  const long long b_bytes = (long long)tilesN * ci.bn * ldb * 4;
+  BufDesc bd{in - (size_t)(ic.W + 1) * ic.C, (unsigned)a_bytes, (unsigned)b_bytes};
+  const BufDesc* pbd =
+      (abuf_enabled() && ic.C % 32 == 0 && fits_buf(a_bytes) && fits_buf(b_bytes)) ? &bd : nullptr;
   if (mode == GEMM_IMPLICIT)
-    return launch_glds<GEMM_IMPLICIT>(cfg, in, 0, Bt, ldb, out, ldo, (int)M, N, Kpad, epi, tilesN, ic, sk, dim3(g),
-                                      stream);
-  return launch_glds<GEMM_IMPLICIT_POOL>(cfg, in, 0, Bt, ldb, out, ldo, (int)M, N, Kpad, epi, tilesN, ic, sk,
+    return launch_glds<GEMM_IMPLICIT>(cfg, in, 0, Bt, ldb, out, ldo, (int)M, N, Kpad, epi, tilesN, ic, sk, pbd,
+                                      dim3(g), stream);
+  return launch_glds<GEMM_IMPLICIT_POOL>(cfg, in, 0, Bt, ldb, out, ldo, (int)M, N, Kpad, epi, tilesN, ic, sk, pbd,
                                          dim3(g), stream);
 }
 

@@ -72,10 +72,12 @@ Variant impl(const char* nm) {
             const int grid = ((M + BM - 1) / BM) * tilesN;
             if (ic.pool)
               hipLaunchKernelGGL((gemm_f32_glds_kernel<BM, BN, WM, WN, MF, NS, GEMM_IMPLICIT_POOL>), dim3(grid),
-                                 dim3(WM * WN * 64), 0, s, in, 0, Bt, Kpad, out, N, M, N, Kpad, epi, tilesN, ic);
+                                 dim3(WM * WN * 64), 0, s, in, 0, Bt, Kpad, out, N, M, N, Kpad, epi, tilesN, ic,
+                                 SplitK{0, 0, 0}, BufDesc{});
             else
               hipLaunchKernelGGL((gemm_f32_glds_kernel<BM, BN, WM, WN, MF, NS, GEMM_IMPLICIT>), dim3(grid),
-                                 dim3(WM * WN * 64), 0, s, in, 0, Bt, Kpad, out, N, M, N, Kpad, epi, tilesN, ic);
+                                 dim3(WM * WN * 64), 0, s, in, 0, Bt, Kpad, out, N, M, N, Kpad, epi, tilesN, ic,
+                                 SplitK{0, 0, 0}, BufDesc{});
           }};
 }
 

@@ -65,14 +65,16 @@ Variant glds_variant(const char* nm) {
             int tilesN = (N + BN - 1) / BN;
             if (SPLIT == 1) {
               hipLaunchKernelGGL((gemm_f32_glds_kernel<BM, BN, WM, WN, MF, NS, 0>), dim3(grid), dim3(WM * WN * 64), 0,
-                                 s, A, lda, B, ldb, C, ldc, M, N, K, e, tilesN, ImplicitConv{}, SplitK{0, 0, 0});
+                                 s, A, lda, B, ldb, C, ldc, M, N, K, e, tilesN, ImplicitConv{}, SplitK{0, 0, 0},
+                                 BufDesc{});
             } else {
               SplitK sk{K / 32 / SPLIT, grid, (long long)M * N};
               hipLaunchKernelGGL((gemm_f32_glds_kernel<BM, BN, WM, WN, MF, NS, 0>), dim3(grid * SPLIT),
                                  dim3(WM * WN * 64), 0, s, A, lda, B, ldb, g_slab, N, M, N, K, e, tilesN,
-                                 ImplicitConv{}, sk);
-              hipLaunchKernelGGL(splitk_reduce_kernel, dim3(2048), dim3(256), 0, s, g_slab, SPLIT, sk.slab, C, M, N,
-                                 ldc, e);
+                                 ImplicitConv{}, sk, BufDesc{});
+              const int nqb = N / 4 < 256 ? N / 4 : 256, rp = 256 / nqb;
+              hipLaunchKernelGGL(splitk_reduce_kernel<float>, dim3(2048), dim3(256), 0, s, g_slab, SPLIT, sk.slab, C, M,
+                                 N, ldc, e, nqb, rp);
             }
           }};
 }
