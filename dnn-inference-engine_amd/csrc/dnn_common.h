@@ -178,9 +178,12 @@ int choose_splitk16(int N, int K);
 int gemm16_cfg_bn(int cfg);
 // mode: GEMM_DENSE (A = [M][lda] fp16), GEMM_IMPLICIT / GEMM_IMPLICIT_POOL (A = NHWC fp16 input
 // described by ic; C % 8 == 0).  Kpad % 64 == 0; C is fp16 [M][ldc]; split-K partials in slab.
+// `tickets`: in-GEMM split-K combine as for launch_gemm (slab: splitk16_fused_slab_floats).
 int launch_gemm16(int cfg, int mode, const half_t* A, int lda, const ImplicitConv& ic, const half_t* Bt, int ldb,
                   half_t* C, int ldc, long long M, int N, int Kpad, const EpiParams& epi, hipStream_t stream,
-                  int splits = 1, float* slab = nullptr);
+                  int splits = 1, float* slab = nullptr, unsigned* tickets = nullptr);
+long long splitk16_fused_slab_floats(int cfg, long long M, int N, int splits);
+long long splitk16_tiles(int cfg, long long M, int N);
 int launch_splitk_reduce16(const float* slab, int splits, long long M, int N, half_t* C, int ldc,
                            const EpiParams& epi, hipStream_t stream);
 int launch_f32_to_f16(const float* in, half_t* out, long long n, hipStream_t s);

@@ -26,11 +26,15 @@ __device__ __forceinline__ f32x16 mfma_f16(f16x8 a, f16x8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
 }
 
-template <int BM, int BN, int WM, int WN, int NS, int MODE, typename OutT>
+// ABUF: buffer-descriptor LDS-DMA as in gemm_f32.h (BufDesc): per-lane 32-bit voffsets fixed per
+// tile, the K-step in a uniform soffset, padding taps as OOB offsets (zero-filled).  Implicit
+// mode supports it for C % 64 == 0 (one tap per 64-half K-step) and C == 32 (two taps per
+// K-step: slots 4..7 of a row take the next tap, one uniform tap-to-tap delta).
+template <int BM, int BN, int WM, int WN, int NS, int MODE, typename OutT, bool ABUF = false>
 __global__ void __launch_bounds__(WM* WN * 64)
 gemm_f16_glds_kernel(const half_t* __restrict__ A, int lda, const half_t* __restrict__ Bt, int ldb,
                      OutT* __restrict__ C, float* __restrict__ slab, int ldc, int M, int N, int K, EpiParams epi,
-                     int tilesN, ImplicitConv ic, SplitK sk) {
+                     int tilesN, ImplicitConv ic, SplitK sk, BufDesc bd) {
   typedef Mfma<32> MM;
   constexpr int BK = 64;  // halves per K-step = 128 B per LDS row
   constexpr int NW = WM * WN;
@@ -47,14 +51,14 @@ gemm_f16_glds_kernel(const half_t* __restrict__ A, int lda, const half_t* __rest
   __shared__ int toff[32];  // implicit: tap -> element offset of (dy, dx) from the window origin
 
   int tile = xcd_tile(blockIdx.x, gridDim.x);
-  int kbeg = 0;
+  int kbeg = 0, split_idx = 0;
   const bool split = sk.steps > 0;
   if (split) {
-    const int s = tile / sk.ntile;
-    tile -= s * sk.ntile;
-    kbeg = s * sk.steps * BK;
+    split_idx = tile / sk.ntile;
+    tile -= split_idx * sk.ntile;
+    kbeg = split_idx * sk.steps * BK;
     K = sk.steps * BK;
-    slab += s * sk.slab;
+    if (!sk.tickets) slab += split_idx * sk.slab;
   }
   const int tm_ = tile / tilesN, tn_ = tile - tm_ * tilesN;
   const int m0 = tm_ * BM, n0 = tn_ * BN;
@@ -73,16 +77,22 @@ gemm_f16_glds_kernel(const half_t* __restrict__ A, int lda, const half_t* __rest
   // ---- A sources (chunk c = wid + i*NW holds rows 8c..8c+7; lane -> row 8c + lane/8 and
   // logical 16-B slot ls = (lane&7) ^ ((row>>1)&7))
   const half_t* srcA[LPSA];
-  int maskA[LPSA], lsA[LPSA];
+  unsigned voA[LPSA];  // ABUF byte offsets (implicit: shifted base, + slot channel)
+  int maskA[LPSA], lsA[LPSA], secA[LPSA];
+  const bool two_taps = MODE != 0 && ic.C == 32;  // ABUF implicit with C == 32
 #pragma unroll
   for (int i = 0; i < LPSA; ++i) {
     const int r = 8 * (wid + i * NW) + (lane >> 3);
     const int ls = (lane & 7) ^ ((r >> 1) & 7);
     lsA[i] = 8 * ls;  // halves
+    secA[i] = two_taps && ls >= 4 ? 1 : 0;
     const int m = m0 + r;
     if constexpr (MODE == 0) {
       const int gm = m < M ? m : M - 1;
-      srcA[i] = A + (size_t)gm * lda + kbeg + 8 * ls;
+      if constexpr (ABUF)
+        voA[i] = (unsigned)(((size_t)gm * lda + 8 * ls) * 2);
+      else
+        srcA[i] = A + (size_t)gm * lda + kbeg + 8 * ls;
       maskA[i] = 0;
     } else {
       int b = 0, oy = 0, ox = 0;
@@ -101,7 +111,10 @@ gemm_f16_glds_kernel(const half_t* __restrict__ A, int lda, const half_t* __rest
         b = t / ic.OH;
       }
       const int iy0 = oy * ic.sh - ic.pt, ix0 = ox * ic.sw - ic.pl;
-      srcA[i] = A + (((long long)b * ic.H + iy0) * ic.W + ix0) * (long long)ic.C;
+      if constexpr (ABUF)
+        voA[i] = (unsigned)(((((long long)b * ic.H + iy0) * ic.W + ix0 + ic.W + 1) * ic.C + 8 * (two_taps ? (ls & 3) : ls)) * 2);
+      else
+        srcA[i] = A + (((long long)b * ic.H + iy0) * ic.W + ix0) * (long long)ic.C;
       int mk = 0;
       if (rv) {
         for (int dy = 0; dy < ic.kh; ++dy)
@@ -113,12 +126,18 @@ gemm_f16_glds_kernel(const half_t* __restrict__ A, int lda, const half_t* __rest
     }
   }
   const half_t* srcB[LPSB];
+  unsigned voB[LPSB];
 #pragma unroll
   for (int j = 0; j < LPSB; ++j) {
     const int r = 8 * (wid + j * NW) + (lane >> 3);
     const int ls = (lane & 7) ^ ((r >> 1) & 7);
-    srcB[j] = Bt + (size_t)(n0 + r) * ldb + kbeg + 8 * ls;
+    if constexpr (ABUF)
+      voB[j] = (unsigned)(((size_t)(n0 + r) * ldb + 8 * ls) * 2);
+    else
+      srcB[j] = Bt + (size_t)(n0 + r) * ldb + kbeg + 8 * ls;
   }
+  const auto rsA = __builtin_amdgcn_make_buffer_rsrc((void*)bd.a, 0, (int)bd.a_bytes, 0x00020000);
+  const auto rsB = __builtin_amdgcn_make_buffer_rsrc((void*)Bt, 0, (int)bd.b_bytes, 0x00020000);
 
   // implicit: uniform cursor (tap, channel) of the next K-step's first element
   int tapb = 0, cb = 0;
@@ -130,6 +149,30 @@ gemm_f16_glds_kernel(const half_t* __restrict__ A, int lda, const half_t* __rest
 
   auto issue = [&](int stage, int k0) {
     float* base = smem + stage * STAGE;
+    if constexpr (ABUF) {
+      const unsigned koff = (unsigned)((kbeg + k0) * 2);
+      unsigned soffA = koff, dsec = 0;
+      if constexpr (MODE != 0) {
+        soffA = (unsigned)((toff[tapb] + cb) * 2);
+        dsec = (unsigned)((toff[tapb + 1] - toff[tapb]) * 2);
+      }
+#pragma unroll
+      for (int i = 0; i < LPSA; ++i) {
+        unsigned vo = voA[i];
+        if constexpr (MODE != 0) vo = ((maskA[i] >> (tapb + secA[i])) & 1) ? vo + (secA[i] ? dsec : 0u) : OOB_OFF;
+        lds_dma16_buf(rsA, vo, soffA, base + (wid + i * NW) * 256);
+      }
+#pragma unroll
+      for (int j = 0; j < LPSB; ++j) lds_dma16_buf(rsB, voB[j], koff, base + (A_CH + wid + j * NW) * 256);
+      if constexpr (MODE != 0) {
+        cb += BK;
+        while (cb >= ic.C) {
+          cb -= ic.C;
+          ++tapb;
+        }
+      }
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < LPSA; ++i) {
       const void* s;
@@ -210,6 +253,15 @@ gemm_f16_glds_kernel(const half_t* __restrict__ A, int lda, const half_t* __rest
     stage = stage + 1 == NS ? 0 : stage + 1;
   }
   const int wm = wm_of(wid, WN), wn = wn_of(wid, WN);
+  if (split && sk.tickets) {  // in-GEMM combine (gemm_f32.h splitk_combine), output OutT
+    if (sk.splits == 3)
+      splitk_combine<3, 32, TM, TN, WTM, WTN, NW, OutT>(acc, slab, sk, split_idx, tile, M, N, m0, n0, wm, wn, wid, lane,
+                                                        epi, reinterpret_cast<unsigned*>(smem));
+    else
+      splitk_combine<2, 32, TM, TN, WTM, WTN, NW, OutT>(acc, slab, sk, split_idx, tile, M, N, m0, n0, wm, wn, wid, lane,
+                                                        epi, reinterpret_cast<unsigned*>(smem));
+    return;
+  }
   if (split) {
     EpiParams raw = epi;
     raw.flags = 0;  // raw partial sums; the reduce kernel applies the epilogue

@@ -352,7 +352,7 @@ struct SplitK {
   // in the accumulator-native layout, the LAST split of a tile to arrive (agent-scope ticket)
   // sums all partials in split order and runs the epilogue into `out` (splitk_combine)
   unsigned* tickets = nullptr;
-  float* out = nullptr;
+  float* out = nullptr;  // OutT* of the kernel (fp16 activations on the fp16 path)
   int ldo = 0;
   int flags = 0;     // epilogue of the final output
   int splits = 1;
@@ -405,7 +405,7 @@ splitk_reduce_kernel(const float* __restrict__ part, int splits, long long slab,
 // ((p0 + p1) + p2 ..., the separate reduce kernel's order, so the same bits) with its own
 // partial taken from registers, the epilogue, and the row-major store.  It re-arms the ticket
 // (0) for the next launch.  Partial tile (split s, tile t) starts at slab + (s*ntile + t)*BM*BN.
-template <int SPL, int MF, int TM, int TN, int WTM, int WTN, int NW>
+template <int SPL, int MF, int TM, int TN, int WTM, int WTN, int NW, typename OutT = float>
 __device__ __forceinline__ void splitk_combine(typename Mfma<MF>::acc_t (&acc)[TM][TN], float* __restrict__ slab,
                                                const SplitK& sk, int s, int tile, int M, int N, int m0, int n0,
                                                int wm, int wn, int wid, int lane, const EpiParams& epi0,
@@ -473,7 +473,9 @@ __device__ __forceinline__ void splitk_combine(typename Mfma<MF>::acc_t (&acc)[T
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int m = m0 + wm * WTM + i * MF + MM::out_row(lane, 4 * q + e);
-          if (m < M) sk.out[(size_t)m * sk.ldo + n] = apply_epilogue(v[e], pb, pm, ps, pg, epi.flags);
+          if (m < M)
+            store_out(reinterpret_cast<OutT*>(sk.out) + (size_t)m * sk.ldo + n,
+                      apply_epilogue(v[e], pb, pm, ps, pg, epi.flags));
         }
       }
     }

@@ -263,14 +263,8 @@ static int launch_glds(int cfg, const float* A, int lda, const float* Bt, int ld
 
 // buffer descriptors fit (offsets are 32-bit, OOB_OFF = 2^31 marks padding taps)?
 static bool fits_buf(long long bytes) { return bytes > 0 && bytes < 0x80000000LL; }
-static bool g_abuf_checked = false, g_abuf_on = true;
-static bool abuf_enabled() {
-  if (!g_abuf_checked) {
-    g_abuf_on = !getenv_flag_off("DNN_HIP_GEMM_BUF");
-    g_abuf_checked = true;
-  }
-  return g_abuf_on;
-}
+// DNN_HIP_GEMM_BUF=0: flat 64-bit DMA addresses (experiments and the equivalence tests)
+static bool abuf_enabled() { return !getenv_flag_off("DNN_HIP_GEMM_BUF"); }
 
 // grid and SplitK descriptor for `splits` (> 1: the kernel writes raw partials to `slab`;
 // with `tickets` it also combines them itself into C)

@@ -42,16 +42,23 @@ int choose_gemm16_cfg(long long M, int N, int K) {
   return GEMM16_64x128;
 }
 
-template <int MODE>
+long long splitk16_tiles(int cfg, long long M, int N) {
+  return ((M + kCfg16[cfg].bm - 1) / kCfg16[cfg].bm) * ((N + kCfg16[cfg].bn - 1) / kCfg16[cfg].bn);
+}
+long long splitk16_fused_slab_floats(int cfg, long long M, int N, int splits) {
+  return splitk16_tiles(cfg, M, N) * kCfg16[cfg].bm * kCfg16[cfg].bn * splits;
+}
+
+template <int MODE, bool ABUF>
 static int launch16(int cfg, const half_t* A, int lda, const half_t* Bt, int ldb, half_t* C, float* slab, int ldc,
                     int M, int N, int Kpad, const EpiParams& epi, int tilesN, const ImplicitConv& ic,
-                    const SplitK& sk, dim3 grid, hipStream_t st) {
+                    const SplitK& sk, const BufDesc& bd, dim3 grid, hipStream_t st) {
   // 8 waves (two workgroups -> 4 waves per SIMD) on the 128- and 64-row tiles: the f16 GEMM
   // is LDS/L2-latency bound, and 8 waves of 32x64 / 32x32 beat 4 of 64x64 / 32x64 by 13-15%
   // on conv2-7 (MI355X, batch 64).  The wave layout does not change any summation order.
 #define DNN_L16(BM_, BN_, WM_, WN_, NS_)                                                                     \
-  hipLaunchKernelGGL((gemm_f16_glds_kernel<BM_, BN_, WM_, WN_, NS_, MODE, half_t>), grid, dim3(WM_ * WN_ * 64), \
-                     0, st, A, lda, Bt, ldb, C, slab, ldc, M, N, Kpad, epi, tilesN, ic, sk)
+  hipLaunchKernelGGL((gemm_f16_glds_kernel<BM_, BN_, WM_, WN_, NS_, MODE, half_t, ABUF>), grid,                 \
+                     dim3(WM_ * WN_ * 64), 0, st, A, lda, Bt, ldb, C, slab, ldc, M, N, Kpad, epi, tilesN, ic, sk, bd)
   switch (cfg) {
     case GEMM16_128x128: DNN_L16(128, 128, 4, 2, 2); break;
     case GEMM16_64x128: DNN_L16(64, 128, 2, 4, 2); break;
@@ -68,9 +75,19 @@ static int launch16(int cfg, const half_t* A, int lda, const half_t* Bt, int ldb
   return check16("gemm_f16");
 }
 
+template <int MODE>
+static int launch16_any(int cfg, const half_t* A, int lda, const half_t* Bt, int ldb, half_t* C, float* slab, int ldc,
+                        int M, int N, int Kpad, const EpiParams& epi, int tilesN, const ImplicitConv& ic,
+                        const SplitK& sk, const BufDesc* bd, dim3 grid, hipStream_t st) {
+  if (bd)
+    return launch16<MODE, true>(cfg, A, lda, Bt, ldb, C, slab, ldc, M, N, Kpad, epi, tilesN, ic, sk, *bd, grid, st);
+  return launch16<MODE, false>(cfg, A, lda, Bt, ldb, C, slab, ldc, M, N, Kpad, epi, tilesN, ic, sk, BufDesc{}, grid,
+                               st);
+}
+
 int launch_gemm16(int cfg, int mode, const half_t* A, int lda, const ImplicitConv& ic, const half_t* Bt, int ldb,
                   half_t* C, int ldc, long long M, int N, int Kpad, const EpiParams& epi, hipStream_t stream,
-                  int splits, float* slab) {
+                  int splits, float* slab, unsigned* tickets) {
   if (M == 0 || N == 0) return 0;
   if (cfg < 0 || cfg >= GEMM16_NUM_CFGS || mode < GEMM_DENSE || mode > GEMM_IMPLICIT_POOL) {
     set_error("gemm16: bad cfg %d / mode %d", cfg, mode);
@@ -87,23 +104,53 @@ int launch_gemm16(int cfg, int mode, const half_t* A, int lda, const ImplicitCon
   int grid = tilesM * tilesN;
   SplitK sk{0, grid, 0};
   if (splits > 1) {
-    if (!slab || (Kpad / 64) % splits != 0 || N % 4 != 0) {
+    if (!slab || (Kpad / 64) % splits != 0 || (!tickets && N % 4 != 0) || (tickets && splits > 3)) {
       set_error("gemm16: split-K %d unsupported (Kpad %d, N %d)", splits, Kpad, N);
       return -2;
     }
     sk = SplitK{Kpad / 64 / splits, grid, M * (long long)N};
+    if (tickets) {
+      if (splitk16_fused_slab_floats(cfg, M, N, splits) * 4 >= 0x80000000LL) {
+        set_error("gemm16: fused split-K slab over 2 GiB (M=%lld N=%d)", M, N);
+        return -2;
+      }
+      sk.tickets = tickets;
+      sk.out = reinterpret_cast<float*>(C);
+      sk.ldo = ldc;
+      sk.flags = epi.flags;
+      sk.splits = splits;
+    }
     grid *= splits;
   }
+  // buffer-descriptor DMA (BufDesc): dense always when the descriptors fit; implicit for
+  // C % 64 == 0 or C == 32
+  long long a_bytes;
+  const half_t* abase = A;
+  if (mode == GEMM_DENSE) {
+    a_bytes = M * (long long)lda * 2;
+  } else {
+    const long long per_img = mode == GEMM_IMPLICIT_POOL ? 4LL * ic.PH * ic.PW : (long long)ic.OH * ic.OW;
+    const long long nimg = per_img > 0 ? M / per_img : 0;
+    a_bytes = (nimg * ic.H * ic.W + ic.W + 1) * (long long)ic.C * 2;
+    abase = A - (size_t)(ic.W + 1) * ic.C;
+  }
+  const long long b_bytes = (long long)tilesN * ci.bn * ldb * 2;
+  BufDesc bd{reinterpret_cast<const float*>(abase), (unsigned)a_bytes, (unsigned)b_bytes};
+  const bool shape_ok = mode == GEMM_DENSE || ic.C % 64 == 0 || ic.C == 32;
+  const BufDesc* pbd = (!getenv_flag_off("DNN_HIP_GEMM_BUF") && shape_ok && a_bytes > 0 && a_bytes < 0x80000000LL &&
+                        b_bytes > 0 && b_bytes < 0x80000000LL)
+                           ? &bd
+                           : nullptr;
   switch (mode) {
     case GEMM_DENSE:
-      return launch16<GEMM_DENSE>(cfg, A, lda, Bt, ldb, C, slab, ldc, (int)M, N, Kpad, epi, tilesN, ic, sk,
-                                  dim3(grid), stream);
+      return launch16_any<GEMM_DENSE>(cfg, A, lda, Bt, ldb, C, slab, ldc, (int)M, N, Kpad, epi, tilesN, ic, sk, pbd,
+                                      dim3(grid), stream);
     case GEMM_IMPLICIT:
-      return launch16<GEMM_IMPLICIT>(cfg, A, lda, Bt, ldb, C, slab, ldc, (int)M, N, Kpad, epi, tilesN, ic, sk,
-                                     dim3(grid), stream);
+      return launch16_any<GEMM_IMPLICIT>(cfg, A, lda, Bt, ldb, C, slab, ldc, (int)M, N, Kpad, epi, tilesN, ic, sk,
+                                         pbd, dim3(grid), stream);
     default:
-      return launch16<GEMM_IMPLICIT_POOL>(cfg, A, lda, Bt, ldb, C, slab, ldc, (int)M, N, Kpad, epi, tilesN, ic,
-                                          sk, dim3(grid), stream);
+      return launch16_any<GEMM_IMPLICIT_POOL>(cfg, A, lda, Bt, ldb, C, slab, ldc, (int)M, N, Kpad, epi, tilesN, ic,
+                                              sk, pbd, dim3(grid), stream);
   }
 }
 

@@ -157,7 +157,7 @@ static void drop_graph(dnn_plan* p) {
   p->g_n = -1;
 }
 
-static bool fused_splitk(const dnn_plan* p) { return p->splitk_fused && !p->fp16; }
+static bool fused_splitk(const dnn_plan* p) { return p->splitk_fused; }
 
 static void layout(dnn_plan* p) {
   size_t off = 0, act = (size_t)p->in_h * p->in_w * p->in_c, col = 0, slab = 0, slab_fused = 0, tickets = 0;
@@ -195,8 +195,10 @@ static void layout(dnn_plan* p) {
         ++nconv;
       }
       if (L.splits > 1 && fused_splitk(p)) {  // partials combined by the GEMM's last-arriving split
-        slab_fused = std::max(slab_fused, (size_t)splitk_fused_slab_floats(L.cfg, (long long)M, L.OC, L.splits));
-        tickets = std::max(tickets, (size_t)splitk_tiles(L.cfg, (long long)M, L.OC));
+        slab_fused = std::max(slab_fused, (size_t)(p->fp16 ? splitk16_fused_slab_floats(L.cfg, (long long)M, L.OC, L.splits)
+                                                           : splitk_fused_slab_floats(L.cfg, (long long)M, L.OC, L.splits)));
+        tickets = std::max(tickets, (size_t)(p->fp16 ? splitk16_tiles(L.cfg, (long long)M, L.OC)
+                                                     : splitk_tiles(L.cfg, (long long)M, L.OC)));
       } else if (L.splits > 1) {  // partials written by the GEMM, summed + epilogue by the reduce kernel
         slab = std::max(slab, (size_t)L.splits * L.OH * L.OW * L.OC);
         snprintf(nm, sizeof(nm), "conv%d.reduce", nconv - 1);
@@ -539,6 +541,7 @@ static int record(dnn_plan* p, int kernel, hipStream_t s) {
 static int run_fp16(dnn_plan* p, int n, const float* d_in, float* d_out, hipStream_t s) {
   half_t* act[2] = {reinterpret_cast<half_t*>(p->ws), reinterpret_cast<half_t*>(p->ws + p->act_floats)};
   float* slab = p->ws + 2 * p->act_floats + p->col_floats;
+  unsigned* tickets = fused_splitk(p) ? reinterpret_cast<unsigned*>(slab + p->slab_floats) : nullptr;
   const float* zero = p->ws + p->ws_floats - dnn_plan::kZeroFloats;
   const int nl = (int)p->layers.size();
   const half_t* cur = nullptr;
@@ -573,14 +576,14 @@ static int run_fp16(dnn_plan* p, int n, const float* d_in, float* d_out, hipStre
         }
         case MODE_DIRECT_A:
           rc = launch_gemm16(L.cfg, GEMM_DENSE, cur, L.C, ImplicitConv{}, wt, L.Kpad, dst, L.OC, Mc, L.OC, L.Kpad,
-                             epi, s, L.splits, slab);
+                             epi, s, L.splits, slab, tickets);
           break;
         case MODE_IMPLICIT: {
           ImplicitConv ic{zero, L.H, L.W, L.C, L.OH, L.OW, L.PH, L.PW, L.kh, L.kw, L.sh, L.sw, L.pt, L.pl,
                           L.pool ? 1 : 0};
           const long long M = L.pool ? 4LL * n * L.PH * L.PW : Mc;
           rc = launch_gemm16(L.cfg, L.pool ? GEMM_IMPLICIT_POOL : GEMM_IMPLICIT, cur, 0, ic, wt, L.Kpad, dst, L.OC,
-                             M, L.OC, L.Kpad, epi, s, L.splits, slab);
+                             M, L.OC, L.Kpad, epi, s, L.splits, slab, tickets);
           break;
         }
         default:
@@ -588,7 +591,7 @@ static int run_fp16(dnn_plan* p, int n, const float* d_in, float* d_out, hipStre
           return -2;
       }
       if (rc) return rc;
-      if (L.splits > 1) {
+      if (L.splits > 1 && !tickets) {
         if ((rc = record(p, ++k, s))) return rc;
         if ((rc = launch_splitk_reduce16(slab, L.splits, Mc, L.OC, dst, L.OC, epi, s))) return rc;
       }

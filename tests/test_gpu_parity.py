@@ -604,6 +604,45 @@ def test_splitk_combine_in_gemm_equals_reduce_kernel(monkeypatch, case):
     assert np.array_equal(yd.cpu().numpy(), y_red)
 
 
+# ------------------------------------------------------------------ buffer-descriptor DMA
+BUF_CASES = [
+    # B, H, W, C, od, pool, precision: implicit GEMMs whose A/B DMAs go through buffer
+    # descriptors (padding taps = out-of-range offsets, zero-filled by the hardware)
+    (3, 20, 18, 32, 64, (2, 2, "SAME"), "fp32"),    # conv2-like, 256x64 / small-M tiles, edges
+    (2, 13, 13, 128, 256, (2, 2, "SAME"), "fp32"),  # odd 13x13 -> 7x7 pool padding
+    (64, 13, 13, 512, 1024, None, "fp32"),           # conv6: split-K 3 + combine
+    (3, 20, 18, 32, 64, (2, 2, "SAME"), "fp16"),    # fp16 C = 32: two taps per K-step
+    (2, 16, 16, 64, 128, None, "fp16"),              # fp16 C = 64: one tap per K-step
+    (64, 13, 13, 256, 512, (2, 1, "SAME"), "fp16"),  # fp16 conv5: split-K 3 + combine, s1 pool
+]
+
+
+@pytest.mark.parametrize("case", BUF_CASES)
+def test_buffer_dma_equals_flat_dma(monkeypatch, case):
+    """Buffer-descriptor LDS-DMA (32-bit voffsets, OOB padding taps) gives the same bits as the
+    flat-address DMA with the zero page (DNN_HIP_GEMM_BUF=0), fp32 and fp16, with and without
+    the in-GEMM split-K combine."""
+    B, H, W, C, od, pool, prec = case
+    rng = np.random.default_rng(B * 3 + C + od)
+    x = rng.standard_normal((B, H, W, C)).astype(np.float32)
+    k = (rng.standard_normal((3, 3, C, od)) * np.sqrt(2.0 / (9 * C))).astype(np.float32)
+    bias = rng.standard_normal(od).astype(np.float32) * 0.1
+    bn = (rng.standard_normal(od).astype(np.float32) * 0.1, rng.uniform(0.5, 1.5, od).astype(np.float32),
+          rng.uniform(0.5, 1.5, od).astype(np.float32))
+    kw = dict(bias=bias, bn=bn, leaky=True, pool=pool)
+    monkeypatch.setenv("DNN_HIP_GEMM_BUF", "0")
+    y_flat = dnn_hip.DnnInferenceEngine(_chain(x.shape, k, **kw), False, precision=prec).run(x)
+    monkeypatch.delenv("DNN_HIP_GEMM_BUF")
+    y_buf = dnn_hip.DnnInferenceEngine(_chain(x.shape, k, **kw), False, precision=prec).run(x)
+    assert np.array_equal(y_buf, y_flat)
+    if prec == "fp16":  # fused combine == the fp16 reduce kernel
+        monkeypatch.setenv("DNN_HIP_SPLITK_FUSED", "0")
+        y_red = dnn_hip.DnnInferenceEngine(_chain(x.shape, k, **kw), False, precision=prec).run(x)
+        assert np.array_equal(y_buf, y_red)
+    ref = _oracle_chain(x, k, **kw)
+    assert R.normwise_err(y_buf, ref) < (LAYER_TOL if prec == "fp32" else 5e-3)
+
+
 # ------------------------------------------------------------------ fp16 path (BASELINE config 5)
 FP16_LAYER_TOL = 5e-3   # normwise vs the fp32 oracle: fp16 inputs/weights/outputs (2^-11 each), fp32 accumulate
 FP16_NET_TOL = 2e-2     # whole net vs the fp32 reference goldens (SURVEY.md §8d suggested bound)

@@ -23,8 +23,8 @@ from collections import defaultdict
 ORDER = ["conv0.direct", "conv1.patch", "conv2.gemm", "conv3.gemm", "conv4.gemm", "conv5.gemm", "pool5",
          "conv6.gemm", "conv7.gemm", "conv8.gemm"]
 # ... the fp16 plan (dnn_plan_set_precision 1): conv1 patch kernel, f16->f32 output conversion
-ORDER_FP16 = ["conv0.direct", "conv1.patch", "conv2.gemm", "conv3.gemm", "conv4.gemm", "conv5.gemm", "conv5.reduce",
-              "pool5", "conv6.gemm", "conv6.reduce", "conv7.gemm", "conv7.reduce", "conv8.gemm", "output.cvt"]
+ORDER_FP16 = ["conv0.direct", "conv1.patch", "conv2.gemm", "conv3.gemm", "conv4.gemm", "conv5.gemm", "pool5",
+              "conv6.gemm", "conv7.gemm", "conv8.gemm", "output.cvt"]
 # ... and with DNN_HIP_FUSE=0 (explicit im2col + GEMM, separate pools)
 ORDER_UNFUSED = []
 for _i in range(9):
@@ -133,7 +133,7 @@ def main():
     if a.reduce:
         ORDER[:] = with_reduces(ORDER)
     if a.fp16:
-        ORDER[:] = ORDER_FP16
+        ORDER[:] = with_reduces(ORDER_FP16) if a.reduce else ORDER_FP16
     s = summarise(a.trace, a.fetch, a.write, a.skip)
     doc = {"note": a.note or __doc__.strip().splitlines()[0], "kernels": s}
     text = json.dumps(doc, indent=1)
