@@ -87,7 +87,8 @@ enum GemmCfg : int {
   GEMM_G32x64_NS4 = 8,   // N <= 64 implicit conv, small M: LDS-DMA 4-stage ring, 32x64 tile, 2 waves
   GEMM_128x256_W8 = 9,   // split-K layers, N % 256 == 0: 128x256, 8 waves of 64x64, one workgroup per CU
   GEMM_128x512_W16 = 10, // split-K layers, N % 512 == 0 (conv5-7): 128x512, 16 waves of 64x64, 160 KB LDS
-  GEMM_NUM_CFGS = 11,
+  GEMM_64x128_NS3 = 11,  // experiment: 64x128 with a 3-stage ring
+  GEMM_NUM_CFGS = 12,
 };
 int gemm_cfg_bm(int cfg);
 int gemm_cfg_bn(int cfg);
@@ -171,7 +172,11 @@ enum Gemm16Cfg : int {
   GEMM16_32x64_NS4 = 4,   // N <= 64, small M
   GEMM16_128x32 = 5,      // N <= 32
   GEMM16_32x32_NS4 = 6,   // N <= 32, small M
-  GEMM16_NUM_CFGS = 7,
+  GEMM16_256x128_W8 = 7,  // experiment: 8 waves of 64x64 (1 workgroup per CU)
+  GEMM16_128x128_W4 = 8,  // experiment: 4 waves of 64x64
+  GEMM16_128x256_W8 = 9,  // experiment: 8 waves of 64x64 (1 workgroup per CU)
+  GEMM16_128x512_W16 = 10, // 16 waves of 64x64, 160 KB LDS: 40 staged B per 1k flop (L2->LDS bound)
+  GEMM16_NUM_CFGS = 11,
 };
 int choose_gemm16_cfg(long long M, int N, int K);
 int choose_splitk16(int N, int K);

@@ -48,7 +48,9 @@ gemm_f16_glds_kernel(const half_t* __restrict__ A, int lda, const half_t* __rest
   static_assert(WTM % 32 == 0 && WTN % 32 == 0, "wave tile must be a multiple of 32");
 
   __shared__ __attribute__((aligned(1024))) float smem[NS * STAGE];
-  __shared__ int toff[32];  // implicit: tap -> element offset of (dy, dx) from the window origin
+  // implicit, flat-address DMA: tap -> element offset of (dy, dx) from the window origin
+  // (the ABUF path keeps a uniform (dy, dx) cursor instead: no LDS beyond the ring)
+  __shared__ int toff[ABUF ? 1 : 32];
 
   int tile = xcd_tile(blockIdx.x, gridDim.x);
   int kbeg = 0, split_idx = 0;
@@ -66,7 +68,7 @@ gemm_f16_glds_kernel(const half_t* __restrict__ A, int lda, const half_t* __rest
   const int wid = wave_uniform(threadIdx.x >> 6);
   const int ntaps = ic.kh * ic.kw;
 
-  if constexpr (MODE != 0) {
+  if constexpr (MODE != 0 && !ABUF) {
     if (threadIdx.x < 32) {
       const int t = threadIdx.x, dy = t / ic.kw, dx = t - (t / ic.kw) * ic.kw;
       toff[t] = (dy * ic.W + dx) * ic.C;
@@ -141,9 +143,12 @@ gemm_f16_glds_kernel(const half_t* __restrict__ A, int lda, const half_t* __rest
 
   // implicit: uniform cursor (tap, channel) of the next K-step's first element
   int tapb = 0, cb = 0;
+  int dyb = 0, dxb = 0;  // ABUF: (dy, dx) of tap tapb
   if constexpr (MODE != 0) {
     tapb = kbeg / ic.C;
     cb = kbeg - tapb * ic.C;
+    dyb = tapb / ic.kw;
+    dxb = tapb - dyb * ic.kw;
   }
   const float* zero = ic.zero;
 
@@ -153,8 +158,9 @@ gemm_f16_glds_kernel(const half_t* __restrict__ A, int lda, const half_t* __rest
       const unsigned koff = (unsigned)((kbeg + k0) * 2);
       unsigned soffA = koff, dsec = 0;
       if constexpr (MODE != 0) {
-        soffA = (unsigned)((toff[tapb] + cb) * 2);
-        dsec = (unsigned)((toff[tapb + 1] - toff[tapb]) * 2);
+        soffA = (unsigned)((((long long)dyb * ic.W + dxb) * ic.C + cb) * 2);
+        // next tap: (dy, dx+1), or (dy+1, 0) past the row
+        dsec = (unsigned)((dxb + 1 == ic.kw ? (ic.W - (ic.kw - 1)) : 1) * ic.C * 2);
       }
 #pragma unroll
       for (int i = 0; i < LPSA; ++i) {
@@ -169,6 +175,10 @@ gemm_f16_glds_kernel(const half_t* __restrict__ A, int lda, const half_t* __rest
         while (cb >= ic.C) {
           cb -= ic.C;
           ++tapb;
+          if (++dxb == ic.kw) {
+            dxb = 0;
+            ++dyb;
+          }
         }
       }
       return;

@@ -150,7 +150,7 @@ struct CfgInfo {
 };
 static const CfgInfo kCfgs[GEMM_NUM_CFGS] = {{256, 16, 32}, {256, 32, 16}, {128, 64, 32}, {128, 128, 32},
                                              {64, 128, 32},  {64, 32, 32},  {256, 64, 32}, {32, 128, 32},
-                                             {32, 64, 32},   {128, 256, 32}, {128, 512, 32}};
+                                             {32, 64, 32},   {128, 256, 32}, {128, 512, 32}, {64, 128, 32}};
 
 int gemm_cfg_bm(int cfg) { return kCfgs[cfg].bm; }
 int gemm_cfg_bn(int cfg) { return kCfgs[cfg].bn; }
@@ -236,6 +236,7 @@ static int launch_glds_t(int cfg, const float* A, int lda, const float* Bt, int 
     case GEMM_G32x64_NS4: DNN_GLDS(32, 64, 1, 2, 32, 4); break;
     case GEMM_128x256_W8: DNN_GLDS(128, 256, 2, 4, 32, 2); break;
     case GEMM_128x512_W16: DNN_GLDS(128, 512, 2, 8, 32, 2); break;
+    case GEMM_64x128_NS3: DNN_GLDS(64, 128, 2, 2, 32, 3); break;
     default:
       set_error("gemm: cfg %d is not an LDS-DMA config", cfg);
       return -2;

@@ -21,7 +21,7 @@ struct Cfg16Info {
   int bm, bn;
 };
 static const Cfg16Info kCfg16[GEMM16_NUM_CFGS] = {{128, 128}, {64, 128}, {32, 128}, {128, 64}, {32, 64},
-                                                  {128, 32},  {32, 32}};
+                                                  {128, 32},  {32, 32},  {256, 128}, {128, 128}, {128, 256}, {128, 512}};
 int gemm16_cfg_bn(int cfg) { return kCfg16[cfg].bn; }
 
 // Same rules as the fp32 chooser (kernels.hip): every config is the 32x32x16 f16 family with
@@ -36,6 +36,11 @@ int choose_gemm16_cfg(long long M, int N, int K) {
   if (N <= 64) return ((M + 127) / 128) < 256 ? GEMM16_32x64_NS4 : GEMM16_128x64;
   const int s = choose_splitk16(N, K);
   const long long t128 = ((M + 127) / 128) * ((N + 127) / 128);
+  // split-K long-K layers with N % 512 == 0 (conv6/conv7): one 16-wave 128x512 workgroup per CU
+  // stages 40 B per 1k flop instead of 64 (two 128x128 workgroups): the fp16 GEMM is bound by
+  // the L2->LDS stream, conv7 0.252 -> 0.226 ms (batch 64).  Needs buffer-descriptor DMA; the
+  // launcher falls back to 128x128 (same MFMA family and K order: same bits) when it is off.
+  if (K >= 4096 && s > 1 && N % 512 == 0 && t128 * s >= 512) return GEMM16_128x512_W16;
   if (K >= 2048 && t128 * s >= 512) return GEMM16_128x128;
   const long long t64 = ((M + 63) / 64) * ((N + 127) / 128);
   if (t64 * s < 256) return GEMM16_32x128_NS4;
@@ -67,6 +72,17 @@ static int launch16(int cfg, const half_t* A, int lda, const half_t* Bt, int ldb
     case GEMM16_32x64_NS4: DNN_L16(32, 64, 1, 2, 4); break;
     case GEMM16_128x32: DNN_L16(128, 32, 4, 1, 2); break;
     case GEMM16_32x32_NS4: DNN_L16(32, 32, 1, 1, 4); break;
+    case GEMM16_256x128_W8: DNN_L16(256, 128, 4, 2, 2); break;
+    case GEMM16_128x128_W4: DNN_L16(128, 128, 2, 2, 2); break;
+    case GEMM16_128x256_W8: DNN_L16(128, 256, 2, 4, 2); break;
+    case GEMM16_128x512_W16:  // the ring takes all 160 KB of LDS: buffer-descriptor DMA only (no tap table)
+      if constexpr (ABUF) {
+        DNN_L16(128, 512, 2, 8, 2);
+        break;
+      } else {
+        set_error("gemm16: cfg 128x512 needs buffer-descriptor DMA (shape too large or C unsupported)");
+        return -2;
+      }
     default:
       set_error("gemm16: bad cfg %d", cfg);
       return -2;
@@ -93,6 +109,23 @@ int launch_gemm16(int cfg, int mode, const half_t* A, int lda, const ImplicitCon
     set_error("gemm16: bad cfg %d / mode %d", cfg, mode);
     return -2;
   }
+  // buffer-descriptor DMA (BufDesc): dense always when the descriptors fit; implicit for
+  // C % 64 == 0 or C == 32.  (b_bytes is bounded with the widest tile's N padding.)
+  long long a_bytes;
+  const half_t* abase = A;
+  if (mode == GEMM_DENSE) {
+    a_bytes = M * (long long)lda * 2;
+  } else {
+    const long long per_img = mode == GEMM_IMPLICIT_POOL ? 4LL * ic.PH * ic.PW : (long long)ic.OH * ic.OW;
+    const long long nimg = per_img > 0 ? M / per_img : 0;
+    a_bytes = (nimg * ic.H * ic.W + ic.W + 1) * (long long)ic.C * 2;
+    abase = A - (size_t)(ic.W + 1) * ic.C;
+  }
+  const long long b_bytes = (long long)((N + 511) / 512) * 512 * ldb * 2;
+  const bool shape_ok = mode == GEMM_DENSE || ic.C % 64 == 0 || ic.C == 32;
+  const bool abuf = !getenv_flag_off("DNN_HIP_GEMM_BUF") && shape_ok && a_bytes > 0 && a_bytes < 0x80000000LL &&
+                    b_bytes > 0 && b_bytes < 0x80000000LL;
+  if (cfg == GEMM16_128x512_W16 && !abuf) cfg = GEMM16_128x128;  // same MFMA family and K order
   const Cfg16Info ci = kCfg16[cfg];
   if (Kpad % 64 != 0 || ldb % 8 != 0 || M > 0x7fffffffLL || (mode == GEMM_DENSE && lda % 8 != 0) ||
       (mode != GEMM_DENSE && (ic.C % 8 != 0 || ic.kh * ic.kw > 30 || !ic.zero)) ||
@@ -122,25 +155,8 @@ int launch_gemm16(int cfg, int mode, const half_t* A, int lda, const ImplicitCon
     }
     grid *= splits;
   }
-  // buffer-descriptor DMA (BufDesc): dense always when the descriptors fit; implicit for
-  // C % 64 == 0 or C == 32
-  long long a_bytes;
-  const half_t* abase = A;
-  if (mode == GEMM_DENSE) {
-    a_bytes = M * (long long)lda * 2;
-  } else {
-    const long long per_img = mode == GEMM_IMPLICIT_POOL ? 4LL * ic.PH * ic.PW : (long long)ic.OH * ic.OW;
-    const long long nimg = per_img > 0 ? M / per_img : 0;
-    a_bytes = (nimg * ic.H * ic.W + ic.W + 1) * (long long)ic.C * 2;
-    abase = A - (size_t)(ic.W + 1) * ic.C;
-  }
-  const long long b_bytes = (long long)tilesN * ci.bn * ldb * 2;
   BufDesc bd{reinterpret_cast<const float*>(abase), (unsigned)a_bytes, (unsigned)b_bytes};
-  const bool shape_ok = mode == GEMM_DENSE || ic.C % 64 == 0 || ic.C == 32;
-  const BufDesc* pbd = (!getenv_flag_off("DNN_HIP_GEMM_BUF") && shape_ok && a_bytes > 0 && a_bytes < 0x80000000LL &&
-                        b_bytes > 0 && b_bytes < 0x80000000LL)
-                           ? &bd
-                           : nullptr;
+  const BufDesc* pbd = abuf ? &bd : nullptr;
   switch (mode) {
     case GEMM_DENSE:
       return launch16_any<GEMM_DENSE>(cfg, A, lda, Bt, ldb, C, slab, ldc, (int)M, N, Kpad, epi, tilesN, ic, sk, pbd,

@@ -199,6 +199,8 @@ static void layout(dnn_plan* p) {
                                                            : splitk_fused_slab_floats(L.cfg, (long long)M, L.OC, L.splits)));
         tickets = std::max(tickets, (size_t)(p->fp16 ? splitk16_tiles(L.cfg, (long long)M, L.OC)
                                                      : splitk_tiles(L.cfg, (long long)M, L.OC)));
+        if (p->fp16 && L.cfg == GEMM16_128x512_W16)  // the launcher's 128x128 fallback has more tiles
+          tickets = std::max(tickets, (size_t)splitk16_tiles(GEMM16_128x128, (long long)M, L.OC));
       } else if (L.splits > 1) {  // partials written by the GEMM, summed + epilogue by the reduce kernel
         slab = std::max(slab, (size_t)L.splits * L.OH * L.OW * L.OC);
         snprintf(nm, sizeof(nm), "conv%d.reduce", nconv - 1);
