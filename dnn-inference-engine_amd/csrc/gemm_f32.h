@@ -29,10 +29,26 @@ typedef _Float16 half_t;
 __device__ __forceinline__ void store_out(float* p, float v) { *p = v; }
 __device__ __forceinline__ void store_out(half_t* p, float v) { *p = (half_t)v; }
 
+// x / d correctly rounded (the reference's division), as Markstein's correction of x * RN(1/d):
+// with y = RN(1/d) and q = RN(x*y) within 1 ulp of x/d, the residual r = x - q*d is exact (one
+// fma) and RN(q + r*y) is the correctly rounded quotient (no midpoint quotients exist in binary
+// floating point).  3 VALU per element instead of the ~11 of the IEEE division sequence; the
+// reciprocal is per output channel, so the compiler hoists it out of the element loops.  Zero,
+// denormal, infinite and NaN q (where the residual step is not exact or loses the sign of a
+// zero) take the IEEE division.  Checked bit for bit against x / d on 3e8 random pairs
+// (tools/markstein_check.c) and by every bit-exact epilogue test.
+__device__ __forceinline__ float div_rn(float x, float d) {
+  const float y = 1.0f / d;
+  const float q = x * y;
+  if (__builtin_amdgcn_classf(q, 0x2F7)) return x / d;  // NaN, +-inf, +-0, +-denormal
+  const float r = __builtin_fmaf(-q, d, x);
+  return __builtin_fmaf(r, y, q);
+}
+
 __device__ __forceinline__ float apply_epilogue(float v, float bias, float mean, float sq, float gamma,
                                                 int flags) {
   if (flags & EPI_BIAS) v = v + bias;
-  if (flags & EPI_BN) v = ((v - mean) / sq) * gamma;
+  if (flags & EPI_BN) v = div_rn(v - mean, sq) * gamma;
   if (flags & EPI_BN_AB) v = v * mean - sq;
   if (flags & EPI_LEAKY_F64) v = v < 0.f ? (float)(0.1 * (double)v) : v;
   if (flags & EPI_LEAKY_F32) {
