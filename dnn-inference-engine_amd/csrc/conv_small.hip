@@ -195,6 +195,7 @@ conv0_mfma_pool_kernel(const float* __restrict__ in, const float* __restrict__ w
 // pixel, the M-tile offset being an immediate.  (RS = 56: every ds_read_b32 is exactly
 // 2-way; no row stride makes the two pixel rows of an M-tile conflict-free.)
 constexpr int C0_RS = 56;  // patch row stride (floats) >= 18 * CIN
+constexpr int C0_ROWS_PER_WAVE = 5;  // 20 row DMAs per tile over 4 waves (rows 18, 19 dummies)
 
 template <int CIN>
 __global__ void __launch_bounds__(256)
@@ -203,7 +204,7 @@ conv0_packed_pool_kernel(const float* __restrict__ in, const float* __restrict__
                          EpiParams epi) {
   constexpr int K = 9 * CIN, KS = (K + 3) / 4, RW = SC_P * CIN, RS = C0_RS;
   static_assert(RW <= RS && RW <= 64, "patch row");
-  __shared__ __attribute__((aligned(16))) float patch[2][SC_P * RS];
+  __shared__ __attribute__((aligned(16))) float patch[3][(4 * C0_ROWS_PER_WAVE) * RS];  // triple buffer
   __shared__ __attribute__((aligned(16))) float stage[4][2][8][16];  // per wave: 2 window rows x 8 windows x 16 ch
 
   const int lane = threadIdx.x & 63;
@@ -238,40 +239,50 @@ conv0_packed_pool_kernel(const float* __restrict__ in, const float* __restrict__
     return Tile{b, tt - b * tilesY, t - tt * tilesX};
   };
   // lane l of a patch row DMA copies float l of the row's 18 * CIN (the row is contiguous in
-  // the NHWC frame); lanes past the frame's edges read the zero page
-  auto issue = [&](const Tile& c, int buf) {
+  // the NHWC frame); lanes past the frame's edges read the zero page.  Every wave issues
+  // exactly C0_ROWS_PER_WAVE DMAs per tile (rows 18, 19 and the tiles past the end are dummies
+  // from the zero page), so the counted waits below are exact.
+  auto issue = [&](const Tile& c, bool valid, int buf) {
     const int x0 = c.tx * SC_T - g.pl, y0 = c.ty * SC_T - g.pt;
     const int px = x0 + lane / CIN;
-    const bool xok = (unsigned)px < (unsigned)g.W;
+    const bool xok = valid && (unsigned)px < (unsigned)g.W;
     const float* rowp = in + (((size_t)c.b * g.H + y0) * g.W + x0) * CIN + lane;
     const size_t rstride = (size_t)g.W * CIN;
 #pragma unroll
-    for (int u = 0; u < (SC_P + 3) / 4; ++u) {
+    for (int u = 0; u < C0_ROWS_PER_WAVE; ++u) {
       const int r = wid + 4 * u;
-      if (r < SC_P && lane < RW) {
-        const bool ok = xok && (unsigned)(y0 + r) < (unsigned)g.H;
+      if (lane < RW) {
+        const bool ok = xok && r < SC_P && (unsigned)(y0 + r) < (unsigned)g.H;
         lds_dma4_opaque(ok ? rowp + r * rstride : zero, &patch[buf][r * RS]);
       }
     }
   };
 
+  // Two tiles in flight: tile t's rows were issued two iterations ago.  Per wave and tile the
+  // VMEM stream is C0_ROWS_PER_WAVE DMAs then one store, so when tile t is consumed the ops
+  // issued after its DMAs are at most: store(t-2), DMAs(t+1), store(t-1).
   const auto orsrc = out_rsrc(out, (unsigned)((size_t)g.B * g.PH * g.PW * 16 * sizeof(float)));
-  int t = blockIdx.x, buf = 0;
+  const int G = gridDim.x;
+  int t = blockIdx.x;
   Tile cur = coords(t < ntiles ? t : 0);
-  if (t < ntiles) issue(cur, 0);
-  for (; t < ntiles; t += gridDim.x) {
-    // this wave's rows of `buf` landed: everything but the previous tile's one store (issued
-    // after those DMAs; always issued, see store16) has completed
-    if (buf == 0 && t == (int)blockIdx.x)
-      wait_vmcnt<0>();
+  Tile nxt = coords(t + G < ntiles ? t + G : 0);
+  if (t < ntiles) {
+    issue(cur, true, 0);
+    issue(nxt, t + G < ntiles, 1);
+  }
+  int buf = 0;
+  for (int it = 0; t < ntiles; t += G, ++it) {
+    if (it == 0)
+      wait_vmcnt<C0_ROWS_PER_WAVE>();
+    else if (it == 1)
+      wait_vmcnt<C0_ROWS_PER_WAVE + 1>();
     else
-      wait_vmcnt<1>();
-    raw_barrier();    // all rows landed; every wave finished reading buf ^ 1
-    Tile nxt = cur;
-    if (t + (int)gridDim.x < ntiles) {
-      nxt = coords(t + gridDim.x);
-      issue(nxt, buf ^ 1);
-    }
+      wait_vmcnt<C0_ROWS_PER_WAVE + 2>();
+    raw_barrier();  // every wave's rows of `buf` landed; every wave finished reading tile t-1's buffer
+    // tile t+2 into the buffer tile t-1 used (dummy past the end: the count stays fixed)
+    const int t2 = t + 2 * G;
+    const Tile nn = coords(t2 < ntiles ? t2 : 0);
+    issue(nn, t2 < ntiles, buf == 0 ? 2 : buf - 1);
     const float* P = patch[buf];
 
     f32x4 acc[4];
@@ -287,6 +298,7 @@ conv0_packed_pool_kernel(const float* __restrict__ in, const float* __restrict__
 
     const int b = cur.b, y0 = cur.ty * SC_T, x0 = cur.tx * SC_T;
     cur = nxt;
+    nxt = nn;
     // pool + epilogue into the wave's LDS stage, then 16-B coalesced stores
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -306,8 +318,9 @@ conv0_packed_pool_kernel(const float* __restrict__ in, const float* __restrict__
       store16(orsrc, off, *reinterpret_cast<const f32x4*>(&stage[wid][lr][0][0] + f));
     }
     wait_lgkm0();
-    buf ^= 1;
+    buf = buf == 2 ? 0 : buf + 1;
   }
+  wait_vmcnt<0>();  // no LDS-DMA may land after the workgroup exits
 }
 
 bool conv0_mfma_supported(int cin, int nout, int kh, int kw, int sh, int sw) {

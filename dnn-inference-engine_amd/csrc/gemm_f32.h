@@ -293,9 +293,11 @@ __device__ __forceinline__ void store4(__amdgpu_buffer_rsrc_t r, unsigned off, f
 // cannot tell a double buffer's halves apart).  The caller orders it with its own counted
 // vmcnt + barrier.  `dst` must be wave-uniform; lane l writes dst + 4*l.
 __device__ __forceinline__ void lds_dma4_opaque(const float* src, const float* dst) {
-  const unsigned m0v = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) float*)dst;
+  const unsigned m0v =
+      __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(const __attribute__((address_space(3))) float*)dst);
   unsigned saved;  // M0 is a reserved register: restore it rather than clobber it
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+  // (s_nop 0: the wait state between the M0 write and the LDS-DMA that reads it)
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
                : "=&s"(saved)
                : "v"(src), "s"(m0v)
                : "memory");
