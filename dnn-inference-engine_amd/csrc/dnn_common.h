@@ -88,7 +88,9 @@ enum GemmCfg : int {
   GEMM_128x256_W8 = 9,   // split-K layers, N % 256 == 0: 128x256, 8 waves of 64x64, one workgroup per CU
   GEMM_128x512_W16 = 10, // split-K layers, N % 512 == 0 (conv5-7): 128x512, 16 waves of 64x64, 160 KB LDS
   GEMM_64x128_NS3 = 11,  // experiment: 64x128 with a 3-stage ring
-  GEMM_NUM_CFGS = 12,
+  GEMM_G256x128_W8 = 12, // experiment (N % 128 == 0): 256x128, 8 waves of 64x64, 96 KB (1 per CU)
+  GEMM_G192x128_W8 = 13, // unsplit long-K N % 128 == 0 layers filling one round (conv4): 192x128, 8 waves of 96x32
+  GEMM_NUM_CFGS = 14,
 };
 int gemm_cfg_bm(int cfg);
 int gemm_cfg_bn(int cfg);
@@ -107,8 +109,13 @@ struct ImplicitConv {
   int PH, PW;         // pooled output (pool = 1)
   int kh, kw, sh, sw, pt, pl;
   int pool;
+  // round-up magic numbers of OW, OH, PW, PH for the kernels' division-free row decode
+  // (div_magic, gemm_f32.h); the launchers fill them (implicit_conv_magic)
+  unsigned mag_ow = 0, mag_oh = 0, mag_pw = 0, mag_ph = 0;
+  int sh_ow = 0, sh_oh = 0, sh_pw = 0, sh_ph = 0;
 };
 bool implicit_conv_supported(int C, int kh, int kw);
+void implicit_conv_magic(ImplicitConv* ic);
 enum GemmMode : int { GEMM_DENSE = 0, GEMM_IMPLICIT = 1, GEMM_IMPLICIT_POOL = 2 };
 
 // ---------------------------------------------------------------- launchers

@@ -97,34 +97,12 @@ gemm_f16_glds_kernel(const half_t* __restrict__ A, int lda, const half_t* __rest
         srcA[i] = A + (size_t)gm * lda + kbeg + 8 * ls;
       maskA[i] = 0;
     } else {
-      int b = 0, oy = 0, ox = 0;
-      bool rv = m < M;
-      if constexpr (MODE == 2) {
-        const int pos = m & 3, w = m >> 2;
-        const int px = w % ic.PW, t = w / ic.PW, py = t % ic.PH;
-        b = t / ic.PH;
-        oy = 2 * py + (pos >> 1);
-        ox = 2 * px + (pos & 1);
-        rv = rv && oy < ic.OH && ox < ic.OW;
-      } else {
-        ox = m % ic.OW;
-        const int t = m / ic.OW;
-        oy = t % ic.OH;
-        b = t / ic.OH;
-      }
-      const int iy0 = oy * ic.sh - ic.pt, ix0 = ox * ic.sw - ic.pl;
+      int b, iy0, ix0;
+      maskA[i] = implicit_row<MODE>(ic, m, M, b, iy0, ix0);
       if constexpr (ABUF)
         voA[i] = (unsigned)(((((long long)b * ic.H + iy0) * ic.W + ix0 + ic.W + 1) * ic.C + 8 * (two_taps ? (ls & 3) : ls)) * 2);
       else
         srcA[i] = A + (((long long)b * ic.H + iy0) * ic.W + ix0) * (long long)ic.C;
-      int mk = 0;
-      if (rv) {
-        for (int dy = 0; dy < ic.kh; ++dy)
-          for (int dx = 0; dx < ic.kw; ++dx)
-            if ((unsigned)(iy0 + dy) < (unsigned)ic.H && (unsigned)(ix0 + dx) < (unsigned)ic.W)
-              mk |= 1 << (dy * ic.kw + dx);
-      }
-      maskA[i] = mk;
     }
   }
   const half_t* srcB[LPSB];

@@ -102,6 +102,44 @@ __device__ __forceinline__ int xcd_tile(int bid, int nb) {
   return (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (bid >> 3);
 }
 
+// n / d for 0 <= n < 2^31 without a division (round-up magic numbers from the launcher,
+// implicit_conv_magic).  The 32-bit sum cannot wrap: umulhi(n, mag) <= n < 2^31.
+__device__ __forceinline__ int div_magic(int n, unsigned mag, int sh) {
+  return (int)((__umulhi((unsigned)n, mag) + (unsigned)n) >> sh);
+}
+
+// Row m of an implicit-GEMM A operand -> image b and the input pixel (iy0, ix0) under its
+// window's top-left tap; returns the bitmask of the taps inside the frame (0 for a row past M
+// or past a ragged pool edge).  MODE 1: m is the output pixel (b, oy, ox); MODE 2: m = 4 *
+// window + 2 * dy + dx over the pooled output's (b, py, px) windows.
+template <int MODE>
+__device__ __forceinline__ int implicit_row(const ImplicitConv& ic, int m, int M, int& b, int& iy0, int& ix0) {
+  int oy, ox;
+  bool rv = m < M;
+  if constexpr (MODE == 2) {
+    const int w = m >> 2, t = div_magic(w, ic.mag_pw, ic.sh_pw);
+    b = div_magic(t, ic.mag_ph, ic.sh_ph);
+    oy = 2 * (t - b * ic.PH) + ((m >> 1) & 1);
+    ox = 2 * (w - t * ic.PW) + (m & 1);
+    rv = rv && oy < ic.OH && ox < ic.OW;
+  } else {
+    const int t = div_magic(m, ic.mag_ow, ic.sh_ow);
+    b = div_magic(t, ic.mag_oh, ic.sh_oh);
+    oy = t - b * ic.OH;
+    ox = m - t * ic.OW;
+  }
+  iy0 = oy * ic.sh - ic.pt;
+  ix0 = ox * ic.sw - ic.pl;
+  if (!rv) return 0;
+  // in-frame taps = (window rows inside the frame) x (window columns inside the frame)
+  int ym = 0, xm = 0;
+  for (int d = 0; d < ic.kh; ++d) ym |= ((unsigned)(iy0 + d) < (unsigned)ic.H ? 1 : 0) << d;
+  for (int d = 0; d < ic.kw; ++d) xm |= ((unsigned)(ix0 + d) < (unsigned)ic.W ? 1 : 0) << d;
+  int mk = 0;
+  for (int d = 0; d < ic.kh; ++d) mk |= ((ym >> d) & 1) ? xm << (d * ic.kw) : 0;
+  return mk;
+}
+
 // Fused epilogue + store of one wave's accumulators (NHWC: row = pixel, col = channel).
 template <int MF, int TM, int TN, int WTM, int WTN, typename OutT = float>
 __device__ __forceinline__ void store_tile(const typename Mfma<MF>::acc_t (&acc)[TM][TN], OutT* __restrict__ C,
@@ -574,34 +612,12 @@ gemm_f32_glds_kernel(const float* __restrict__ A, int lda, const float* __restri
         srcA[i] = A + (size_t)gm * lda + kbeg + 4 * ls;
       maskA[i] = 0;
     } else {
-      int b = 0, oy = 0, ox = 0;
-      bool rv = m < M;
-      if constexpr (MODE == 2) {
-        const int pos = m & 3, w = m >> 2;
-        const int px = w % ic.PW, t = w / ic.PW, py = t % ic.PH;
-        b = t / ic.PH;
-        oy = 2 * py + (pos >> 1);
-        ox = 2 * px + (pos & 1);
-        rv = rv && oy < ic.OH && ox < ic.OW;
-      } else {
-        ox = m % ic.OW;
-        const int t = m / ic.OW;
-        oy = t % ic.OH;
-        b = t / ic.OH;
-      }
-      const int iy0 = oy * ic.sh - ic.pt, ix0 = ox * ic.sw - ic.pl;
+      int b, iy0, ix0;
+      maskA[i] = implicit_row<MODE>(ic, m, M, b, iy0, ix0);
       if constexpr (ABUF)
         voA[i] = (unsigned)(((((long long)b * ic.H + iy0) * ic.W + ix0 + ic.W + 1) * ic.C + 4 * ls) * 4);
       else
         srcA[i] = A + (((long long)b * ic.H + iy0) * ic.W + ix0) * (long long)ic.C;
-      int mk = 0;
-      if (rv) {
-        for (int dy = 0; dy < ic.kh; ++dy)
-          for (int dx = 0; dx < ic.kw; ++dx)
-            if ((unsigned)(iy0 + dy) < (unsigned)ic.H && (unsigned)(ix0 + dx) < (unsigned)ic.W)
-              mk |= 1 << (dy * ic.kw + dx);
-      }
-      maskA[i] = mk;
     }
   }
   const float* srcB[LPSB];

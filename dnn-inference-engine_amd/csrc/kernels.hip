@@ -150,7 +150,8 @@ struct CfgInfo {
 };
 static const CfgInfo kCfgs[GEMM_NUM_CFGS] = {{256, 16, 32}, {256, 32, 16}, {128, 64, 32}, {128, 128, 32},
                                              {64, 128, 32},  {64, 32, 32},  {256, 64, 32}, {32, 128, 32},
-                                             {32, 64, 32},   {128, 256, 32}, {128, 512, 32}, {64, 128, 32}};
+                                             {32, 64, 32},   {128, 256, 32}, {128, 512, 32}, {64, 128, 32},
+                                             {256, 128, 32}, {192, 128, 32}};
 
 int gemm_cfg_bm(int cfg) { return kCfgs[cfg].bm; }
 int gemm_cfg_bn(int cfg) { return kCfgs[cfg].bn; }
@@ -183,6 +184,11 @@ int choose_gemm_cfg(long long M, int N, int K) {
     // unsplit long-K layers (conv4: N = 256, K = 1152): with buffer-addressed DMA the 64x128
     // ring (3 per CU) beats 128x128 (2 per CU, 1.3 rounds at batch 64): 0.273 -> 0.224 ms
     if (s > 1) return GEMM_128x128_K32;
+    // ... and 192x128 (8 waves of 96x32, 2 per CU) beats both when its tiles fill one round of
+    // the 512 slots (conv4 at batch 64: 452 tiles instead of 1.76 rounds of 64x128, 26 instead
+    // of 46 staged KB per MFLOP): 0.224 -> 0.215 ms.  (conv3, K = 576, measured slower on it.)
+    const long long t192 = ((M + 191) / 192) * ((N + 127) / 128);
+    if (N % 128 == 0 && t192 <= 512 && t192 * 5 >= 512 * 4) return GEMM_G192x128_W8;
   }
   // small M (batch 1 and the like): 64x128 would leave most CUs idle and each workgroup
   // waiting on a 2-stage ring; 32-row tiles with a 4-stage ring (same family, same K order)
@@ -202,6 +208,26 @@ int choose_gemm_cfg_implicit(long long M, int N, int K) {
 
 bool implicit_conv_supported(int C, int kh, int kw) {
   return (C == 16 || C % 32 == 0) && kh * kw <= 30;
+}
+
+// n / d == (umulhi(n, mag) + n) >> sh for 0 <= n < 2^31: the round-up method of Granlund and
+// Montgomery with sh = ceil(log2 d), mag = floor(2^32 (2^sh - d) / d) + 1 (d = 1: mag 1, sh 0)
+static void magic_u32(int d, unsigned* mag, int* sh) {
+  if (d <= 0) {
+    *mag = 0;
+    *sh = 0;
+    return;
+  }
+  int l = 0;
+  while ((1LL << l) < d) ++l;
+  *mag = (unsigned)(((1ULL << 32) * ((1ULL << l) - (unsigned long long)d)) / (unsigned long long)d + 1);
+  *sh = l;
+}
+void implicit_conv_magic(ImplicitConv* ic) {
+  magic_u32(ic->OW, &ic->mag_ow, &ic->sh_ow);
+  magic_u32(ic->OH, &ic->mag_oh, &ic->sh_oh);
+  magic_u32(ic->PW, &ic->mag_pw, &ic->sh_pw);
+  magic_u32(ic->PH, &ic->mag_ph, &ic->sh_ph);
 }
 
 // Split-K for the long-K wide layers: 680 128x128 tiles of conv6/7 at batch 64 fill 512
@@ -237,6 +263,8 @@ static int launch_glds_t(int cfg, const float* A, int lda, const float* Bt, int 
     case GEMM_128x256_W8: DNN_GLDS(128, 256, 2, 4, 32, 2); break;
     case GEMM_128x512_W16: DNN_GLDS(128, 512, 2, 8, 32, 2); break;
     case GEMM_64x128_NS3: DNN_GLDS(64, 128, 2, 2, 32, 3); break;
+    case GEMM_G256x128_W8: DNN_GLDS(256, 128, 4, 2, 32, 2); break;
+    case GEMM_G192x128_W8: DNN_GLDS(192, 128, 2, 4, 32, 2); break;
     default:
       set_error("gemm: cfg %d is not an LDS-DMA config", cfg);
       return -2;
@@ -344,10 +372,12 @@ int launch_gemm(int cfg, const float* A, int lda, const float* Bt, int ldb, floa
   return check_launch("gemm");
 }
 
-int launch_gemm_implicit(int cfg, int mode, const float* in, const ImplicitConv& ic, const float* Bt, int ldb,
+int launch_gemm_implicit(int cfg, int mode, const float* in, const ImplicitConv& ic_in, const float* Bt, int ldb,
                          float* C, int ldc, long long M, int N, int Kpad, const EpiParams& epi, hipStream_t stream,
                          int splits, float* slab, unsigned* tickets) {
   if (M == 0 || N == 0) return 0;
+  ImplicitConv ic = ic_in;
+  implicit_conv_magic(&ic);
   if (cfg < GEMM_128x128_K32 || cfg >= GEMM_NUM_CFGS || (mode != GEMM_IMPLICIT && mode != GEMM_IMPLICIT_POOL)) {
     set_error("gemm_implicit: bad cfg %d / mode %d", cfg, mode);
     return -2;

@@ -101,10 +101,12 @@ static int launch16_any(int cfg, const half_t* A, int lda, const half_t* Bt, int
                                st);
 }
 
-int launch_gemm16(int cfg, int mode, const half_t* A, int lda, const ImplicitConv& ic, const half_t* Bt, int ldb,
+int launch_gemm16(int cfg, int mode, const half_t* A, int lda, const ImplicitConv& ic_in, const half_t* Bt, int ldb,
                   half_t* C, int ldc, long long M, int N, int Kpad, const EpiParams& epi, hipStream_t stream,
                   int splits, float* slab, unsigned* tickets) {
   if (M == 0 || N == 0) return 0;
+  ImplicitConv ic = ic_in;
+  implicit_conv_magic(&ic);
   if (cfg < 0 || cfg >= GEMM16_NUM_CFGS || mode < GEMM_DENSE || mode > GEMM_IMPLICIT_POOL) {
     set_error("gemm16: bad cfg %d / mode %d", cfg, mode);
     return -2;
