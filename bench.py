@@ -366,13 +366,16 @@ def main():
     backend = os.environ.get("DNN_BENCH_BACKEND", "nccl")
     torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)
-    if world > 1:
+    # under torch.distributed.run (any world size, including 1) the process group exists and
+    # every collective below runs over it; a plain `python bench.py` runs without one
+    distributed = world > 1 or "TORCHELASTIC_RUN_ID" in os.environ or os.environ.get("DNN_BENCH_DIST") == "1"
+    if distributed:
         D.init(backend, device=dev)
 
     B = args.batch
-    # rank 0 holds the weights; the other ranks only lay the plan out and receive the
-    # packed buffer by broadcast
-    ws = synth.yolo_weights() if rank == 0 else yolo_graph.zero_weights_like(synth.yolo_weights())
+    # rank 0 holds the weights; the other ranks only lay the plan out (zero weights of the
+    # right shapes, no generator run) and receive the packed buffer by broadcast
+    ws = synth.yolo_weights() if rank == 0 else synth.yolo_zero_weights()
     g, _ = yolo_graph.build_graph(dnn_hip.DnnGraphBuilder, ws, in_shape=(B, 416, 416, 3))
     entries = dnn_hip.lower_graph(g)
     wbytes, sbytes = dnn_hip.Plan.memory(B, (416, 416, 3), entries, precision=args.precision)
@@ -392,25 +395,27 @@ def main():
     def compute(inp, out, n):
         plan.run_device(n, inp.data_ptr(), out.data_ptr(), stream)
 
-    runner = D.ShardedRunner(compute, B * world, (416, 416, 3), (13, 13, 125), dev)
+    runner = D.ShardedRunner(compute, B * world, (416, 416, 3), (13, 13, 125), dev,
+                             timing=os.environ.get("DNN_BENCH_STEP_EVENTS", "1") == "1",
+                             gather_mode=os.environ.get("DNN_BENCH_GATHER_MODE", "sized"))
     if args.gather == "detections":
         import yolo_post
-        dbufs = [yolo_post.DetectionBuffers(runner.shard_cap, dev) for _ in range(2)]
+        dbufs = [yolo_post.DetectionBuffers(runner.shard_cap, dev) for _ in range(runner.slots)]
         dbuf = dbufs[0]
 
         def post(out, n, slot, post_stream):
             dbufs[slot].run(out.data_ptr(), n, post_stream)
             return dbufs[slot].pack(n, post_stream)
 
-        # two steps in flight: step k+1's forward is enqueued before step k's detections are
-        # collected (side stream), so the host sync, D2H and gathers overlap the GPU's work;
-        # the last step is collected before the clock stops
+        # runner.slots (3) steps in flight: steps k+1 and k+2 are enqueued before step k's
+        # detections are gathered (side stream) and collected, so gathers, D2H and rank 0's
+        # wait overlap the GPU's work; every step is collected before the clock stops
         pending = []
 
         def one_step():
-            pending.append(runner.launch_detections(frames, post, one_step.k & 1))
+            pending.append(runner.launch_detections(frames, post, one_step.k % runner.slots))
             one_step.k += 1
-            return runner.finish_detections(pending.pop(0)) if len(pending) == 2 else None
+            return runner.finish_detections(pending.pop(0)) if len(pending) == runner.slots else None
 
         one_step.k = 0
 
@@ -430,12 +435,14 @@ def main():
         one_step()
     drain()
     torch.cuda.synchronize()
-    if world > 1:
+    if distributed:
         tdist.barrier()
+    if args.gather == "detections":
+        runner.reset_stats()
 
     plan.timing_begin(args.steps)
     torch.cuda.synchronize()
-    if world > 1:
+    if distributed:
         tdist.barrier()
     t0 = time.perf_counter()
     full = None
@@ -445,14 +452,22 @@ def main():
     r = drain()
     full = r if r is not None else full
     torch.cuda.synchronize()
-    if world > 1:
+    if distributed:
         tdist.barrier()
     elapsed = time.perf_counter() - t0
     ms, cnt = plan.timing_end()
-    if world > 1:
+    # per-rank breakdown of the timed steps (means per step, ms), gathered to every rank
+    keys = ("wall_ms", "forward_ms", "post_ms", "gather_ms", "host_blocked_ms")
+    st = runner.stats() if args.gather == "detections" else {}
+    mine = [elapsed / args.steps * 1e3] + [float(st.get(k, float("nan"))) for k in keys[1:]]
+    per_rank = [mine]
+    if distributed:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
         elapsed = float(t.item())
+        parts = [torch.zeros(len(keys), dtype=torch.float64, device=dev) for _ in range(world)]
+        tdist.all_gather(parts, torch.tensor(mine, dtype=torch.float64, device=dev))
+        per_rank = [p.tolist() for p in parts]
 
     post_ms = None
     if args.gather == "detections":  # the postprocess kernel alone, for the per-kernel table
@@ -518,7 +533,9 @@ def main():
                           "net_pct_fp32_peak": round(100 * 6.971e9 * value / world / 1e12 / FP32_MFMA_PEAK_TFLOPS,
                                                      2)},
             "kernel_ms_per_step": round(total_kernel_ms, 4),
-            "dist_backend": ("rccl" if backend == "nccl" else backend) if world > 1 else None,
+            "dist_backend": ("rccl" if backend == "nccl" else backend) if distributed else None,
+            "per_rank": [dict(rank=r, **{k: (round(v, 4) if v == v else None) for k, v in zip(keys, vals)})
+                         for r, vals in enumerate(per_rank)],
         }
         if args.gather == "detections":
             res["postprocess"] = {"ms": round(post_ms, 4), "detections_last_step": n_det,
@@ -543,7 +560,7 @@ def main():
         print(json.dumps(res), flush=True)
 
     plan.close()
-    if world > 1:
+    if distributed:
         tdist.destroy_process_group()
 
 

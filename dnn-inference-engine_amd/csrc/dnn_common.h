@@ -121,6 +121,8 @@ enum GemmMode : int { GEMM_DENSE = 0, GEMM_IMPLICIT = 1, GEMM_IMPLICIT_POOL = 2 
 // ---------------------------------------------------------------- launchers
 // All launchers are asynchronous on `stream` and return 0 / negative on launch error.
 int launch_im2col(const float* in, float* col, const ConvGeom& g, hipStream_t stream);
+// K order (ic, kh, kw), K == Kpad, one image on a padded input (the per-op im2col ABI)
+int launch_im2col_ckk(const float* in, float* col, const ConvGeom& g, hipStream_t stream);
 // With splits > 1 (LDS-DMA configs only) the GEMM writes `splits` raw fp32 partials
 // [splits][M][N] to `slab` and NO epilogue; launch_splitk_reduce then sums them in split order
 // and applies the epilogue into C.  choose_splitk depends on (N, K) only.

@@ -29,20 +29,23 @@ typedef _Float16 half_t;
 __device__ __forceinline__ void store_out(float* p, float v) { *p = v; }
 __device__ __forceinline__ void store_out(half_t* p, float v) { *p = (half_t)v; }
 
-// x / d correctly rounded (the reference's division), as Markstein's correction of x * RN(1/d):
-// with y = RN(1/d) and q = RN(x*y) within 1 ulp of x/d, the residual r = x - q*d is exact (one
-// fma) and RN(q + r*y) is the correctly rounded quotient (no midpoint quotients exist in binary
-// floating point).  3 VALU per element instead of the ~11 of the IEEE division sequence; the
-// reciprocal is per output channel, so the compiler hoists it out of the element loops.  Zero,
-// denormal, infinite and NaN q (where the residual step is not exact or loses the sign of a
-// zero) take the IEEE division.  Checked bit for bit against x / d on 3e8 random pairs
-// (tools/markstein_check.c) and by every bit-exact epilogue test.
+// x / d correctly rounded (the reference's fp32 division), as RN32(RN64(x * RN64(1/d))).
+// Proof: for significands a = sig(x), b = sig(d) in [1, 2) no quotient a/b is a float
+// midpoint, and its relative distance to every midpoint exceeds 2^-49 (in the [1/2, 1) binade
+// a - m*b is a non-zero multiple of 2^-48 for a midpoint m = (2k+1)*2^-25, so
+// |a/b - m| >= 2^-48/b > 2^-49 * a/b; in [1, 2) it is a multiple of 2^-47 with m = (2k+1)*2^-24,
+// so |a/b - m| > 2^-48 > 2^-49 * a/b).  The double product is within (1+2^-53)^2 - 1 < 2^-51
+// of x/d (a correctly rounded double reciprocal, one double rounding), so it lies on the same
+// side of every float midpoint as x/d and rounds to RN32(x/d) — also at the overflow
+// threshold, which is the midpoint between FLT_MAX and 2^128.  Zero and denormal quotients
+// (where the float rounding step is coarser) take the IEEE division.  The reciprocal is per
+// output channel, so the compiler hoists it out of the element loops; per element: two
+// conversions and one f64 multiply.
 __device__ __forceinline__ float div_rn(float x, float d) {
-  const float y = 1.0f / d;
-  const float q = x * y;
-  if (__builtin_amdgcn_classf(q, 0x2F7)) return x / d;  // NaN, +-inf, +-0, +-denormal
-  const float r = __builtin_fmaf(-q, d, x);
-  return __builtin_fmaf(r, y, q);
+  const double y = 1.0 / (double)d;
+  const float q = (float)((double)x * y);
+  if (__builtin_amdgcn_classf(q, 0x0F0)) return x / d;  // +-0, +-denormal
+  return q;
 }
 
 __device__ __forceinline__ float apply_epilogue(float v, float bias, float mean, float sq, float gamma,

@@ -145,6 +145,33 @@ int launch_im2col(const float* in, float* col, const ConvGeom& g, hipStream_t st
   return check_launch("im2col");
 }
 
+// The per-op ABI's im2col (proj3/dnn_openblas.c:135-158): K order (ic, kh, kw) on an
+// already padded input, col[m][c*kh*kw + t] = in[oy*sh + t/kw][ox*sw + t%kw][c] for one image.
+// Diagnostic entry point (the plan never materialises this layout): one thread per column
+// element, consecutive threads write consecutive K columns of a row (coalesced stores).
+__global__ void __launch_bounds__(256)
+im2col_ckk_kernel(const float* __restrict__ in, float* __restrict__ col, ConvGeom g, long long total) {
+  const int khw = g.kh * g.kw;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (long long)gridDim.x * blockDim.x) {
+    const long long m = e / g.K;
+    const int k = (int)(e - m * g.K);
+    const int c = k / khw, t = k - c * khw;
+    const int dy = t / g.kw, dx = t - dy * g.kw;
+    const int ox = (int)(m % g.OW), oy = (int)(m / g.OW);
+    col[e] = in[((long long)(oy * g.sh + dy) * g.W + (ox * g.sw + dx)) * g.C + c];
+  }
+}
+
+int launch_im2col_ckk(const float* in, float* col, const ConvGeom& g, hipStream_t stream) {
+  const long long total = (long long)g.OH * g.OW * g.K;
+  if (total == 0) return 0;
+  const long long blocks = (total + 255) / 256;
+  hipLaunchKernelGGL(im2col_ckk_kernel, dim3((unsigned)(blocks < 65536 ? blocks : 65536)), dim3(256), 0, stream, in,
+                     col, g, total);
+  return check_launch("im2col_ckk");
+}
+
 struct CfgInfo {
   int bm, bn, bk;
 };

@@ -112,25 +112,20 @@ int legacy_conv(const float* in, const float* w, int order, float* out, int B, i
 
 int legacy_im2col(const float* imb, float* colb, int oh, int ow, int ih, int iw, int ic, int kh, int kw, int sh,
                   int sw) {
-  // K order (ic, kh, kw) as dnn_openblas.c:135-158: run our (kh, kw, ic) im2col on the
-  // device, then permute the columns on the host.  Diagnostic entry point only.
+  // K order (ic, kh, kw) as dnn_openblas.c:135-158, gathered in that order on the device
+  // (im2col_ckk_kernel).  Diagnostic entry point only: the plan uses implicit GEMM.
   DNN_REQUIRE(oh > 0 && ow > 0 && ic > 0 && kh > 0 && kw > 0 && sh > 0 && sw > 0, "im2col: bad shape");
   DNN_REQUIRE((oh - 1) * sh + kh <= ih && (ow - 1) * sw + kw <= iw, "im2col: window exceeds input");
   std::lock_guard<std::mutex> lk(g_mu);
   if (int rc = ensure_device()) return rc;
-  const int K = kh * kw * ic, Kpad = (K + 3) / 4 * 4;
+  const int K = kh * kw * ic;
   const size_t M = (size_t)oh * ow, n_in = (size_t)ih * iw * ic;
   SLOT(d_in, 0, n_in);
-  SLOT(d_col, 3, M * Kpad);
+  SLOT(d_col, 3, M * K);
   if (int rc = h2d(d_in, imb, n_in)) return rc;
-  ConvGeom g{1, ih, iw, ic, oh, ow, kh, kw, sh, sw, 0, 0, K, Kpad};
-  if (int rc = launch_im2col(d_in, d_col, g, 0)) return rc;
-  std::vector<float> tmp(M * Kpad);
-  if (int rc = d2h(tmp.data(), d_col, tmp.size())) return rc;
-  for (size_t m = 0; m < M; ++m)
-    for (int c = 0; c < ic; ++c)
-      for (int t = 0; t < kh * kw; ++t) colb[m * K + (size_t)c * kh * kw + t] = tmp[m * Kpad + (size_t)t * ic + c];
-  return 0;
+  ConvGeom g{1, ih, iw, ic, oh, ow, kh, kw, sh, sw, 0, 0, K, K};
+  if (int rc = launch_im2col_ckk(d_in, d_col, g, 0)) return rc;
+  return d2h(colb, d_col, M * K);
 }
 
 int legacy_pool(const float* in, float* out, int B, int oh, int ow, int od, int ih, int iw, int ic, int kh, int kw,

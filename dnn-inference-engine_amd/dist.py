@@ -5,13 +5,17 @@ are independent, so a global batch is split into contiguous per-rank shards with
 exchange between layers.  The only collectives are the ones the north star names:
   * one broadcast of the packed weight buffer from rank 0 at start-up (63.5 MB fp32);
   * per batch, a gather to rank 0 of either the raw outputs ([n,13,13,125] fp32 per rank,
-    gather_outputs) or — after the on-GPU postprocessing (yolo_post.py) — only the packed
-    detections (40 B each, gather_detections: a few kB per image instead of 84.5 kB).
+    gather_outputs) or — after the on-GPU postprocessing (yolo_post.py) — the packed
+    detections (DetectionGather: sizes all-gathered then max-over-ranks valid rows, with
+    three steps in flight so the host wait is on a step whose successors are queued; or a
+    fixed-capacity buffer sent without any host synchronisation).
 One process per GPU, torch.distributed over RCCL ("nccl" backend) on the GPU box, gloo
 for the CPU tests; the compute step is injected, so the same runner drives the HIP plan
 (bench.py) and a CPU stand-in (tests/test_dist_cpu.py).
 """
 import os
+import time
+from contextlib import nullcontext as _nullcontext
 
 import numpy as np
 import torch
@@ -56,9 +60,15 @@ def _host_staged(t):
     return t.is_cuda and dist.get_backend() == "gloo"
 
 
+def _collectives():
+    """Collectives run whenever a process group exists — also at world size 1, so a
+    one-process RCCL group executes the same broadcast/gather code the 8-GPU job does."""
+    return dist.is_available() and dist.is_initialized()
+
+
 def broadcast_weights(buf, src=0):
     """Broadcast a flat weight tensor in place from `src` (once, at start-up)."""
-    if dist.is_initialized() and dist.get_world_size() > 1:
+    if _collectives():
         if _host_staged(buf):
             h = buf.cpu()
             dist.broadcast(h, src=src)
@@ -79,21 +89,11 @@ def _gather(t, parts, dst):
         dist.gather(t, parts, dst=dst)
 
 
-def _all_gather(parts, t):
-    if _host_staged(t):
-        hp = [torch.empty(p.shape, dtype=p.dtype) for p in parts]
-        dist.all_gather(hp, t.cpu())
-        for p, h in zip(parts, hp):
-            p.copy_(h)
-    else:
-        dist.all_gather(parts, t)
-
-
 def gather_outputs(local, dst=0):
     """Gather equal-shaped per-rank output tensors to `dst`; returns the concatenation on
     `dst` (rank order = shard order) and None elsewhere.  Shards of unequal size are padded
     to the largest by the caller (see ShardedRunner)."""
-    if not dist.is_initialized() or dist.get_world_size() == 1:
+    if not _collectives():
         return local
     rank, world = dist.get_rank(), dist.get_world_size()
     parts = [torch.empty_like(local) for _ in range(world)] if rank == dst else None
@@ -101,42 +101,108 @@ def gather_outputs(local, dst=0):
     return torch.cat(parts, 0) if rank == dst else None
 
 
-def gather_detections(packed, total, counts, n, dst=0):
-    """Gather this rank's packed detections to `dst`.
+class DetectionGather(object):
+    """Gather of every rank's packed detections to `dst` (the "gather of
+    detections").  Per step each rank contributes
+      meta    int32 [2 + cap]: valid rows of `packed`, valid images n, counts[:cap]
+              (counts < 0: that image's error code);
+      payload rows of its packed buffer [cap * max_det, 40] uint8 (image-major).
+    Two modes:
+      "sized" (default)  meta is all-gathered (fixed size, 264 B at cap 64), every rank reads
+              the sizes on the host and the payload gather moves max-over-ranks valid rows
+              (≈45 detections per image with the synthetic weights: ≈115 kB per rank).  The
+              host read waits for that step on all ranks, so the caller keeps steps in
+              flight (ShardedRunner: three) and the wait is on a step whose successors are
+              already queued on the GPU;
+      "fixed"  meta is gathered to `dst` and the payload is the whole packed buffer (its
+              capacity is the most detections `cap` images can have, 845 each: 2.16 MB per
+              rank at 64 images), so no rank ever reads a size on the host before sending and
+              non-root ranks never wait; costs a longer RCCL kernel per step beside the
+              forward (measured: 0.13 ms at one rank vs 0.02 ms sized).
+    Receive buffers are allocated once per slot."""
 
-    packed  [rows, 40] uint8 tensor: the rank's detections image-major (yolo_post
-            DetectionBuffers.pack / dnn_yolo_pack_detections), rows >= total
-    total   [1] int32 tensor: valid rows of `packed`
-    counts  [cap] int32 tensor: detections per image (< 0: the image's error code)
-    n       valid images of this rank's shard
-    Returns on `dst` (dets_u8 [P, 40] numpy, counts [sum of n over ranks] numpy int32) in
-    global (rank, image) order; None elsewhere.  One scalar sync for the row count, then
-    (N > 1) an all_gather of two scalars and gathers of max_rank(P) * 40 B and the counts."""
-    p = int(total.item())
-    if not dist.is_initialized() or dist.get_world_size() == 1:
-        return packed[:p].cpu().numpy(), counts[:n].cpu().numpy()
-    rank, world = dist.get_rank(), dist.get_world_size()
-    dev = packed.device
-    sizes = [torch.zeros(2, dtype=torch.int64, device=dev) for _ in range(world)]
-    _all_gather(sizes, torch.tensor([p, n], dtype=torch.int64, device=dev))
-    sizes = [tuple(int(v) for v in t.cpu()) for t in sizes]
-    pmax, nmax = max(max(sz[0] for sz in sizes), 1), max(max(sz[1] for sz in sizes), 1)
-    if packed.shape[0] >= pmax:
-        pbuf = packed[:pmax].contiguous()
-    else:
-        pbuf = torch.zeros((pmax, packed.shape[1]), dtype=torch.uint8, device=dev)
-        pbuf[:p] = packed[:p]
-    cbuf = torch.zeros(nmax, dtype=torch.int32, device=dev)
-    cbuf[:n] = counts[:n]
-    pparts = [torch.empty_like(pbuf) for _ in range(world)] if rank == dst else None
-    cparts = [torch.empty_like(cbuf) for _ in range(world)] if rank == dst else None
-    _gather(pbuf, pparts, dst)
-    _gather(cbuf, cparts, dst)
-    if rank != dst:
-        return None
-    d = torch.cat([pparts[r][:sizes[r][0]] for r in range(world)], 0).cpu().numpy()
-    cnt = torch.cat([cparts[r][:sizes[r][1]] for r in range(world)], 0).cpu().numpy()
-    return d, cnt
+    def __init__(self, cap, rows, device, slots=2, dst=0, mode="sized"):
+        if mode not in ("sized", "fixed"):
+            raise ValueError(f"mode {mode!r}")
+        self.cap, self.rows, self.dst, self.mode = int(cap), int(rows), dst, mode
+        self.rank = dist.get_rank() if _collectives() else 0
+        self.world = dist.get_world_size() if _collectives() else 1
+        self.meta = [torch.zeros(2 + self.cap, dtype=torch.int32, device=device) for _ in range(slots)]
+        root = self.rank == dst
+        coll = _collectives()
+        all_meta = coll and mode == "sized"
+        self.mparts = [[torch.empty_like(m) for _ in range(self.world)] if coll and (root or all_meta) else None
+                       for m in self.meta]
+        self.pparts = [[torch.empty((self.rows, 40), dtype=torch.uint8, device=device) for _ in range(self.world)]
+                       if coll and root else None for _ in range(slots)]
+
+    def launch(self, slot, packed, total, counts, n):
+        """Enqueue slot `slot`'s gathers on the current stream ("sized": after reading the
+        all-gathered sizes on the host); returns a handle for finish()."""
+        if packed.shape[0] != self.rows:
+            raise ValueError(f"packed has {packed.shape[0]} rows, the gather was sized for {self.rows}")
+        meta = self.meta[slot]
+        meta[0:1].copy_(total[:1], non_blocking=True)
+        meta[1].fill_(int(n))
+        k = min(self.cap, counts.shape[0])
+        meta[2:2 + k].copy_(counts[:k], non_blocking=True)
+        coll, root = _collectives(), self.rank == self.dst
+        sizes = None
+        if not coll:
+            mparts, pparts = [meta], [packed]
+        elif self.mode == "sized":
+            mparts = self.mparts[slot]
+            if _host_staged(meta):
+                hp = [torch.empty(p.shape, dtype=p.dtype) for p in mparts]
+                dist.all_gather(hp, meta.cpu())
+                for p, h in zip(mparts, hp):
+                    p.copy_(h)
+            else:
+                dist.all_gather(mparts, meta)
+            sizes = torch.stack(mparts).cpu().numpy()  # host read: this step, every rank
+            pmax = int(sizes[:, 0].max())
+            pparts = self.pparts[slot]
+            if pmax > 0:
+                _gather(packed[:pmax], [p[:pmax] for p in pparts] if root else None, self.dst)
+        else:
+            mparts, pparts = self.mparts[slot], self.pparts[slot]
+            _gather(meta, mparts if root else None, self.dst)
+            _gather(packed, pparts if root else None, self.dst)
+        done, stream = None, None
+        if packed.is_cuda:
+            stream = torch.cuda.current_stream(packed.device)
+            done = torch.cuda.Event()
+            done.record(stream)
+        return (mparts, pparts, sizes) if root else None, done, stream
+
+    @staticmethod
+    def finish(handle):
+        """On `dst`: wait for the slot's gather, then (dets_u8 [P, 40] numpy, counts numpy
+        int32) in global (rank, image) order; None on other ranks (no wait).  The copies out
+        run on the stream the gather was enqueued on, never behind later forwards."""
+        parts, done, stream = handle
+        if parts is None:
+            return None
+        if done is not None:
+            done.synchronize()
+        mparts, pparts, meta = parts
+        with torch.cuda.stream(stream) if stream is not None else _nullcontext():
+            if meta is None:
+                meta = torch.stack(mparts).cpu().numpy()  # [world, 2 + cap]
+            dets = [pparts[r][:int(meta[r, 0])] for r in range(len(mparts))]
+            d = torch.cat(dets, 0).cpu().numpy()
+        cnt = np.concatenate([meta[r, 2:2 + int(meta[r, 1])] for r in range(len(mparts))]).astype(np.int32)
+        return d, cnt
+
+
+def gather_detections(packed, total, counts, n, dst=0, mode="sized"):
+    """Synchronous one-step form of DetectionGather: this rank's packed detections (packed
+    [rows, 40] uint8 image-major from dnn_yolo_pack_detections, total [1] int32 valid rows,
+    counts [>= n] int32 per image, n valid images) gathered to `dst`.  Returns (dets_u8
+    [P, 40] numpy, counts numpy int32) in global (rank, image) order on `dst`, None
+    elsewhere."""
+    g = DetectionGather(counts.shape[0], packed.shape[0], packed.device, slots=1, dst=dst, mode=mode)
+    return g.finish(g.launch(0, packed, total, counts, n))
 
 
 def unpack_detections(dets_u8, counts):
@@ -162,7 +228,13 @@ class ShardedRunner(object):
     in_shape  per-frame input shape, out_shape per-frame output shape
     """
 
-    def __init__(self, compute, global_batch, in_shape, out_shape, device, dtype=torch.float32):
+    def __init__(self, compute, global_batch, in_shape, out_shape, device, dtype=torch.float32, timing=True,
+                 slots=3, gather_mode="sized"):
+        self.timing = bool(timing)  # per-step HIP timing events for stats()
+        self.gather_mode = gather_mode  # DetectionGather mode of the pipelined path
+        # steps in flight on the pipelined path (launch_detections / finish_detections):
+        # step k is collected after step k + slots - 1 has been launched
+        self.slots = int(slots)
         self.rank = dist.get_rank() if dist.is_initialized() else 0
         self.world = dist.get_world_size() if dist.is_initialized() else 1
         self.global_batch = int(global_batch)
@@ -192,48 +264,76 @@ class ShardedRunner(object):
         return torch.cat(rows, 0)
 
     def launch_detections(self, local_in, post, slot):
-        """Pipelined form of step_detections, first half: enqueue the forward for this rank's
-        shard into output slot `slot` (0/1) on the current stream, and `post(out, n, slot,
-        stream_ptr)` (postprocess + pack) on a post stream that waits only for that forward,
-        without waiting; returns a handle for finish_detections.  The postprocessing of step
-        k (one workgroup per image: a quarter of the CUs) thus runs beside step k+1's first
-        layers instead of between the two forwards.  The slot's previous gather must have
-        been finished (its reads are ordered before this launch, and through the forward's
-        event before this post)."""
+        """Pipelined form of step_detections, first half — nothing here waits on the host:
+        the forward for this rank's shard into output slot `slot` (< slots) on the current
+        stream (after the slot's previous gather has drained, device-side), then
+        `post(out, n, slot, stream_ptr)` (postprocess + pack) on a post stream that waits
+        only for that forward, so step k's postprocessing runs beside step k+1's first
+        layers.  Returns a handle for finish_detections."""
         dev = self.out.device
         if not hasattr(self, "_outs"):
-            self._outs = [self.out, torch.zeros_like(self.out)]
+            self._outs = [self.out] + [torch.zeros_like(self.out) for _ in range(self.slots - 1)]
             self._side = torch.cuda.Stream(dev)
             self._post = torch.cuda.Stream(dev)
-            self._freed = [None, None]
+            self._freed = [None] * self.slots
+            self._gather = None
+            self.reset_stats()
         cur = torch.cuda.current_stream(dev)
         if self._freed[slot] is not None:
             cur.wait_event(self._freed[slot])
+        ev = [torch.cuda.Event(enable_timing=self.timing) for _ in range(5)]
         out = self._outs[slot]
+        ev[0].record(cur)
         self.compute(local_in, out, self.count)
-        done = torch.cuda.Event()
-        done.record(cur)
-        self._post.wait_event(done)
+        ev[1].record(cur)
+        self._post.wait_event(ev[1])
         with torch.cuda.stream(self._post):
             packed, total, counts = post(out, self.count, slot, self._post.cuda_stream)
-        ready = torch.cuda.Event()
-        ready.record(self._post)
-        return slot, packed, total, counts, ready
+            ev[2].record(self._post)
+        return slot, packed, total, counts, ev
 
     def finish_detections(self, handle):
-        """Second half: on a side stream that waits only for that step's pack (so later steps
-        already enqueued keep the GPU busy), read the row count and gather the packed
-        detections (as gather_detections).  Returns what step_detections returns."""
-        slot, packed, total, counts, ready = handle
+        """Second half, called once the next slots - 1 steps have been launched (three steps
+        in flight by default, so rank 0 waits for a gather that finished a forward ago and
+        the host never starves the queue while an RCCL gather waits for CUs): enqueue the
+        detection gather (DetectionGather) on a side stream that waits only
+        for this step's pack — enqueued this late so that no stream whose hardware queue may
+        be shared with the run stream holds a wait ahead of the next forward — then on
+        rank 0 wait for it and return (dets_u8 [P, 40], counts [global_batch]) numpy; other
+        ranks return None at once (no host synchronisation)."""
+        slot, packed, total, counts, ev = handle
+        if self._gather is None:
+            self._gather = DetectionGather(self.shard_cap, packed.shape[0], self.out.device,
+                                           slots=self.slots, mode=self.gather_mode)
+        t0 = time.perf_counter()
         with torch.cuda.stream(self._side):
-            self._side.wait_event(ready)
-            r = gather_detections(packed, total, counts, self.count)
-            freed = torch.cuda.Event()
-            freed.record(self._side)
-        self._freed[slot] = freed
+            self._side.wait_event(ev[2])
+            ev[3].record(self._side)
+            gh = self._gather.launch(slot, packed, total, counts, self.count)
+            ev[4].record(self._side)
+        self._freed[slot] = ev[4]
+        r = DetectionGather.finish(gh)
+        self._host_blocked += time.perf_counter() - t0
+        self._events.append(ev)
         return r
 
-    def step_detections(self, local_in, post):
+    def reset_stats(self):
+        self._events, self._host_blocked = [], 0.0
+
+    def stats(self):
+        """Per-step means (ms) over the steps finished since reset_stats(): forward (run
+        stream), post (postprocess + pack), gather (the collectives on the side stream),
+        host_blocked (host time inside finish_detections).  Call after synchronising."""
+        n = len(self._events)
+        if n == 0 or not self.timing:
+            return {"host_blocked_ms": round(self._host_blocked * 1e3 / max(n, 1), 4), "steps": n}
+        f = sum(e[0].elapsed_time(e[1]) for e in self._events) / n
+        p = sum(e[1].elapsed_time(e[2]) for e in self._events) / n
+        g = sum(e[3].elapsed_time(e[4]) for e in self._events) / n
+        return {"forward_ms": round(f, 4), "post_ms": round(p, 4), "gather_ms": round(g, 4),
+                "host_blocked_ms": round(self._host_blocked * 1e3 / n, 4), "steps": n}
+
+    def step_detections(self, local_in, post, mode="sized"):
         """One batch ending in detections: local compute, then `post(out, n)` -> (packed
         [rows, 40] uint8, total [1] int32, counts [cap] int32) on this rank's device (the
         on-GPU postprocessing + pack), then the packed detection gather.  Returns (dets_u8
@@ -241,4 +341,4 @@ class ShardedRunner(object):
         None elsewhere."""
         self.compute(local_in, self.out, self.count)
         packed, total, counts = post(self.out, self.count)
-        return gather_detections(packed, total, counts, self.count)
+        return gather_detections(packed, total, counts, self.count, mode=mode)

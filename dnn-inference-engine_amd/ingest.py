@@ -44,7 +44,18 @@ def resize_input_gpu(im, device=0):
 class FrameIngest(object):
     """Double-buffered uint8 upload + GPU preprocessing for batches of `batch` frames of
     h x w x 3 uint8 BGR.  submit(frames) returns the fp32 [n,416,416,3] device tensor for
-    that batch; it is ready in stream order on `compute_stream`."""
+    that batch; it is ready in stream order on `compute_stream`.
+
+    Slot reuse is ordered without any call from the caller: before slot k is refilled,
+      * the host waits until the previous upload out of pinned host[k] has completed
+        (next_host_buffer / submit_host), so the CPU never rewrites a buffer the copy
+        engine is still reading;
+      * the copy stream waits for the previous preprocess that read dev_u8[k], so an upload
+        never overwrites 8-bit frames that are still being resized;
+      * the preprocess writing out[k] runs on the compute stream after everything enqueued
+        there before it (the forward that read out[k] two batches ago).
+    release(stream) is needed only when the returned tensor is consumed on ANOTHER stream:
+    it records that consumption so the preprocess that next overwrites the slot waits for it."""
 
     def __init__(self, batch, h, w, device, compute_stream=None, out_hw=(IN_SIZE, IN_SIZE)):
         import torch
@@ -58,17 +69,18 @@ class FrameIngest(object):
                     for _ in range(2)]
         self.copy_stream = torch.cuda.Stream(self.dev)
         self.compute = compute_stream or torch.cuda.current_stream(self.dev)
-        self.uploaded = [torch.cuda.Event() for _ in range(2)]
-        self.consumed = [torch.cuda.Event() for _ in range(2)]
-        for e in self.consumed:
-            e.record(self.compute)
+        self.uploaded = [None, None]   # upload out of host[k] (copy stream)
+        self.prepped = [None, None]    # preprocess that read dev_u8[k] (compute stream)
+        self.consumed = [None, None]   # off-stream consumer of out[k] (release())
         self.slot = 0
+        self.last = None
 
     def next_host_buffer(self):
         """The pinned uint8 [batch, h, w, 3] buffer the next submit_host() uploads: a frame
-        decoder can write into it directly (no extra host copy).  Waits until the slot's
-        previous batch has been consumed."""
-        self.consumed[self.slot].synchronize()
+        decoder can write into it directly (no extra host copy).  Waits (host) until the
+        previous upload out of that buffer has completed."""
+        if self.uploaded[self.slot] is not None:
+            self.uploaded[self.slot].synchronize()
         return self.host[self.slot]
 
     def submit(self, frames):
@@ -83,18 +95,38 @@ class FrameIngest(object):
 
     def submit_host(self, n):
         """Upload the first n frames of the current pinned slot and preprocess them."""
+        torch = self.torch
         k = self.slot
         self.slot ^= 1
-        self.consumed[k].synchronize()
-        with self.torch.cuda.stream(self.copy_stream):
+        if not 0 <= n <= self.batch:
+            raise ValueError(f"n={n} outside [0, {self.batch}]")
+        up = torch.cuda.Event()
+        with torch.cuda.stream(self.copy_stream):
+            if self.prepped[k] is not None:
+                self.copy_stream.wait_event(self.prepped[k])  # dev_u8[k]'s last reader is done
             self.dev_u8[k][:n].copy_(self.host[k][:n], non_blocking=True)
-            self.uploaded[k].record(self.copy_stream)
-        self.compute.wait_event(self.uploaded[k])
+            up.record(self.copy_stream)
+        self.uploaded[k] = up
+        self.compute.wait_event(up)
+        if self.consumed[k] is not None:
+            self.compute.wait_event(self.consumed[k])  # an off-stream reader of out[k]
+            self.consumed[k] = None
         preprocess_device(self.dev_u8[k].data_ptr(), n, self.h, self.w, self.out[k].data_ptr(),
                           self.compute.cuda_stream, self.out_hw)
+        pe = torch.cuda.Event()
+        pe.record(self.compute)
+        self.prepped[k] = pe
+        self.last = k
         return self.out[k][:n]
 
-    def release(self):
-        """Mark the most recently returned batch as consumed: call after the work that reads
-        it (the forward) has been enqueued on the compute stream."""
-        self.consumed[self.slot ^ 1].record(self.compute)
+    def release(self, stream=None):
+        """The most recently returned batch is being read on `stream` (default: the compute
+        stream, where nothing needs recording): call after that work has been enqueued, so
+        the preprocess that reuses the slot waits for it.  Optional on the compute stream."""
+        if self.last is None:
+            return
+        if stream is None or stream == self.compute:
+            return
+        e = self.torch.cuda.Event()
+        e.record(stream)
+        self.consumed[self.last] = e

@@ -97,6 +97,22 @@ def yolo_weights(seed=WEIGHT_SEED, channels=CHANNELS, in_c=IN_SHAPE[2]):
     return ws
 
 
+def yolo_zero_weights(channels=CHANNELS, in_c=IN_SHAPE[2]):
+    """yolo_weights' shapes with zero values, without running the generator: what a
+    non-root rank lays its plan out with before the weight broadcast fills it."""
+    ws, ic = [], in_c
+    for i, od in enumerate(channels):
+        last = i == len(channels) - 1
+        k = 1 if last else 3
+        w = {"kernel": np.zeros((k, k, ic, od), np.float32), "biases": np.zeros(od, np.float32)}
+        if not last:
+            for key in ("moving_mean", "moving_variance", "gamma"):
+                w[key] = np.zeros(od, np.float32)
+        ws.append(w)
+        ic = od
+    return ws
+
+
 def frame(index, shape=IN_SHAPE):
     """Synthetic frame `index`: uniform [0,1) fp32 NHWC [1,H,W,C]
     (the range of `proj3/__init__.py:8-12` resize_input output)."""

@@ -30,6 +30,10 @@ typedef struct dnn_plan dnn_plan;
 /* Last error message of the calling thread ("" if none). */
 const char* dnn_last_error(void);
 
+/* First 16 hex digits of the SHA-256 of the sources this library was built from
+ * (csrc/Makefile SRCS); tests/conftest.py refuses a library whose id does not match. */
+const char* dnn_build_id(void);
+
 /* Create an empty plan for inputs [batch, in_h, in_w, in_c]. */
 int dnn_plan_create(int batch, int in_h, int in_w, int in_c, dnn_plan** out);
 void dnn_plan_destroy(dnn_plan* plan);

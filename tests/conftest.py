@@ -19,12 +19,53 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs through the HIP C-ABI)")
 
 
+CSRC = os.path.join(PKG, "csrc")
+LIBS = [os.path.join(PKG, "libdnn_hip.so"), os.path.join(PKG, "libdnn_hip_avx.so")]
+
+
+def source_hash():
+    """csrc/Makefile's SRC_HASH: SHA-256 (16 hex) of Makefile + sorted csrc/*.{hip,cpp,h} +
+    sorted include/*.h, concatenated."""
+    import glob
+    import hashlib
+    names = sorted(os.path.basename(p) for e in ("*.hip", "*.cpp", "*.h") for p in glob.glob(os.path.join(CSRC, e)))
+    files = [os.path.join(CSRC, "Makefile")] + [os.path.join(CSRC, n) for n in names]
+    files += sorted(glob.glob(os.path.join(REPO, "include", "*.h")))
+    h = hashlib.sha256()
+    for f in files:
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def library_build_id(path):
+    import ctypes
+    lib = ctypes.CDLL(path)
+    lib.dnn_build_id.restype = ctypes.c_char_p
+    return lib.dnn_build_id().decode()
+
+
+def _stale(path, want):
+    """Read the id in a child process: this process must not keep a stale library mapped."""
+    if not os.path.exists(path):
+        return True
+    r = subprocess.run([sys.executable, "-c", "import ctypes,sys; l=ctypes.CDLL(sys.argv[1]); "
+                        "l.dnn_build_id.restype=ctypes.c_char_p; print(l.dnn_build_id().decode())", path],
+                       capture_output=True, text=True)
+    return r.returncode != 0 or r.stdout.strip() != want
+
+
 def _ensure_built():
-    libs = [os.path.join(PKG, "libdnn_hip.so"), os.path.join(PKG, "libdnn_hip_avx.so")]
-    if not all(os.path.exists(p) for p in libs):
-        subprocess.run(["make", "-s", "-j8", "-C", os.path.join(PKG, "csrc")], check=True)
-    if not os.path.exists(os.path.join(ORACLE, "liboracle_dnn.so")):
-        subprocess.run(["make", "-s", "-C", ORACLE], check=True)
+    """The HIP libraries must be built from exactly the sources in this tree: a library whose
+    dnn_build_id() differs is rebuilt (incremental make) where a toolchain exists, and the
+    session fails if it still differs — a stale .so is never tested as-is."""
+    want = source_hash()
+    if any(_stale(p, want) for p in LIBS):
+        subprocess.run(["make", "-s", "-j8", "-C", CSRC], check=True)
+        bad = [p for p in LIBS if _stale(p, want)]
+        if bad:
+            raise RuntimeError(f"{bad}: dnn_build_id() != source hash {want} after make")
+    subprocess.run(["make", "-s", "-C", ORACLE], check=True)
 
 
 _ensure_built()

@@ -29,3 +29,45 @@ def test_bench_two_ranks_one_gpu(gather):
     assert d["cpu_baseline"] is None  # rank-0, N=1 only
     if gather == "detections":
         assert d["postprocess"]["detections_last_step"] > 0
+
+
+def _torchrun(script_args, timeout=300):
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1", "--master-addr",
+           "127.0.0.1", "--master-port", str(port)] + script_args
+    return subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=timeout)
+
+
+@pytest.mark.gpu
+def test_rccl_world1_broadcast_and_gathers():
+    """A real RCCL process group (backend "nccl", world size 1, cuda:0): the weight-arena
+    broadcast, gather_outputs and the pipelined detection gather (both modes) all execute
+    on MI355X and agree with the same work done without a process group."""
+    r = _torchrun([os.path.join(REPO, "tests", "rccl_world1_job.py")])
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert d["backend"] == "nccl" and d["arena_ok"] and d["detections"] > 0
+    assert d["outputs_shape"] == [8, 13, 13, 125]
+    for mode in ("sized", "fixed"):
+        m = d["modes"][mode]
+        assert m["ok"] and m["steps"] == 5, (mode, m)
+        assert m["stats"]["steps"] == 5 and m["stats"]["forward_ms"] > 0
+
+
+@pytest.mark.gpu
+def test_bench_under_torchrun_world1_rccl():
+    """bench.py as the driver launches it for N > 1 (torch.distributed.run), at one rank:
+    RCCL group, broadcast, detection gathers and the per-rank breakdown in the JSON line."""
+    r = _torchrun([os.path.join(REPO, "bench.py"), "--gpus", "1", "--batch", "8", "--steps", "3", "--warmup", "1",
+                   "--no-cpu", "--no-latency", "--no-e2e", "--no-fp16", "--no-unfused"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-3000:]
+    d = json.loads(lines[0])
+    assert d["dist_backend"] == "rccl" and d["n_gpus"] == 1
+    pr = d["per_rank"]
+    assert len(pr) == 1 and pr[0]["forward_ms"] > 0 and pr[0]["gather_ms"] >= 0
+    assert d["postprocess"]["detections_last_step"] > 0

@@ -94,17 +94,41 @@ def test_conv2d_mul_batched_and_strided(oc):
         assert R.normwise_err(node.result, oc.conv2d_mul(xp, kr, oh, ow, 3, 3, s, s)) < LAYER_TOL
 
 
-def test_im2col_abi_bit_exact(oc):
+@pytest.mark.parametrize("shape", [(9, 8, 6, 4, 3, 3, 3, 2, 2), (18, 18, 3, 16, 16, 3, 3, 1, 1),
+                                   (7, 7, 33, 7, 7, 1, 1, 1, 1), (10, 12, 5, 4, 5, 3, 2, 2, 2)])
+def test_im2col_abi_bit_exact(oc, shape):
+    """(ic, kh, kw) column order of dnn_openblas.c:135-158, gathered on the device."""
+    ih, iw, ic, oh, ow, kh, kw, sh, sw = shape
     lib = dnn_hip.mylib
     rng = np.random.default_rng(4)
-    xp = rng.standard_normal((1, 9, 8, 6)).astype(np.float32)
-    oh, ow, kh, kw, sh, sw = 4, 3, 3, 3, 2, 2
-    col = np.zeros((oh * ow, 6 * 9), np.float32)
-    lib.im2col(_p(xp), _p(col), oh, ow, 9, 8, 6, kh, kw, sh, sw)
+    xp = rng.standard_normal((1, ih, iw, ic)).astype(np.float32)
+    col = np.zeros((oh * ow, ic * kh * kw), np.float32)
+    lib.im2col(_p(xp), _p(col), oh, ow, ih, iw, ic, kh, kw, sh, sw)
     assert dnn_hip.last_error() == ""
     ref = np.empty_like(col)
-    oc.lib.oracle_im2col(xp.ctypes.data, ref.ctypes.data, oh, ow, 9, 8, 6, kh, kw, sh, sw)
+    oc.lib.oracle_im2col(xp.ctypes.data, ref.ctypes.data, oh, ow, ih, iw, ic, kh, kw, sh, sw)
     assert np.array_equal(col, ref)
+
+
+@pytest.mark.parametrize("name", ["c3_same", "c3_valid", "c1_same", "c2_same", "c3_wide"])
+def test_conv2d_cublas_abi_vs_golden(golden_ops, name):
+    """conv2d_cublas with the argument layout of proj3/dnn_cublas.py:176-191 (np.pad'ed input,
+    col scratch [batch, oh*ow, ic*kh*kw], kernel_r = kernel.transpose(2,0,1,3) as [K, od],
+    result shape, padded input shape, window, strides) vs the reference's conv golden."""
+    x, k = golden_ops[f"conv_{name}_x"], golden_ops[f"conv_{name}_k"]
+    pad = str(golden_ops[f"conv_{name}_pad"])
+    kh, kw, ic, od = k.shape
+    xp, oh, ow = R.pad_nhwc(x, kh, kw, 1, 1, pad)
+    xp = np.ascontiguousarray(xp, dtype=np.float32)
+    kr = np.ascontiguousarray(k.transpose(2, 0, 1, 3).reshape(-1, od))
+    col = np.zeros((x.shape[0], oh * ow, ic * kh * kw), np.float32)
+    out = np.zeros((x.shape[0], oh, ow, od), np.float32)
+    dnn_hip.mylib.conv2d_cublas(_p(xp), _p(col), _p(kr), _p(out), *map(ctypes.c_int, out.shape),
+                                *map(ctypes.c_int, xp.shape[1:]), ctypes.c_int(kh), ctypes.c_int(kw),
+                                ctypes.c_int(1), ctypes.c_int(1))
+    assert dnn_hip.last_error() == ""
+    assert R.normwise_err(out, golden_ops[f"conv_{name}_y"]) < 1e-5
+    assert R.normwise_err(out, R.conv2d(x, k, padding=pad)) < LAYER_TOL
 
 
 def test_legacy_error_is_raised():
@@ -731,3 +755,39 @@ def test_frame_ingest_pipeline_double_buffer(yolo_b1):
     for b, o in zip(batches, outs):
         ref = np.stack([IN.resize_input(f) for f in b])
         assert np.array_equal(o.cpu().numpy(), ref)
+
+
+def test_frame_ingest_reuse_ordered_without_release():
+    """slot reuse must be ordered without release().  Six batches through two
+    slots; a frame decoder rewrites the pinned buffer as soon as next_host_buffer() returns,
+    and each batch is read by a slow "forward" on the compute stream (a matmul chain first,
+    so the copy stream runs ahead of the compute stream) with no release() call.  A second
+    pass reads each batch on a side stream and records that with release(side).  Every batch
+    must equal the restated preprocess of its own frames."""
+    import torch
+    import ingest
+    import ingest_numpy as IN
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(31)
+    batches = [rng.integers(0, 256, size=(4, 120, 160, 3), dtype=np.uint8) for _ in range(6)]
+    busy = torch.randn(2048, 2048, device=dev)
+    for use_side in (False, True):
+        fi = ingest.FrameIngest(4, 120, 160, dev)
+        side = torch.cuda.Stream(dev)
+        outs = []
+        for b in batches:
+            fi.next_host_buffer()[:len(b)].numpy()[...] = b  # the decoder writes in place
+            x = fi.submit_host(len(b))
+            reader = side if use_side else fi.compute
+            reader.wait_stream(fi.compute)
+            with torch.cuda.stream(reader):
+                y = busy
+                for _ in range(8):
+                    y = y @ busy  # keeps the reader late
+                outs.append(x.clone())
+            if use_side:
+                fi.release(side)
+        torch.cuda.synchronize()
+        for b, o in zip(batches, outs):
+            ref = np.stack([IN.resize_input(f) for f in b])
+            assert np.array_equal(o.cpu().numpy(), ref)
