@@ -390,7 +390,14 @@ def main():
     gen = torch.Generator(device=dev)
     gen.manual_seed(1234 + rank)
     frames = torch.rand((B, 416, 416, 3), generator=gen, device=dev, dtype=torch.float32)
-    stream = torch.cuda.current_stream(dev).cuda_stream
+    # the run stream: a high-priority stream has a hardware queue of its own, so no RCCL,
+    # postprocess or gather stream can share its queue and serialise with the forwards
+    # (tools/stream_queue_probe.py: the null stream shares a queue with torch pool streams
+    # once RCCL has taken its own)
+    run_stream = torch.cuda.Stream(dev, priority=-1)
+    run_stream.wait_stream(torch.cuda.current_stream(dev))
+    torch.cuda.set_stream(run_stream)
+    stream = run_stream.cuda_stream
 
     def compute(inp, out, n):
         plan.run_device(n, inp.data_ptr(), out.data_ptr(), stream)

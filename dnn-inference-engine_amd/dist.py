@@ -273,8 +273,12 @@ class ShardedRunner(object):
         dev = self.out.device
         if not hasattr(self, "_outs"):
             self._outs = [self.out] + [torch.zeros_like(self.out) for _ in range(self.slots - 1)]
-            self._side = torch.cuda.Stream(dev)
-            self._post = torch.cuda.Stream(dev)
+            # high-priority streams: HIP gives each its own hardware queue (GPU_MAX_HW_QUEUES
+            # = 4 normal queues are shared round-robin by torch's stream pool, RCCL's internal
+            # streams and the null stream; tools/stream_queue_probe.py), so neither the
+            # postprocess nor the gather can end up serialised behind later forwards
+            self._side = torch.cuda.Stream(dev, priority=-1)
+            self._post = torch.cuda.Stream(dev, priority=-1)
             self._freed = [None] * self.slots
             self._gather = None
             self.reset_stats()

@@ -35,9 +35,10 @@ def main():
         t = torch.ones(4, device=dev)
         tdist.all_reduce(t)
     streams = {"null": torch.cuda.default_stream(dev)}
-    for i in range(6):
+    for i in range(4):
         streams[f"pool{i}"] = torch.cuda.Stream(dev)
-    streams["hi0"] = torch.cuda.Stream(dev, priority=-1)
+    for i in range(3):
+        streams[f"hi{i}"] = torch.cuda.Stream(dev, priority=-1)
     names = list(streams)
     print("queue-sharing matrix (X = serialised):", flush=True)
     for a in names:
