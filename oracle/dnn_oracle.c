@@ -56,6 +56,26 @@ void oracle_conv2d_mul(const float* in, const float* kernel_r, float* out, int b
   free(col);
 }
 
+/* proj3/dnn_openblas.c:160-194 as the OpenBLAS engine runs it (BASELINE config 1): per image
+ * single-thread im2col into a col buffer, then one cblas_sgemm(RowMajor, NoTrans, NoTrans,
+ * M, od, K, 1, col, K, kernel_r, od, 0, out, od).  The sgemm is OpenBLAS itself, reached
+ * through a function pointer the caller resolves in the OpenBLAS build numpy/scipy ship
+ * (oracle_c.openblas_sgemm: scipy_cblas_sgemm, 32-bit ints); no cblas.h is needed. */
+typedef void (*cblas_sgemm_fn)(int order, int ta, int tb, int m, int n, int k, float alpha, const float* a,
+                               int lda, const float* b, int ldb, float beta, float* c, int ldc);
+
+void oracle_conv2d_sgemm(const float* in, const float* kernel_r, float* out, int batch, int oh, int ow, int od,
+                         int ih, int iw, int ic, int kh, int kw, int sh, int sw, void* sgemm) {
+  const int K = ic * kh * kw, M = oh * ow;
+  float* col = (float*)malloc((size_t)M * K * sizeof(float));
+  for (int b = 0; b < batch; ++b) {
+    oracle_im2col(in + (size_t)b * ih * iw * ic, col, oh, ow, ih, iw, ic, kh, kw, sh, sw);
+    ((cblas_sgemm_fn)sgemm)(101 /* RowMajor */, 111 /* NoTrans */, 111, M, od, K, 1.0f, col, K, kernel_r, od, 0.0f,
+                            out + (size_t)b * M * od, od);
+  }
+  free(col);
+}
+
 /* ---- AVX-engine-equivalent direct conv (proj3/dnn_avx.c:33-126): output rows split over
  * nthreads pthreads (P_THREADS = 4 in the reference, dnn_avx.c:13), accumulation order
  * (c, di, dj) per output pixel, vectorisable over od. */

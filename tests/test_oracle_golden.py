@@ -112,6 +112,18 @@ def test_whole_net_numpy_vs_golden(golden_frames, yolo_weights, frame):
     assert err < 1e-5, err
 
 
+def test_openblas_engine_ctypes_vs_golden(golden_frames, yolo_weights, oc):
+    """BASELINE config 1 (the bench's cpu_baseline value): the OpenBLAS engine's per-node C
+    calls with conv2d_mul = im2col + OpenBLAS cblas_sgemm, one frame, vs the reference golden."""
+    import oracle_c
+    sg = oracle_c.openblas_sgemm()
+    if sg is None:
+        pytest.skip("no OpenBLAS build to bind")
+    y = oracle_c.yolo_forward_openblas(oc, yolo_weights, synth.frame(0), sg[0])
+    assert y.shape == (1, 13, 13, 125)
+    assert R.normwise_err(y, golden_frames[0]) < 1e-5
+
+
 def test_node_stats_vs_golden(yolo_weights):
     import os
     from conftest import GOLDEN
