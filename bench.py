@@ -171,18 +171,20 @@ def cpu_baseline(seconds):
     return res
 
 
-def latency_b1(dnn_hip, yolo_graph, ws, dev, iters=200):
+def latency_b1(dnn_hip, yolo_graph, ws, dev, iters=200, latency=True):
     """BASELINE.json configs[1]: one 416x416 frame, fp32, 1 GPU — issue-to-completion time of a
-    single-frame forward (frame resident in HBM), eager (13 launches) and as one HIP-graph
-    launch (dnn_plan_run_graph), median over `iters` synchronised runs."""
+    single-frame forward (frame resident in HBM), eager (one launch per kernel) and as one
+    HIP-graph launch (dnn_plan_run_graph), median over `iters` synchronised runs.  latency=True:
+    the latency plan (dnn_plan_set_latency_mode: conv4-conv8 K-split over the chip); False: the
+    batch plan's choices at batch 1 (bit-equal to a batch-64 row)."""
     import torch
     g1, _ = yolo_graph.build_graph(dnn_hip.DnnGraphBuilder, ws, in_shape=(1, 416, 416, 3))
     entries = dnn_hip.lower_graph(g1)
-    wb, sb = dnn_hip.Plan.memory(1, (416, 416, 3), entries)
+    wb, sb = dnn_hip.Plan.memory(1, (416, 416, 3), entries, latency=latency)
     wbuf = torch.empty(wb, dtype=torch.uint8, device=dev)
     sbuf = torch.empty(max(sb, 1), dtype=torch.uint8, device=dev)
     p1 = dnn_hip.Plan(1, (416, 416, 3), entries, device=dev.index, weights_ptr=wbuf.data_ptr(),
-                      workspace_ptr=sbuf.data_ptr())
+                      workspace_ptr=sbuf.data_ptr(), latency=latency)
     x = torch.rand((1, 416, 416, 3), device=dev)
     y = torch.empty((1, 13, 13, 125), device=dev)
     s = torch.cuda.Stream(dev)
@@ -215,9 +217,23 @@ def latency_b1(dnn_hip, yolo_graph, ws, dev, iters=200):
         p1.run_device(1, x.data_ptr(), y.data_ptr(), sp)
     ms, cnt = p1.timing_end()
     out["kernel_ms"] = {k["name"]: round(m / max(c, 1), 4) for k, m, c in zip(p1.kernels(), ms, cnt)}
+    out["plan"] = "latency (K splits chosen for M = 169)" if latency else "batch rules (bit-equal to batch-64 rows)"
     out["note"] = "median issue-to-completion wall time of one synchronised single-frame forward"
+    if latency:  # the same frame through this plan vs the batch plan's result: fp32 tolerance
+        xb = synth_frame_dev(dev)
+        yl = torch.empty((1, 13, 13, 125), device=dev)
+        p1.run_device(1, xb.data_ptr(), yl.data_ptr(), sp)
+        torch.cuda.synchronize()
+        out["_y"] = yl
+        out["_x"] = xb
     p1.close()
     return out
+
+
+def synth_frame_dev(dev):
+    import synth
+    import torch
+    return torch.from_numpy(synth.frame(0)).to(dev)
 
 
 def end_to_end(plan, B, dev, stream, steps=10, hw=(480, 640)):
@@ -579,7 +595,15 @@ def main():
                               for n, v in by_name.items()}
 
     if rank == 0 and world == 1 and not args.no_latency:
-        res["latency_b1"] = latency_b1(dnn_hip, yolo_graph, ws, dev)
+        lat = latency_b1(dnn_hip, yolo_graph, ws, dev)
+        inv = latency_b1(dnn_hip, yolo_graph, ws, dev, latency=False)
+        yb = torch.empty((B, 13, 13, 125), device=dev)
+        plan.run_device(1, lat["_x"].data_ptr(), yb.data_ptr(), stream)
+        torch.cuda.synchronize()
+        lat["normwise_err_vs_batch_plan"] = float((lat.pop("_y") - yb[:1]).abs().max() / yb[:1].abs().max())
+        lat.pop("_x")
+        lat["batch_plan_at_batch1"] = inv
+        res["latency_b1"] = lat
     if rank == 0 and world == 1 and not args.no_e2e:
         res["end_to_end_host_frames"] = end_to_end(plan, B, dev, stream)
     if rank == 0 and world == 1 and args.precision == "fp32" and not args.no_unfused:

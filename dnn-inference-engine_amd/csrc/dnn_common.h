@@ -90,7 +90,8 @@ enum GemmCfg : int {
   GEMM_64x128_NS3 = 11,  // experiment: 64x128 with a 3-stage ring
   GEMM_G256x128_W8 = 12, // experiment (N % 128 == 0): 256x128, 8 waves of 64x64, 96 KB (1 per CU)
   GEMM_G192x128_W8 = 13, // unsplit long-K N % 128 == 0 layers filling one round (conv4): 192x128, 8 waves of 96x32
-  GEMM_NUM_CFGS = 14,
+  GEMM_G192x64_W4 = 14,  // latency plans, M <= 192 (one frame's 169 rows in one tile), N % 64 == 0: 4 waves of 96x32
+  GEMM_NUM_CFGS = 15,
 };
 int gemm_cfg_bm(int cfg);
 int gemm_cfg_bn(int cfg);
@@ -127,6 +128,10 @@ int launch_im2col_ckk(const float* in, float* col, const ConvGeom& g, hipStream_
 // [splits][M][N] to `slab` and NO epilogue; launch_splitk_reduce then sums them in split order
 // and applies the epilogue into C.  choose_splitk depends on (N, K) only.
 int choose_splitk(int N, int K, bool combine = false);
+// Latency plans (dnn_plan_set_latency_mode): tile config and split count of a small-M layer so
+// that its work units fill the chip (depends on M: batch-1 results are not bit-equal to a
+// batch plan's rows).  In: the batch rule's (cfg, splits); kept when they fill the chip.
+void choose_latency_plan(long long M, int N, int K, int* cfg, int* splits);
 // With `tickets` (>= the cfg's tile count of unsigned, zero before the first launch and left
 // zero by every launch) the split-K GEMM finishes itself: the last-arriving split of each tile
 // sums the partials in split order and writes C with the epilogue (splitk_combine, gemm_f32.h),

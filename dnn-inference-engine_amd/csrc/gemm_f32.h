@@ -541,6 +541,88 @@ __device__ __forceinline__ void splitk_combine(typename Mfma<MF>::acc_t (&acc)[T
   }
 }
 
+// Fused split-K combine for any split count (latency plans: 2..32 splits of a small-M layer)
+// and for the pool-fused mode: the same hand-off as splitk_combine (write-through raw partial
+// in the accumulator-native layout, drain, barrier, agent-scope ticket, acquire by the last
+// split), but the last split only SUMS the partials in split order ((p0 + p1) + p2) + ... into
+// its own accumulators and returns true; the caller then runs its normal store path (plain or
+// pool-then-epilogue) with the real epilogue.  Returns false in every other split.
+template <int MF, int TM, int TN, int NW>
+__device__ __forceinline__ bool splitk_sum(typename Mfma<MF>::acc_t (&acc)[TM][TN], float* __restrict__ slab,
+                                           const SplitK& sk, int s, int tile, int wid, int lane, unsigned* lds_word) {
+  typedef Mfma<MF> MM;
+  constexpr int Q = MM::REGS / 4;
+  constexpr long long TILE_F = (long long)NW * TM * TN * Q * 256;  // = BM * BN
+  const int S = sk.splits;
+  const unsigned slab_bytes = (unsigned)((long long)S * sk.ntile * TILE_F * 4);
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(slab, 0, (int)slab_bytes, 0x00020000);
+  auto idx = [&](int i, int j, int q) { return ((((wid * TM + i) * TN + j) * Q + q) * 64 + lane) * 4; };
+  const long long own = ((long long)s * sk.ntile + tile) * TILE_F;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        const f32x4 v = {acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]};
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs,
+                                               (unsigned)((own + idx(i, j, q)) * 4), 0, 16 /* sc1 */);
+      }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // EVERY storing wave drains
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned t = __hip_atomic_fetch_add(sk.tickets + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned last = t == (unsigned)(S - 1) ? 1u : 0u;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      __hip_atomic_store(sk.tickets + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    *lds_word = last;
+  }
+  __syncthreads();
+  if (!*lds_word) return false;
+  // partials of up to 8 splits in flight at once (uniform branches, no wait between the
+  // loads), then added in split order
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      f32x4 own_v[Q], v[Q];
+#pragma unroll
+      for (int q = 0; q < Q; ++q)
+        own_v[q] = f32x4{acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]};
+      for (int s0 = 0; s0 < S; s0 += 8) {
+        f32x4 p[8][Q];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int ss = s0 + u;
+          if (ss < S && ss != s) {
+            const float* src = slab + ((long long)ss * sk.ntile + tile) * TILE_F;
+#pragma unroll
+            for (int q = 0; q < Q; ++q) p[u][q] = *reinterpret_cast<const f32x4*>(src + idx(i, j, q));
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int ss = s0 + u;
+          if (ss < S) {
+#pragma unroll
+            for (int q = 0; q < Q; ++q) {
+              const f32x4 x = ss == s ? own_v[q] : p[u][q];
+              v[q] = ss == 0 ? x : v[q] + x;
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < Q; ++q)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[i][j][4 * q + e] = v[q][e];
+    }
+  return true;
+}
+
 // Buffer-resource addressing of the LDS-DMA sources (ABUF kernels): A and Bt are read by
 // buffer_load ... lds with a per-lane 32-bit byte offset fixed for the whole tile (voffset) and
 // the K-step's position as a wave-uniform soffset, so a DMA costs no 64-bit address arithmetic;
@@ -780,11 +862,19 @@ gemm_f32_glds_kernel(const float* __restrict__ A, int lda, const float* __restri
     wait_lgkm0();
     stage = stage + 1 == NS ? 0 : stage + 1;
   }
+  if (sk.steps > 0 && sk.tickets && (MODE == 2 || sk.splits > 3)) {
+    // latency plans (any split count) and pool-fused split layers: the last split sums, then
+    // the normal store path below runs with the real epilogue
+    if (!splitk_sum<MF, TM, TN, NW>(acc, C, sk, split, tile, wid, lane, reinterpret_cast<unsigned*>(smem))) return;
+    epi.flags = sk.flags;
+    C = sk.out;
+    ldc = sk.ldo;
+  }
   if constexpr (MODE == 2) {
     store_tile_pool<MF, TM, TN, WTM, WTN>(acc, C, ldc, M, N, m0, n0, wm, wn, lane, epi, ic);
   } else {
-    if (sk.steps > 0 && sk.tickets) {
-      // the launcher admits splits 2..3 only (choose_splitk gives 3)
+    if (sk.steps > 0 && sk.tickets && sk.splits <= 3) {
+      // batch plans: 3 splits (choose_splitk), partials loaded all at once
       if (sk.splits == 3)
         splitk_combine<3, MF, TM, TN, WTM, WTN, NW>(acc, C, sk, split, tile, M, N, m0, n0, wm, wn, wid, lane, epi,
                                                     reinterpret_cast<unsigned*>(smem));

@@ -178,7 +178,7 @@ struct CfgInfo {
 static const CfgInfo kCfgs[GEMM_NUM_CFGS] = {{256, 16, 32}, {256, 32, 16}, {128, 64, 32}, {128, 128, 32},
                                              {64, 128, 32},  {64, 32, 32},  {256, 64, 32}, {32, 128, 32},
                                              {32, 64, 32},   {128, 256, 32}, {128, 512, 32}, {64, 128, 32},
-                                             {256, 128, 32}, {192, 128, 32}};
+                                             {256, 128, 32}, {192, 128, 32}, {192, 64, 32}};
 
 int gemm_cfg_bm(int cfg) { return kCfgs[cfg].bm; }
 int gemm_cfg_bn(int cfg) { return kCfgs[cfg].bn; }
@@ -271,6 +271,54 @@ int choose_splitk(int N, int K, bool combine) {
   return 1;
 }
 
+// Latency plans.  When the batch rule's (cfg, splits) leaves the chip under 90 % occupied
+// (DNN_HIP_LAT_UNITS work units, default 256 = one per CU), every candidate tile config --
+// the batch rule's, 32x64 for N <= 128, and (DNN_HIP_LAT_CAND bit 2) 192x64 when M <= 192 --
+// is tried with every split S <= 32 that divides its K-steps into parts of at least
+// DNN_HIP_LAT_MINSTEPS (default 6); the pick maximises the balance
+// units / (256 * ceil(units / 256)), then prefers fewer splits (less partial traffic in the
+// combine), then fewer units.  Batch 1 of YOLOv2-tiny: conv6/conv7 -> 32x128 x 16 splits (768
+// units), conv5 -> x 9, conv4 -> x 4, conv3 -> x 3, conv8 -> 32x64 x 4 (tools/lat_cfg_sweep_job.sh:
+// every tile/split choice of conv7 lands within 0.050-0.060 ms; the split-K combine's chain of
+// memory round trips costs ~5 us per layer).
+void choose_latency_plan(long long M, int N, int K, int* cfg, int* splits) {
+  if (*cfg < GEMM_128x128_K32) return;
+  const char* e = getenv("DNN_HIP_LAT_UNITS");
+  const long long target = e && atoi(e) > 0 ? atoi(e) : 256;
+  const char* ms = getenv("DNN_HIP_LAT_MINSTEPS");
+  const int minsteps = ms && atoi(ms) > 0 ? atoi(ms) : 6;
+  if (splitk_tiles(*cfg, M, N) * *splits * 10 >= target * 9) return;
+  // DNN_HIP_LAT_CAND (experiments): bit mask of the candidates tried; default 5 = the batch
+  // rule's config and 32x64 (192x64 measured slower at batch 1: conv7 0.060 vs 0.051 ms)
+  const char* ce = getenv("DNN_HIP_LAT_CAND");
+  const int cmask = ce && atoi(ce) > 0 ? atoi(ce) : 5;
+  int cand[3] = {(cmask & 1) ? *cfg : -1, -1, -1};
+  if ((cmask & 2) && M <= 192 && N % 64 == 0) cand[1] = GEMM_G192x64_W4;
+  if ((cmask & 4) && N <= 128) cand[2] = GEMM_G32x64_NS4;
+  double best_eff = -1.0;
+  long long best_units = 0;
+  int best_cfg = *cfg, best_s = *splits;
+  for (int c : cand) {
+    if (c < 0 || K % kCfgs[c].bk != 0) continue;
+    const int nk = K / kCfgs[c].bk;
+    const long long tiles = splitk_tiles(c, M, N);
+    for (int sp = 1; sp <= 32; ++sp) {
+      if (nk % sp != 0 || (sp > 1 && nk / sp < minsteps)) continue;
+      const long long units = tiles * sp;
+      const double eff = (double)units / (double)(target * ((units + target - 1) / target));
+      if (eff > best_eff + 1e-9 ||
+          (eff > best_eff - 1e-9 && (sp < best_s || (sp == best_s && units < best_units)))) {
+        best_eff = eff;
+        best_units = units;
+        best_cfg = c;
+        best_s = sp;
+      }
+    }
+  }
+  *cfg = best_cfg;
+  *splits = best_s;
+}
+
 // LDS-DMA configs for one A mode (dense / implicit / implicit + pool); `abuf`: buffer-resource
 // addressed DMA (BufDesc, gemm_f32.h), else flat 64-bit addresses
 template <int MODE, bool ABUF>
@@ -292,6 +340,7 @@ static int launch_glds_t(int cfg, const float* A, int lda, const float* Bt, int 
     case GEMM_64x128_NS3: DNN_GLDS(64, 128, 2, 2, 32, 3); break;
     case GEMM_G256x128_W8: DNN_GLDS(256, 128, 4, 2, 32, 2); break;
     case GEMM_G192x128_W8: DNN_GLDS(192, 128, 2, 4, 32, 2); break;
+    case GEMM_G192x64_W4: DNN_GLDS(192, 64, 2, 2, 32, 3); break;
     default:
       set_error("gemm: cfg %d is not an LDS-DMA config", cfg);
       return -2;
@@ -338,8 +387,8 @@ static int split_setup(int cfg, long long M, int N, int Kpad, int splits, float*
     }
     *sk = SplitK{Kpad / 32 / splits, *grid, M * (long long)N};
     if (tickets) {
-      if (splits > 3) {
-        set_error("gemm: fused split-K combine supports 2 or 3 splits (got %d)", splits);
+      if (splits > 32) {
+        set_error("gemm: fused split-K combine supports 2..32 splits (got %d)", splits);
         return -2;
       }
       if (splitk_fused_slab_floats(cfg, M, N, splits) * 4 >= 0x80000000LL) {
@@ -411,7 +460,7 @@ int launch_gemm_implicit(int cfg, int mode, const float* in, const ImplicitConv&
   }
   const CfgInfo ci = kCfgs[cfg];
   if (Kpad % ci.bk != 0 || !implicit_conv_supported(ic.C, ic.kh, ic.kw) || M > 0x7fffffffLL || !ic.zero ||
-      (mode == GEMM_IMPLICIT_POOL && (M % 4 != 0 || splits > 1))) {
+      (mode == GEMM_IMPLICIT_POOL && (M % 4 != 0 || (splits > 1 && !tickets)))) {
     set_error("gemm_implicit: unsupported shape M=%lld C=%d Kpad=%d splits=%d", M, ic.C, Kpad, splits);
     return -2;
   }

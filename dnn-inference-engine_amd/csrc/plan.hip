@@ -121,6 +121,7 @@ struct dnn_plan {
   bool patch = true;
   bool splitk_fused = true;  // fp32 split-K layers combine in the GEMM (no reduce kernel)
   int fp16 = 0;  // 1: fp16 activations/weights, fp16 MFMA, fp32 accumulate + epilogue
+  bool latency = false;  // split K by M too (dnn_plan_set_latency_mode): batch-1 latency plans
   std::vector<PlanLayer> layers;
   std::vector<KernelDesc> kernels;
   int device = -1;
@@ -195,10 +196,11 @@ static void layout(dnn_plan* p) {
         ++nconv;
       }
       if (L.splits > 1 && fused_splitk(p)) {  // partials combined by the GEMM's last-arriving split
-        slab_fused = std::max(slab_fused, (size_t)(p->fp16 ? splitk16_fused_slab_floats(L.cfg, (long long)M, L.OC, L.splits)
-                                                           : splitk_fused_slab_floats(L.cfg, (long long)M, L.OC, L.splits)));
-        tickets = std::max(tickets, (size_t)(p->fp16 ? splitk16_tiles(L.cfg, (long long)M, L.OC)
-                                                     : splitk_tiles(L.cfg, (long long)M, L.OC)));
+        const long long Mg = L.pool ? 4LL * p->batch * L.PH * L.PW : (long long)M;  // the GEMM's rows
+        slab_fused = std::max(slab_fused, (size_t)(p->fp16 ? splitk16_fused_slab_floats(L.cfg, Mg, L.OC, L.splits)
+                                                           : splitk_fused_slab_floats(L.cfg, Mg, L.OC, L.splits)));
+        tickets = std::max(tickets, (size_t)(p->fp16 ? splitk16_tiles(L.cfg, Mg, L.OC)
+                                                     : splitk_tiles(L.cfg, Mg, L.OC)));
         if (p->fp16 && L.cfg == GEMM16_128x512_W16)  // the launcher's 128x128 fallback has more tiles
           tickets = std::max(tickets, (size_t)splitk16_tiles(GEMM16_128x128, (long long)M, L.OC));
       } else if (L.splits > 1) {  // partials written by the GEMM, summed + epilogue by the reduce kernel
@@ -291,12 +293,37 @@ static void set_cfg(dnn_plan* p, PlanLayer& L) {
   L.Kpad = (int)align_up(L.K, gemm_cfg_bk(L.cfg));
   L.Npad = (int)align_up(L.OC, gemm_cfg_bn(L.cfg));
   L.splits = (L.cfg >= GEMM_128x128_K32 && L.Kpad == L.K) ? choose_splitk(L.OC, L.K, fused_splitk(p)) : 1;
+  if (p->latency && fused_splitk(p) && L.Kpad == L.K) {
+    // a tile config and split for this M when the batch rule leaves the chip idle
+    int cfg = L.cfg, sp = L.splits;
+    choose_latency_plan(M, L.OC, L.K, &cfg, &sp);
+    if (const char* e = getenv("DNN_HIP_SPLIT")) {  // tuning experiments: "K:splits,..."
+      for (const char* q = e; *q;) {
+        int k = 0, v = 0, n = 0;
+        if (sscanf(q, "%d:%d%n", &k, &v, &n) != 2) break;
+        if (k == L.K && v >= 1 && v <= 32 && (L.Kpad / gemm_cfg_bk(cfg)) % v == 0 && cfg >= GEMM_128x128_K32) sp = v;
+        q += n;
+        if (*q == ',') ++q;
+      }
+    }
+    L.cfg = cfg;
+    L.splits = sp;
+    L.Npad = (int)align_up(L.OC, gemm_cfg_bn(L.cfg));
+  }
 }
 
 int dnn_plan_set_precision(dnn_plan* p, int precision) {
   DNN_REQUIRE(p && !p->finalized && p->layers.empty(), "dnn_plan_set_precision: call before adding layers");
   DNN_REQUIRE(precision == 0 || precision == 1, "dnn_plan_set_precision: precision must be 0 (fp32) or 1 (fp16)");
   p->fp16 = precision;
+  return 0;
+}
+
+int dnn_plan_set_latency_mode(dnn_plan* p, int on) {
+  DNN_REQUIRE(p && !p->finalized && p->layers.empty(), "dnn_plan_set_latency_mode: call before adding layers");
+  DNN_REQUIRE(on == 0 || on == 1, "dnn_plan_set_latency_mode: on must be 0 or 1");
+  DNN_REQUIRE(!on || !p->fp16, "dnn_plan_set_latency_mode: fp32 plans only");
+  p->latency = on != 0;
   return 0;
 }
 
@@ -384,11 +411,13 @@ int dnn_plan_add_max_pool(dnn_plan* p, int kh, int kw, int stride_h, int stride_
   if (p->fuse && !p->layers.empty() && kh == 2 && kw == 2 && stride_h == 2 && stride_w == 2 && L.pt == 0 &&
       L.pl == 0) {
     PlanLayer& prev = p->layers.back();
-    if (prev.type == 0 && !prev.pool && prev.splits == 1) {
+    // (latency plans: a split implicit conv keeps its split, the combine pools)
+    if (prev.type == 0 && !prev.pool &&
+        (prev.splits == 1 || (prev.mode == MODE_IMPLICIT && !p->fp16 && fused_splitk(p)))) {
       bool ok = false;
       if (prev.mode == MODE_IMPLICIT) {
         ok = true;
-        if (!p->fp16 && p->patch && patch_conv_pool_supported(prev.C, prev.OC, prev.H, prev.W, prev.OH, prev.OW, prev.kh, prev.kw,
+        if (!p->fp16 && p->patch && prev.splits == 1 && patch_conv_pool_supported(prev.C, prev.OC, prev.H, prev.W, prev.OH, prev.OW, prev.kh, prev.kw,
                                                   prev.sh, prev.sw, prev.pt, prev.pl) &&
             prev.Kpad == patch_conv_kpad(prev.C))
           prev.mode = MODE_PATCH;  // same packed weights (Bt[Npad][Kpad]) as the implicit GEMM
@@ -758,12 +787,14 @@ int dnn_plan_describe(const dnn_plan* p, char* buf, int buf_len) {
   char line[256];
   for (size_t i = 0; i < p->layers.size(); ++i) {
     const PlanLayer& L = p->layers[i];
-    if (L.type == 0)
-      snprintf(line, sizeof(line), "conv %dx%dx%d -> %dx%dx%d k%dx%d s%d mode=%s cfg=%d K=%d Kpad=%d%s%s%s%s\n", L.H,
+    if (L.type == 0) {
+      char sk[32] = "";
+      if (L.splits > 1) snprintf(sk, sizeof(sk), " splitK=%d", L.splits);
+      snprintf(line, sizeof(line), "conv %dx%dx%d -> %dx%dx%d k%dx%d s%d mode=%s cfg=%d K=%d Kpad=%d%s%s%s%s%s\n", L.H,
                L.W, L.C, L.out_h(), L.out_w(), L.OC, L.kh, L.kw, L.sh, kModeName[L.mode], L.cfg, L.K, L.Kpad,
-               L.pool ? " +pool2x2s2" : "", L.splits > 1 ? (L.splits == 3 ? " splitK=3" : " splitK") : "",
-               L.splits > 1 && fused_splitk(p) ? " combine" : "", p->fp16 ? " fp16" : "");
-    else
+               L.pool ? " +pool2x2s2" : "", sk, L.splits > 1 && fused_splitk(p) ? " combine" : "",
+               p->fp16 ? " fp16" : "", p->latency ? " latency" : "");
+    } else
       snprintf(line, sizeof(line), "pool %dx%dx%d -> %dx%dx%d k%dx%d s%d%s\n", L.H, L.W, L.C, L.OH, L.OW, L.OC, L.kh,
                L.kw, L.sh, p->fp16 ? " fp16" : "");
     s += line;

@@ -65,6 +65,7 @@ def _bind_plan_api(lib):
         "dnn_plan_run_host": (i, [vp, i, vp, vp]),
         "dnn_plan_run_graph": (i, [vp, i, vp, vp, vp]),
         "dnn_plan_set_precision": (i, [vp, i]),
+        "dnn_plan_set_latency_mode": (i, [vp, i]),
         "dnn_plan_num_kernels": (i, [vp]),
         "dnn_plan_kernel_info": (i, [vp, i, ctypes.c_char_p, i, P(ctypes.c_double), P(ctypes.c_double)]),
         "dnn_plan_timing_begin": (i, [vp, i]),
@@ -141,12 +142,15 @@ def _precision(p):
 class DnnInferenceEngine(object):
     """proj3/dnn_openblas.py:23-57.  `device` picks the GPU (default $DNN_HIP_DEVICE or 0);
     `precision` "fp32" (default, the reference's arithmetic) or "fp16" (fp16 MFMA conv path,
-    BASELINE config 5; default from $DNN_HIP_PRECISION)."""
+    BASELINE config 5; default from $DNN_HIP_PRECISION); `latency` True (default
+    $DNN_HIP_LATENCY=1) builds a latency plan (dnn_plan_set_latency_mode: K splits chosen for
+    the graph's batch, for single-frame inference as proj3/__init__.py:24-26 runs it)."""
 
-    def __init__(self, graph, debug, device=None, precision=None):
+    def __init__(self, graph, debug, device=None, precision=None, latency=None):
         self.g = graph
         self.debug = debug
         self.precision = _precision(precision)
+        self.latency = os.environ.get("DNN_HIP_LATENCY") == "1" if latency is None else bool(latency)
         self.device = int(os.environ.get("DNN_HIP_DEVICE", "0")) if device is None else device
         self.save_dir = os.path.join(os.getcwd(), "intermediate")
         self._plan = None
@@ -156,7 +160,8 @@ class DnnInferenceEngine(object):
     def plan(self):
         """The lowered plan (built on first use; weights uploaded once)."""
         if self._plan is None:
-            self._plan = Plan.from_graph(self.g, device=self.device, precision=self.precision)
+            self._plan = Plan.from_graph(self.g, device=self.device, precision=self.precision,
+                                         latency=self.latency)
         return self._plan
 
     def run(self, tin):
@@ -506,7 +511,7 @@ class Plan(object):
     """Owner of a dnn_plan handle (include/dnn_hip_plan.h)."""
 
     def __init__(self, batch, in_shape, entries, device=0, weights_ptr=None, workspace_ptr=None, upload=True,
-                 leaky_variant=1, lib=None, precision="fp32"):
+                 leaky_variant=1, lib=None, precision="fp32", latency=False):
         self.lib = lib or mylib
         self.batch = int(batch)
         self.in_shape = tuple(int(v) for v in in_shape)
@@ -516,6 +521,9 @@ class Plan(object):
         self.h = h
         _check(self.lib.dnn_plan_set_precision(self.h, PRECISIONS[self.precision]), "dnn_plan_set_precision",
                self.lib)
+        self.latency = bool(latency)
+        if self.latency:
+            _check(self.lib.dnn_plan_set_latency_mode(self.h, 1), "dnn_plan_set_latency_mode", self.lib)
         self.entries = entries
         for e in entries:
             if isinstance(e, ConvEntry):
@@ -555,13 +563,15 @@ class Plan(object):
         return cls(g.in_node.in_shape[0], tuple(g.in_node.in_shape[1:]), entries, device=device, **kw)
 
     @staticmethod
-    def memory(batch, in_shape, entries, lib=None, precision="fp32"):
+    def memory(batch, in_shape, entries, lib=None, precision="fp32", latency=False):
         """(weight_bytes, workspace_bytes) a plan of this shape needs, without finalizing."""
         lib = lib or mylib
         h = ctypes.c_void_p()
         _check(lib.dnn_plan_create(int(batch), *in_shape, ctypes.byref(h)), "dnn_plan_create", lib)
         try:
             _check(lib.dnn_plan_set_precision(h, PRECISIONS[_precision(precision)]), "dnn_plan_set_precision", lib)
+            if latency:
+                _check(lib.dnn_plan_set_latency_mode(h, 1), "dnn_plan_set_latency_mode", lib)
             for e in entries:
                 if isinstance(e, ConvEntry):
                     kh, kw, _, od = e.conv.kernel.shape

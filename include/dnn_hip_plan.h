@@ -45,6 +45,14 @@ void dnn_plan_destroy(dnn_plan* plan);
  * 3x3 first conv followed by a 2x2/s2 pool; tolerance vs fp32: DESIGN.md. */
 int dnn_plan_set_precision(dnn_plan* plan, int precision);
 
+/* Latency mode (call before adding layers; fp32 plans): on = 1 lets the K split of a GEMM
+ * layer depend on M, so a small-M forward (one frame: BASELINE config 2, the single timed
+ * frame of proj3/__init__.py:24-26) spreads conv4-conv8 over the whole chip (2..16 K splits,
+ * combined in split order inside the GEMM).  Outputs stay within the fp32 tolerance of the
+ * reference but are no longer bit-equal to the same frame's row of a batch plan (whose
+ * summation order depends on (N, K) only).  Default 0. */
+int dnn_plan_set_latency_mode(dnn_plan* plan, int on);
+
 /* Append a Conv2D (proj3/dnn_openblas.py:144-188) with its trailing BiasAdd / BatchNorm /
  * LeakyReLU fused.  kernel: [kh][kw][in_c][od] HWIO.  biases may be NULL (no BiasAdd);
  * mean/var/gamma all NULL means no BatchNorm (else all three, eps as in

@@ -243,3 +243,73 @@ def test_weight_pickle_round_trip_and_safety(tmp_path):
     del bad[2]["gamma"]
     with pytest.raises(YW.WeightFileError):
         YW.validate(bad)
+
+
+def _describe_yolo(batch, latency, env=None):
+    """Plan layout of YOLOv2-tiny at `batch` (shapes only, no GPU): describe() lines."""
+    import synth
+    import yolo_graph
+    old = {k: os.environ.get(k) for k in (env or {})}
+    os.environ.update(env or {})
+    try:
+        g, _ = yolo_graph.build_graph(dnn_hip.DnnGraphBuilder, synth.yolo_zero_weights(),
+                                      in_shape=(batch, 416, 416, 3))
+        lib = dnn_hip.mylib
+        h = ctypes.c_void_p()
+        assert lib.dnn_plan_create(batch, 416, 416, 3, ctypes.byref(h)) == 0
+        try:
+            assert lib.dnn_plan_set_latency_mode(h, 1 if latency else 0) == 0
+            for e in dnn_hip.lower_graph(g):
+                if isinstance(e, dnn_hip.ConvEntry):
+                    kh, kw, _, od = e.conv.kernel.shape
+                    assert lib.dnn_plan_add_conv(h, kh, kw, od, 1, 1, 1, None, None, None, None, None, 0.0, 1) == 0
+                else:
+                    assert lib.dnn_plan_add_max_pool(h, 2, 2, e.pool.strides[1], e.pool.strides[2], 1) == 0
+            buf = ctypes.create_string_buffer(8192)
+            assert lib.dnn_plan_describe(h, buf, 8192) == 0
+            return buf.value.decode().splitlines()
+        finally:
+            lib.dnn_plan_destroy(h)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+def test_latency_plan_layout():
+    """dnn_plan_set_latency_mode: at batch 1 conv4-conv8 split K (combined in the GEMM, conv4
+    with its pool), conv0/conv1 keep their direct/patch kernels; batch plans are unchanged."""
+    lat = _describe_yolo(1, True)
+    base = _describe_yolo(1, False)
+    assert all(l.endswith(" latency") for l in lat if l.startswith("conv"))
+    conv = [l for l in lat if l.startswith("conv")]
+    assert "mode=direct" in conv[0] and "mode=patch" in conv[1]
+    for i in (4, 5, 6, 7, 8):
+        assert " splitK=" in conv[i] and " combine" in conv[i], conv[i]
+    assert "+pool2x2s2" in conv[4]
+    # the batch plan at batch 1: only the (N, K) rule's 3 splits of conv5-conv7
+    assert [l for l in base if " splitK=" in l] == [l for l in base if " splitK=3 " in l] and \
+        sum(" splitK=3 " in l for l in base) == 3
+    assert sum(" splitK=16 " in l for l in conv) == 2  # conv6/conv7 at batch 1: 48 tiles x 16
+    # batch 64: latency mode leaves the (N, K)-only rule in charge of every layer that fills the chip
+    assert [l.replace(" latency", "") for l in _describe_yolo(64, True)] == _describe_yolo(64, False)
+    # without the in-GEMM combine (DNN_HIP_SPLITK_FUSED=0) latency mode adds no split
+    assert [l.replace(" latency", "") for l in _describe_yolo(1, True, {"DNN_HIP_SPLITK_FUSED": "0"})] == \
+        _describe_yolo(1, False, {"DNN_HIP_SPLITK_FUSED": "0"})
+
+
+def test_latency_mode_errors():
+    lib = dnn_hip.mylib
+    h = ctypes.c_void_p()
+    assert lib.dnn_plan_create(1, 8, 8, 32, ctypes.byref(h)) == 0
+    try:
+        assert lib.dnn_plan_set_latency_mode(h, 2) != 0
+        assert lib.dnn_plan_set_precision(h, 1) == 0
+        assert lib.dnn_plan_set_latency_mode(h, 1) != 0  # fp32 plans only
+        assert lib.dnn_plan_set_precision(h, 0) == 0
+        assert lib.dnn_plan_add_conv(h, 3, 3, 64, 1, 1, 1, None, None, None, None, None, 0.0, 1) == 0
+        assert lib.dnn_plan_set_latency_mode(h, 1) != 0  # after a layer
+    finally:
+        lib.dnn_plan_destroy(h)

@@ -791,3 +791,63 @@ def test_frame_ingest_reuse_ordered_without_release():
         for b, o in zip(batches, outs):
             ref = np.stack([IN.resize_input(f) for f in b])
             assert np.array_equal(o.cpu().numpy(), ref)
+
+
+# ------------------------------------------------------------------ latency plans (config 2)
+LAT_CASES = [
+    # B, H, W, C, od, kernel, pool, forced split (DNN_HIP_SPLIT) or None
+    (1, 26, 26, 128, 256, 3, (2, 2, "SAME"), None),   # conv4 at batch 1: split + pool in the combine
+    (1, 13, 13, 128, 256, 3, (2, 2, "SAME"), None),   # odd 13x13 -> 7x7 pool (ragged windows)
+    (1, 13, 13, 1024, 1024, 3, None, None),           # conv7 at batch 1
+    (1, 13, 13, 1024, 125, 1, None, None),            # conv8: 1x1, N = 125 (not a multiple of 4)
+    (1, 13, 13, 512, 512, 3, None, 16),               # 16 splits (the most the combine takes)
+    (2, 9, 11, 256, 384, 3, (2, 2, "VALID"), 9),      # M = 2*4*4*5 pooled rows, 9 splits
+]
+
+
+@pytest.mark.parametrize("case", LAT_CASES)
+def test_latency_split_combine_vs_oracle(monkeypatch, case):
+    """Latency plans split K by M (2..16 splits, the last split sums the partials in split
+    order inside the GEMM, gemm_f32.h splitk_sum, then its normal or pool-fused store): within
+    the layer tolerance of the float64 oracle, identical across runs and HIP-graph replays."""
+    B, H, W, C, od, kk, pool, force = case
+    if force:
+        monkeypatch.setenv("DNN_HIP_SPLIT", f"{kk * kk * C}:{force}")
+    rng = np.random.default_rng(B + C + od + kk)
+    x = rng.standard_normal((B, H, W, C)).astype(np.float32)
+    k = (rng.standard_normal((kk, kk, C, od)) * np.sqrt(2.0 / (kk * kk * C))).astype(np.float32)
+    bias = rng.standard_normal(od).astype(np.float32) * 0.1
+    gam = rng.uniform(0.5, 1.5, od).astype(np.float32)
+    gam[::5] *= -1
+    bn = (rng.standard_normal(od).astype(np.float32) * 0.1, rng.uniform(0.5, 1.5, od).astype(np.float32), gam)
+    kw = dict(bias=bias, bn=bn, leaky=True, pool=pool)
+    eng = dnn_hip.DnnInferenceEngine(_chain(x.shape, k, **kw), False, latency=True)
+    desc = eng.plan().describe()
+    want = f" splitK={force} combine" if force else " combine"
+    assert want in desc and " latency" in desc, desc
+    y1 = eng.run(x)
+    y2 = eng.run(x)
+    assert np.array_equal(y1, y2)
+    assert R.normwise_err(y1, _oracle_chain(x, k, **kw)) < LAYER_TOL
+    import torch
+    plan = eng.plan()
+    xd = torch.from_numpy(x).cuda()
+    yd = torch.empty((B,) + plan.out_shape, device="cuda")
+    st = torch.cuda.Stream()
+    for _ in range(3):
+        plan.run_graph(B, xd.data_ptr(), yd.data_ptr(), st.cuda_stream)
+    st.synchronize()
+    assert np.array_equal(yd.cpu().numpy(), y1)
+
+
+@pytest.mark.parametrize("frame", [0, 1, 2, 3])
+def test_yolo_latency_plan_vs_reference_golden(yolo_weights, golden_frames, frame, latency_b1_engine=[]):
+    """BASELINE config 2 in latency mode: conv4-conv8 split over the chip; within the net
+    tolerance of the reference goldens (not bit-equal to the batch plan's rows)."""
+    if not latency_b1_engine:
+        g, _ = yolo_graph.build_graph(dnn_hip.DnnGraphBuilder, yolo_weights, in_shape=(1, 416, 416, 3))
+        latency_b1_engine.append(dnn_hip.DnnInferenceEngine(g, False, latency=True))
+    eng = latency_b1_engine[0]
+    assert eng.plan().describe().count(" combine latency") >= 5
+    y = eng.run(synth.frame(frame))
+    assert R.normwise_err(y, golden_frames[frame]) < NET_TOL
