@@ -132,6 +132,8 @@ int choose_splitk(int N, int K, bool combine = false);
 // that its work units fill the chip (depends on M: batch-1 results are not bit-equal to a
 // batch plan's rows).  In: the batch rule's (cfg, splits); kept when they fill the chip.
 void choose_latency_plan(long long M, int N, int K, int* cfg, int* splits);
+// tile order of a GEMM launch (SplitK::nmajor): 1 = N-major
+int nmajor_order(int N, int tilesN);
 // With `tickets` (>= the cfg's tile count of unsigned, zero before the first launch and left
 // zero by every launch) the split-K GEMM finishes itself: the last-arriving split of each tile
 // sums the partials in split order and writes C with the epilogue (splitk_combine, gemm_f32.h),

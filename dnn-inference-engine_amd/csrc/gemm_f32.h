@@ -415,7 +415,21 @@ struct SplitK {
   int ldo = 0;
   int flags = 0;     // epilogue of the final output
   int splits = 1;
+  int nmajor = 0;    // tile -> (tm, tn) N-major: an XCD's contiguous tile range shares one N panel
 };
+
+// tile index -> (M tile, N tile): M-major (consecutive tiles walk N) or N-major (an XCD's
+// contiguous range of tiles shares one weight panel, which then stays in its L2)
+__device__ __forceinline__ void tile_coords(int tile, int tilesN, const SplitK& sk, int& tm, int& tn) {
+  if (sk.nmajor) {
+    const int tilesM = sk.ntile / tilesN;
+    tn = tile / tilesM;
+    tm = tile - tn * tilesM;
+  } else {
+    tm = tile / tilesN;
+    tn = tile - tm * tilesN;
+  }
+}
 
 // Sum of the split-K partials in split order, ((p0 + p1) + p2) ..., then the fused epilogue.
 // part: [splits][M][N] (slab floats apart), C: [M][ldc].  HBM-bound: (splits + 1) * M * N * 4 B.
@@ -672,7 +686,8 @@ gemm_f32_glds_kernel(const float* __restrict__ A, int lda, const float* __restri
     if (!sk.tickets) C += split * sk.slab;
     epi.flags = 0;  // raw partial sums; the reduce kernel / the combine applies the epilogue
   }
-  const int tm_ = tile / tilesN, tn_ = tile - tm_ * tilesN;
+  int tm_, tn_;
+  tile_coords(tile, tilesN, sk, tm_, tn_);
   const int m0 = tm_ * BM, n0 = tn_ * BN;
   const int lane = threadIdx.x & 63;
   const int wid = wave_uniform(threadIdx.x >> 6);

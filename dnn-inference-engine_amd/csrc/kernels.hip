@@ -41,7 +41,7 @@ static int check_launch(const char* what) {
 constexpr int IM2COL_THREADS = 256;
 constexpr int IM2COL_KCH = 1024;      // K columns per block
 constexpr int IM2COL_MAX_ROWS = 256;  // rows per block
-constexpr int IM2COL_BLOCK_FLOATS = 4096 * 4;
+constexpr int IM2COL_BLOCK_FLOATS = 8192;  // long-K layers (measured: 8 K floats per block beats 16 K-64 K)
 constexpr int IM2COL_ILP = 4;
 
 template <bool VEC>
@@ -126,6 +126,56 @@ im2col_nhwc_kernel(const float* __restrict__ in, float* __restrict__ col, ConvGe
   }
 }
 
+// Row-staged im2col for C % 4 != 0 (conv0: C = 3): one block per output row (b, oy).  The kh
+// input rows under it are read once, coalesced, into LDS (kh x ((OW-1)*sw + kw) x C floats,
+// zeros for the padding; dynamic LDS sized to that), then the row's OW x Kpad col block is
+// written as consecutive float4s (fully coalesced).  Kpad / 4 divides the 256 threads, so each
+// thread keeps one float4 column j for the whole row: its 4 LDS source offsets are computed
+// once, and a store costs 4 LDS reads.  Replaces four scalar HBM gathers (plus table lookups)
+// per float4 (conv0: 3.0 TB/s).
+__global__ void __launch_bounds__(256)
+im2col_rows_kernel(const float* __restrict__ in, float* __restrict__ col, ConvGeom g) {
+  extern __shared__ float s_in[];
+  const int oy = blockIdx.x % g.OH, b = blockIdx.x / g.OH;
+  const int npx = (g.OW - 1) * g.sw + g.kw;  // staged pixels per input row
+  const int rowlen = npx * g.C;
+  const int ix0 = -g.pl;
+  for (int dy = 0; dy < g.kh; ++dy) {
+    const int iy = oy * g.sh - g.pt + dy;
+    const bool rok = (unsigned)iy < (unsigned)g.H;
+    const float* src = in + (((long long)b * g.H + (rok ? iy : 0)) * g.W) * g.C;
+    float* d = s_in + dy * rowlen;
+    for (int px = threadIdx.x; px < npx; px += 256) {
+      const int ix = ix0 + px;
+      const bool ok = rok && (unsigned)ix < (unsigned)g.W;
+      for (int c = 0; c < g.C; ++c) d[px * g.C + c] = ok ? src[ix * g.C + c] : 0.f;
+    }
+  }
+  const int kq = g.Kpad >> 2;   // divides 256 (launcher)
+  const int j = threadIdx.x % kq, ox0 = threadIdx.x / kq, oxs = 256 / kq;
+  int t[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int k = 4 * j + q;
+    t[q] = -1;
+    if (k < g.K) {
+      const int tap = k / g.C, c = k - tap * g.C;
+      const int dy = tap / g.kw, dx = tap - dy * g.kw;
+      t[q] = dy * rowlen + dx * g.C + c;
+    }
+  }
+  __syncthreads();
+  float* dst = col + ((long long)b * g.OH + oy) * g.OW * g.Kpad + 4 * j;
+  const int xstep = g.sw * g.C;
+  for (int ox = ox0; ox < g.OW; ox += oxs) {
+    const int xo = ox * xstep;
+    float x[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) x[q] = t[q] >= 0 ? s_in[t[q] + xo] : 0.f;
+    *reinterpret_cast<float4*>(dst + (size_t)ox * g.Kpad) = make_float4(x[0], x[1], x[2], x[3]);
+  }
+}
+
 int launch_im2col(const float* in, float* col, const ConvGeom& g, hipStream_t stream) {
   long long M = (long long)g.B * g.OH * g.OW;
   if (M == 0) return 0;
@@ -134,8 +184,23 @@ int launch_im2col(const float* in, float* col, const ConvGeom& g, hipStream_t st
     return -2;
   }
   const bool vec = (g.C % 4) == 0;
+  const long long row_floats = (long long)g.kh * ((g.OW - 1) * g.sw + g.kw) * g.C;
+  if (!vec && g.Kpad <= 1024 && 256 % (g.Kpad / 4) == 0 && row_floats <= 16384 &&
+      (long long)g.B * g.OH < 0x7fffffffLL && !getenv_flag_off("DNN_HIP_IM2COL_ROWS")) {
+    hipLaunchKernelGGL(im2col_rows_kernel, dim3((unsigned)(g.B * g.OH)), dim3(256), (size_t)row_floats * 4, stream,
+                       in, col, g);
+    return check_launch("im2col_rows");
+  }
   const int kch = g.Kpad < IM2COL_KCH ? g.Kpad : IM2COL_KCH;
-  int rows = IM2COL_BLOCK_FLOATS / kch;
+  // floats moved per block: 4 K for K-chunks of <= 1024 columns' worth of short rows (conv1-3:
+  // 5.4 -> 6.1 TB/s), 8 K for the long-K layers (conv4-7 lose with 4 K); DNN_HIP_IM2COL_FLOATS
+  // overrides (experiments)
+  static const int blk_env = [] {
+    const char* e = getenv("DNN_HIP_IM2COL_FLOATS");
+    return e && atoi(e) >= 1024 ? atoi(e) : 0;
+  }();
+  const int blk_floats = blk_env ? blk_env : (g.Kpad < IM2COL_KCH ? 4096 : IM2COL_BLOCK_FLOATS);
+  int rows = blk_floats / kch;
   rows = rows < 1 ? 1 : (rows > IM2COL_MAX_ROWS ? IM2COL_MAX_ROWS : rows);
   dim3 grid(ceil_div_i(M, rows), ceil_div_i(g.Kpad, IM2COL_KCH));
   if (vec)
@@ -371,6 +436,13 @@ static bool fits_buf(long long bytes) { return bytes > 0 && bytes < 0x80000000LL
 // DNN_HIP_GEMM_BUF=0: flat 64-bit DMA addresses (experiments and the equivalence tests)
 static bool abuf_enabled() { return !getenv_flag_off("DNN_HIP_GEMM_BUF"); }
 
+// N-major tile order (DNN_HIP_NMAJOR=1, experiment): tiles of one weight panel on one XCD
+int nmajor_order(int N, int tilesN) {
+  const char* e = getenv("DNN_HIP_NMAJOR");
+  (void)N;
+  return (e && e[0] == '1' && tilesN > 1) ? 1 : 0;
+}
+
 // grid and SplitK descriptor for `splits` (> 1: the kernel writes raw partials to `slab`;
 // with `tickets` it also combines them itself into C)
 static int split_setup(int cfg, long long M, int N, int Kpad, int splits, float* slab, unsigned* tickets, float* C,
@@ -403,6 +475,7 @@ static int split_setup(int cfg, long long M, int N, int Kpad, int splits, float*
     }
     *grid *= splits;
   }
+  sk->nmajor = nmajor_order(N, *tilesN);
   return 0;
 }
 

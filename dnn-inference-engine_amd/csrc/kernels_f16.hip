@@ -157,6 +157,7 @@ int launch_gemm16(int cfg, int mode, const half_t* A, int lda, const ImplicitCon
     }
     grid *= splits;
   }
+  sk.nmajor = nmajor_order(N, tilesN);
   BufDesc bd{reinterpret_cast<const float*>(abase), (unsigned)a_bytes, (unsigned)b_bytes};
   const BufDesc* pbd = abuf ? &bd : nullptr;
   switch (mode) {

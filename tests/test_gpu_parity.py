@@ -851,3 +851,32 @@ def test_yolo_latency_plan_vs_reference_golden(yolo_weights, golden_frames, fram
     assert eng.plan().describe().count(" combine latency") >= 5
     y = eng.run(synth.frame(frame))
     assert R.normwise_err(y, golden_frames[frame]) < NET_TOL
+
+
+IM2COL_ROW_CASES = [
+    # B, H, W, C, kh, stride, pad: C % 4 != 0 -> the row-staged explicit im2col
+    (2, 40, 38, 3, 3, 1, "SAME"),   # conv0-like
+    (3, 9, 11, 5, 3, 2, "SAME"),    # stride 2, C = 5: Kpad / 4 = 12 does not divide 256 -> gather path
+    (2, 9, 11, 3, 3, 2, "SAME"),    # stride 2 through the row-staged kernel
+    (1, 10, 9, 3, 3, 1, "VALID"),
+    (2, 7, 6, 6, 1, 1, "SAME"),     # 1x1 on C = 6 (explicit path: C % 32 != 0)
+]
+
+
+@pytest.mark.parametrize("case", IM2COL_ROW_CASES)
+def test_im2col_rows_equals_gather_path(monkeypatch, case):
+    """The unfused plan's explicit im2col for C % 4 != 0 stages the kh input rows of an output
+    row in LDS and writes coalesced float4s (im2col_rows_kernel); its col buffer, hence the
+    plan's output, is bit-identical to the per-element gather kernel (DNN_HIP_IM2COL_ROWS=0)."""
+    B, H, W, C, kh, s, pad = case
+    rng = np.random.default_rng(H * W + C)
+    x = rng.standard_normal((B, H, W, C)).astype(np.float32)
+    k = (rng.standard_normal((kh, kh, C, 16)) * 0.3).astype(np.float32)
+    kw = dict(strides=(1, s, s, 1), pad=pad, bias=rng.standard_normal(16).astype(np.float32), leaky=True)
+    monkeypatch.setenv("DNN_HIP_FUSE", "0")
+    outs = []
+    for rows in ("1", "0"):
+        monkeypatch.setenv("DNN_HIP_IM2COL_ROWS", rows)
+        outs.append(dnn_hip.DnnInferenceEngine(_chain(x.shape, k, **kw), False).run(x))
+    assert np.array_equal(outs[0], outs[1])
+    assert R.normwise_err(outs[0], _oracle_chain(x, k, **kw)) < LAYER_TOL
