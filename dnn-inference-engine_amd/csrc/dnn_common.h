@@ -134,6 +134,10 @@ int choose_splitk(int N, int K, bool combine = false);
 void choose_latency_plan(long long M, int N, int K, int* cfg, int* splits);
 // tile order of a GEMM launch (SplitK::nmajor): 1 = N-major
 int nmajor_order(int N, int tilesN);
+// Persistent implicit GEMM for unsplit short-K layers (gemm_persist.h; DNN_HIP_PERSIST=0 off):
+// same arguments and bits as launch_gemm_implicit with splits = 1; -3 = not covered (fall back).
+int launch_gemm_persist(int cfg, int mode, const float* in, const ImplicitConv& ic, const float* Bt, int ldb,
+                        float* C, int ldc, long long M, int N, int Kpad, const EpiParams& epi, hipStream_t stream);
 // With `tickets` (>= the cfg's tile count of unsigned, zero before the first launch and left
 // zero by every launch) the split-K GEMM finishes itself: the last-arriving split of each tile
 // sums the partials in split order and writes C with the epilogue (splitk_combine, gemm_f32.h),

@@ -17,6 +17,7 @@
 #include <cfloat>
 #include "dnn_common.h"
 #include "gemm_f32.h"
+#include "gemm_persist.h"
 
 namespace dnnhip {
 
@@ -555,6 +556,89 @@ int launch_gemm_implicit(int cfg, int mode, const float* in, const ImplicitConv&
                                       dim3(g), stream);
   return launch_glds<GEMM_IMPLICIT_POOL>(cfg, in, 0, Bt, ldb, out, ldo, (int)M, N, Kpad, epi, tilesN, ic, sk, pbd,
                                          dim3(g), stream);
+}
+
+// ---- persistent short-K implicit GEMM (gemm_persist.h)
+static int device_cus() {
+  static int cus[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+  if (!cus[dev]) {
+    int v = 0;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) v = 0;
+    cus[dev] = v;
+  }
+  return cus[dev];
+}
+
+template <int BM, int BN, int WM, int WN, int MF, int NS, int MODE, int NTN>
+static int launch_persist_t(const float* Bt, int ldb, float* C, int ldc, int M, int N, int Kpad,
+                            const EpiParams& epi, int tilesN, int ntiles, const ImplicitConv& ic, const BufDesc& bd,
+                            unsigned out_bytes, hipStream_t stream) {
+  auto kern = gemm_f32_persist_kernel<BM, BN, WM, WN, MF, NS, MODE, NTN>;
+  static int per_cu = -1;  // resident workgroups per CU (LDS, registers, waves)
+  if (per_cu < 0) {
+    int v = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, kern, WM * WN * 64, 0) != hipSuccess) v = 0;
+    per_cu = v;
+  }
+  int wgs = per_cu;
+  if (const char* e = getenv("DNN_HIP_PERSIST_WGS")) {  // experiments: workgroups per CU
+    const int v = atoi(e);
+    if (v > 0 && v < wgs) wgs = v;
+  }
+  long long grid = (long long)device_cus() * wgs;
+  // fewer than two tiles per workgroup: the tail of the ones holding two costs more than the
+  // pipelining gains (conv4 at batch 64: 452 tiles on 448 slots, 0.224 -> 0.317 ms)
+  if (ntiles < 2 * grid || Kpad / 32 < NS) return -3;
+  grid -= grid % 8;
+  if (grid < 8) return -3;
+  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(WM * WN * 64), 0, stream, Bt, ldb, C, ldc, M, N, Kpad, epi,
+                     tilesN, ntiles, ic, bd, out_bytes);
+  return check_launch("gemm_persist");
+}
+
+bool persist_enabled() { return !getenv_flag_off("DNN_HIP_PERSIST"); }
+
+// Persistent launch of an unsplit implicit conv on the batch configs conv2-conv4 use;
+// returns -3 (caller falls back to launch_gemm_implicit) when the shape or config is not one
+// it covers.
+int launch_gemm_persist(int cfg, int mode, const float* in, const ImplicitConv& ic_in, const float* Bt, int ldb,
+                        float* C, int ldc, long long M, int N, int Kpad, const EpiParams& epi, hipStream_t stream) {
+  if (M == 0 || N == 0) return 0;
+  if (!persist_enabled() || (mode != GEMM_IMPLICIT && mode != GEMM_IMPLICIT_POOL) || ic_in.C % 32 != 0 ||
+      M > 0x7fffffffLL || Kpad % 32 != 0 || !implicit_conv_supported(ic_in.C, ic_in.kh, ic_in.kw) ||
+      (mode == GEMM_IMPLICIT_POOL && M % 4 != 0))
+    return -3;
+  ImplicitConv ic = ic_in;
+  implicit_conv_magic(&ic);
+  const CfgInfo ci = kCfgs[cfg];
+  const int tilesM = ceil_div_i(M, ci.bm), tilesN = ceil_div_i(N, ci.bn);
+  const long long ntiles = (long long)tilesM * tilesN;
+  const long long per_img = mode == GEMM_IMPLICIT_POOL ? 4LL * ic.PH * ic.PW : (long long)ic.OH * ic.OW;
+  const long long nimg = per_img > 0 ? M / per_img : 0;
+  const long long a_bytes = ((nimg * ic.H * ic.W + ic.W + 1) * (long long)ic.C) * 4;
+  const long long b_bytes = (long long)tilesN * ci.bn * ldb * 4;
+  const long long o_rows = mode == GEMM_IMPLICIT_POOL ? M / 4 : M;
+  const long long o_bytes = o_rows * (long long)ldc * 4;
+  if (!fits_buf(a_bytes) || !fits_buf(b_bytes) || !fits_buf(o_bytes) || ntiles > 0x7fffffffLL || tilesN > 2)
+    return -3;
+  const BufDesc bd{in - (size_t)(ic.W + 1) * ic.C, (unsigned)a_bytes, (unsigned)b_bytes};
+  const int m = (int)M, nt = (int)ntiles;
+  const unsigned ob = (unsigned)o_bytes;
+#define DNN_PERSIST(BM_, BN_, WM_, WN_, MF_, NS_)                                                                      \
+  return mode == GEMM_IMPLICIT                                                                                        \
+             ? launch_persist_t<BM_, BN_, WM_, WN_, MF_, NS_, 1, 2>(Bt, ldb, C, ldc, m, N, Kpad, epi, tilesN, nt, ic, bd, \
+                                                                    ob, stream)                                       \
+             : launch_persist_t<BM_, BN_, WM_, WN_, MF_, NS_, 2, 2>(Bt, ldb, C, ldc, m, N, Kpad, epi, tilesN, nt, ic, bd, \
+                                                                    ob, stream)
+  switch (cfg) {
+    case GEMM_G256x64_K32: DNN_PERSIST(256, 64, 4, 2, 32, 2);
+    case GEMM_64x128_K32: DNN_PERSIST(64, 128, 2, 2, 32, 2);
+    case GEMM_G192x128_W8: DNN_PERSIST(192, 128, 2, 4, 32, 2);
+    default: return -3;
+  }
+#undef DNN_PERSIST
 }
 
 int launch_splitk_reduce(const float* slab, int splits, long long M, int N, float* C, int ldc,

@@ -680,8 +680,13 @@ int dnn_plan_run(dnn_plan* p, int n, const float* d_in, float* d_out, void* stre
           ImplicitConv ic{zero, L.H, L.W, L.C, L.OH, L.OW, L.PH, L.PW, L.kh, L.kw, L.sh, L.sw, L.pt, L.pl,
                           L.pool ? 1 : 0};
           const long long M = L.pool ? 4LL * n * L.PH * L.PW : Mc;
-          rc = launch_gemm_implicit(L.cfg, L.pool ? GEMM_IMPLICIT_POOL : GEMM_IMPLICIT, cur, ic, wt, L.Kpad, dst,
-                                    L.OC, M, L.OC, L.Kpad, epi, s, L.splits, slab, tickets);
+          const int gm = L.pool ? GEMM_IMPLICIT_POOL : GEMM_IMPLICIT;
+          // unsplit layers: the persistent kernel (same bits) when it covers the config
+          rc = L.splits == 1 ? launch_gemm_persist(L.cfg, gm, cur, ic, wt, L.Kpad, dst, L.OC, M, L.OC, L.Kpad, epi, s)
+                             : -3;
+          if (rc == -3)
+            rc = launch_gemm_implicit(L.cfg, gm, cur, ic, wt, L.Kpad, dst, L.OC, M, L.OC, L.Kpad, epi, s, L.splits,
+                                      slab, tickets);
           break;
         }
         case MODE_DIRECT: {

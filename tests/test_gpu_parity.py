@@ -880,3 +880,40 @@ def test_im2col_rows_equals_gather_path(monkeypatch, case):
         outs.append(dnn_hip.DnnInferenceEngine(_chain(x.shape, k, **kw), False).run(x))
     assert np.array_equal(outs[0], outs[1])
     assert R.normwise_err(outs[0], _oracle_chain(x, k, **kw)) < LAYER_TOL
+
+
+PERSIST_CASES = [
+    # B, H, W, C, od, pool: unsplit implicit layers on the configs the persistent kernel covers
+    (16, 104, 104, 32, 64, True),   # conv2 at batch 16: 256x64 tiles, 676 tiles > one round
+    (16, 52, 52, 64, 128, True),    # conv3: 64x128
+    (64, 26, 26, 128, 256, True),   # conv4 at batch 64: 64x128 forced (DNN_HIP_CFG), two N tiles
+    (9, 27, 25, 64, 128, True),     # odd 27x25 -> 14x13 pool windows (ragged), partial last tile
+    (12, 30, 30, 32, 128, False),   # no pool (MODE 1)
+]
+
+
+@pytest.mark.parametrize("case", PERSIST_CASES)
+def test_persistent_gemm_equals_tile_kernel(monkeypatch, case):
+    """The persistent implicit GEMM (gemm_persist.h: one workgroup walks many tiles, the LDS-DMA
+    ring runs across tile boundaries, counted waits include the epilogue's fixed store count)
+    gives the same bits as one tile per workgroup (DNN_HIP_PERSIST=0), and matches the oracle."""
+    B, H, W, C, od, pool = case
+    rng = np.random.default_rng(B + H + C + od)
+    x = rng.standard_normal((B, H, W, C)).astype(np.float32)
+    k = (rng.standard_normal((3, 3, C, od)) * np.sqrt(2.0 / (9 * C))).astype(np.float32)
+    gam = rng.uniform(0.5, 1.5, od).astype(np.float32)
+    gam[::3] *= -1
+    kw = dict(bias=rng.standard_normal(od).astype(np.float32) * 0.1,
+              bn=(rng.standard_normal(od).astype(np.float32) * 0.1, rng.uniform(0.5, 1.5, od).astype(np.float32), gam),
+              leaky=True, pool=(2, 2, "SAME") if pool else None)
+    outs = {}
+    if C == 128:
+        monkeypatch.setenv("DNN_HIP_CFG", "1152:4")  # 64x128: 1352 tiles, per-N-tile epilogue params
+    for on in ("1", "0"):
+        monkeypatch.setenv("DNN_HIP_PERSIST", on)
+        eng = dnn_hip.DnnInferenceEngine(_chain(x.shape, k, **kw), False)
+        outs[on] = eng.run(x)
+        outs[on + "b"] = eng.run(x)
+    assert np.array_equal(outs["1"], outs["0"]) and np.array_equal(outs["1b"], outs["1"])
+    idx = np.arange(0, B, max(1, B // 3))
+    assert R.normwise_err(outs["1"][idx], _oracle_chain(x[idx], k, **kw)) < LAYER_TOL
