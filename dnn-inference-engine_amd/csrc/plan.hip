@@ -366,6 +366,13 @@ int dnn_plan_add_conv(dnn_plan* p, int kh, int kw, int od, int stride_h, int str
   set_cfg(p, L);
   L.epi_flags = (biases ? EPI_BIAS : 0) | (mean ? EPI_BN : 0) |
                 (leaky == 1 ? EPI_LEAKY_F64 : leaky == 2 ? EPI_LEAKY_F32 : 0);
+  // fp16 plans (tolerance, not bit parity): BiasAdd + BatchNorm folded into v * alpha - beta
+  // (alpha = gamma / sqrt(var + eps), beta = (mean - bias) * alpha) and the leaky as
+  // max(v, 0.1f v): 4 VALU per output instead of ~30 for the reference's exact division and
+  // double-rounded leaky (the VALU-bound small-channel kernels run on the epilogue)
+  const bool fold16 = p->fp16 && mean;
+  if (fold16)
+    L.epi_flags = EPI_BN_AB | ((L.epi_flags & (EPI_LEAKY_F64 | EPI_LEAKY_F32)) ? EPI_LEAKY_F32 : 0);
   if (kernel) {
     L.have_host = true;
     L.w.assign(kernel, kernel + (size_t)L.K * od);
@@ -382,6 +389,14 @@ int dnn_plan_add_conv(dnn_plan* p, int kh, int kw, int od, int stride_h, int str
         volatile float s = var[d] + eps;
         L.sq[d] = sqrtf(s);
         L.gamma[d] = gamma[d];
+      }
+      if (fold16) {  // EPI_BN_AB: mean slot = alpha, sq slot = beta
+        const float alpha = L.gamma[d] / L.sq[d];
+        const float beta = (L.mean[d] - (biases ? biases[d] : 0.f)) * alpha;
+        L.mean[d] = alpha;
+        L.sq[d] = beta;
+        L.bias[d] = 0.f;
+        L.gamma[d] = 1.f;
       }
     }
   }

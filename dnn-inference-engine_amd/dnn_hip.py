@@ -538,9 +538,10 @@ class Plan(object):
                 keep = (c.kernel, bias, mean, var, gamma)  # noqa: F841 (alive across the call)
                 rc = self.lib.dnn_plan_add_conv(
                     self.h, kh, kw, od, int(c.strides[1]), int(c.strides[2]), _pad_code(c.padding),
-                    _vp(c.kernel) if upload else None, _vp(bias) if upload else None,
-                    _vp(mean) if upload else None, _vp(var) if upload else None,
-                    _vp(gamma) if upload else None, eps, leaky_variant if e.leaky else 0)
+                    # without upload only the kernel is withheld: the epilogue pointers still
+                    # declare which of bias / BN the layer has (the values arrive with the arena)
+                    _vp(c.kernel) if upload else None, _vp(bias), _vp(mean), _vp(var), _vp(gamma), eps,
+                    leaky_variant if e.leaky else 0)
                 _check(rc, "dnn_plan_add_conv", self.lib)
             else:
                 p = e.pool

@@ -917,3 +917,34 @@ def test_persistent_gemm_equals_tile_kernel(monkeypatch, case):
     assert np.array_equal(outs["1"], outs["0"]) and np.array_equal(outs["1b"], outs["1"])
     idx = np.arange(0, B, max(1, B // 3))
     assert R.normwise_err(outs["1"][idx], _oracle_chain(x[idx], k, **kw)) < LAYER_TOL
+
+
+@pytest.mark.parametrize("precision", ["fp32", "fp16"])
+def test_shape_only_plan_with_copied_arena(yolo_weights, precision):
+    """A rank that lays the plan out without weights (upload=False: the bench's non-root ranks,
+    whose packed arena arrives by broadcast) must run the same epilogue as the uploading rank:
+    with rank 0's arena copied in, its outputs equal rank 0's bit for bit."""
+    import torch
+    g, _ = yolo_graph.build_graph(dnn_hip.DnnGraphBuilder, yolo_weights, in_shape=(2, 416, 416, 3))
+    entries = dnn_hip.lower_graph(g)
+    wb, sb = dnn_hip.Plan.memory(2, (416, 416, 3), entries, precision=precision)
+    bufs = [(torch.empty(wb, dtype=torch.uint8, device="cuda"), torch.empty(sb, dtype=torch.uint8, device="cuda"))
+            for _ in range(2)]
+    plans = [dnn_hip.Plan(2, (416, 416, 3), entries, device=0, weights_ptr=w.data_ptr(), workspace_ptr=s.data_ptr(),
+                          upload=(k == 0), precision=precision) for k, (w, s) in enumerate(bufs)]
+    bufs[1][0].copy_(bufs[0][0])
+    x = torch.from_numpy(synth.frames([0, 1])).cuda()
+    ys = [torch.empty((2, 13, 13, 125), device="cuda") for _ in range(2)]
+    for p, y in zip(plans, ys):
+        p.run_device(2, x.data_ptr(), y.data_ptr())
+    torch.cuda.synchronize()
+    assert torch.equal(ys[0], ys[1])
+    assert R.normwise_err(ys[0][:1].cpu().numpy(), golden_frames_0()) < (NET_TOL if precision == "fp32" else 2e-2)
+    for p in plans:
+        p.close()
+
+
+def golden_frames_0():
+    import os
+    from conftest import GOLDEN
+    return np.load(os.path.join(GOLDEN, "net_frame0.npy"))
