@@ -66,6 +66,27 @@ def _sigmoid(x):
     return _F(_F(1) / _F(_F(1) + _E ** _F(-x)))
 
 
+def decode_one(p, row, col, b):
+    """Box (row, col, anchor) of a [13,13,5,25] float32 tensor: [[left, top, right, bottom],
+    score, class] (yolov2tiny.py:118-140)."""
+    tx, ty, tw, th, tc = (p[row, col, b, k] for k in range(5))
+    cx = _F(_F(_F(col) + _sigmoid(tx)) * _F(32.0))
+    cy = _F(_F(_F(row) + _sigmoid(ty)) * _F(32.0))
+    rw = _F(_F(np.exp(tw) * _F(ANCHORS[2 * b])) * _F(32.0))
+    rh = _F(_F(np.exp(th) * _F(ANCHORS[2 * b + 1])) * _F(32.0))
+    conf = _sigmoid(tc)
+    logits = p[row, col, b, 5:]
+    e = np.exp(logits - np.max(logits))
+    s = _pairwise_sum_f32(e)
+    probs = [_F(v / s) for v in e]
+    best = max(range(N_CLASSES), key=lambda k: (probs[k], -k))
+    left = int(_F(cx - _F(rw / _F(2.0))))
+    right = int(_F(cx + _F(rw / _F(2.0))))
+    top = int(_F(cy - _F(rh / _F(2.0))))
+    bottom = int(_F(cy + _F(rh / _F(2.0))))
+    return [[left, top, right, bottom], _F(conf * probs[best]), best]
+
+
 def decode(predictions):
     """All 845 boxes of one image in (row, col, anchor) order:
     [(left, top, right, bottom), score, class] for those above the threshold (unsorted)."""
@@ -74,24 +95,9 @@ def decode(predictions):
     for row in range(13):
         for col in range(13):
             for b in range(5):
-                tx, ty, tw, th, tc = (p[row, col, b, k] for k in range(5))
-                cx = _F(_F(_F(col) + _sigmoid(tx)) * _F(32.0))
-                cy = _F(_F(_F(row) + _sigmoid(ty)) * _F(32.0))
-                rw = _F(_F(np.exp(tw) * _F(ANCHORS[2 * b])) * _F(32.0))
-                rh = _F(_F(np.exp(th) * _F(ANCHORS[2 * b + 1])) * _F(32.0))
-                conf = _sigmoid(tc)
-                logits = p[row, col, b, 5:]
-                e = np.exp(logits - np.max(logits))
-                s = _pairwise_sum_f32(e)
-                probs = [_F(v / s) for v in e]
-                best = max(range(N_CLASSES), key=lambda k: (probs[k], -k))
-                left = int(_F(cx - _F(rw / _F(2.0))))
-                right = int(_F(cx + _F(rw / _F(2.0))))
-                top = int(_F(cy - _F(rh / _F(2.0))))
-                bottom = int(_F(cy + _F(rh / _F(2.0))))
-                score = _F(conf * probs[best])
-                if score > _THR:
-                    out.append([[left, top, right, bottom], score, best])
+                d = decode_one(p, row, col, b)
+                if d[1] > _THR:
+                    out.append(d)
     return out
 
 
