@@ -213,7 +213,14 @@ int launch_splitk_reduce16(const float* slab, int splits, long long M, int N, ha
                            const EpiParams& epi, hipStream_t stream);
 int launch_f32_to_f16(const float* in, half_t* out, long long n, hipStream_t s);
 int launch_f16_to_f32(const half_t* in, float* out, long long n, hipStream_t s);
-int launch_maxpool16(const half_t* in, half_t* out, const PoolGeom& g, hipStream_t s);
+int launch_maxpool16(const half_t* in, half_t* out, const PoolGeom& g, hipStream_t s, int opad = 0);
+// fp16 3x3/s1/SAME conv with a zero-bordered input [B][H+2][W+2][C] (C % 64 == 0, N % 256 == 0),
+// weights packed K-order (chunk, tap, c) (launch_pack_weights order 2); out_padded: write the
+// output zero-bordered too (gemm_f16_patch.h)
+bool conv_patch16_supported(int C, int OC, int H, int W, int OH, int OW, int kh, int kw, int sh, int sw, int pt,
+                            int pl);
+int launch_conv_patch16(const half_t* in_padded, const half_t* Bt, int ldb, half_t* out, int out_padded, long long M,
+                        int N, int K, int H, int W, int C, const EpiParams& epi, hipStream_t stream);
 // conv0 direct kernel with an fp16 output (fp32 input frames)
 int launch_conv3x3_pool2_direct_f16out(const float* in, const float* w, half_t* out, const DirectGeom& g, int cin,
                                        int nout, const EpiParams& epi, hipStream_t stream);

@@ -775,6 +775,11 @@ __global__ void pack_weights_kernel(const float* __restrict__ w, float* __restri
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
     int n = (int)(i / Kpad), k = (int)(i % Kpad);
+    if (order == 3) {  // MFMA fragment order of the order-2 K (conv_patch16): [n/32][k/16][lane][8]
+      const long long e = i & 7, lane = (i >> 3) & 63, kq = (i >> 9) % (Kpad / 16), nb = (i >> 9) / (Kpad / 16);
+      n = (int)(nb * 32 + (lane & 31));
+      k = (int)(kq * 16 + 8 * (lane >> 5) + e);
+    }
     float v = 0.f;
     if (n < N && k < K) {
       int src = k;
@@ -782,6 +787,10 @@ __global__ void pack_weights_kernel(const float* __restrict__ w, float* __restri
         int tap = k / C, c = k - tap * C;
         int dy = tap / kw, dx = tap - dy * kw;
         src = (c * kh + dy) * kw + dx;
+      } else if (order >= 2) {  // k = (chunk * taps + tap) * 64 + cc, c = 64 * chunk + cc (conv_patch16)
+        const int taps = kh * kw, blk = k / 64, cc = k - blk * 64;
+        const int chunk = blk / taps, tap = blk - chunk * taps;
+        src = tap * C + 64 * chunk + cc;
       }
       v = w[(long long)src * N + n];
     }

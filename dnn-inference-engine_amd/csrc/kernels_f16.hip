@@ -5,6 +5,7 @@
 #include <cfloat>
 #include "dnn_common.h"
 #include "gemm_f16.h"
+#include "gemm_f16_patch.h"
 
 namespace dnnhip {
 
@@ -214,7 +215,8 @@ int launch_f16_to_f32(const half_t* in, float* out, long long n, hipStream_t s) 
 
 // ---- max pool on fp16 NHWC (C % 8 == 0): 8 channels per thread, the reference's window
 // order and `m >= x ? m : x`, pad cells (-FLT_MAX in the reference) skipped
-__global__ void maxpool16_kernel(const half_t* __restrict__ in, half_t* __restrict__ out, PoolGeom g, long long total) {
+__global__ void maxpool16_kernel(const half_t* __restrict__ in, half_t* __restrict__ out, PoolGeom g, long long total,
+                                 int opad) {
   typedef _Float16 h8 __attribute__((ext_vector_type(8)));
   const int cq = g.C / 8;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
@@ -246,18 +248,71 @@ __global__ void maxpool16_kernel(const half_t* __restrict__ in, half_t* __restri
     h8 o;
 #pragma unroll
     for (int e = 0; e < 8; ++e) o[e] = (half_t)m[e];
-    *reinterpret_cast<h8*>(out + (((size_t)b * g.OH + oy) * g.OW + ox) * g.C + c) = o;
+    // opad: write into the interior of a zero-bordered [B][OH+2][OW+2][C] buffer (the input of a
+    // conv3x3_f16_patch_kernel layer)
+    *reinterpret_cast<h8*>(out + (((size_t)b * (g.OH + 2 * opad) + oy + opad) * (g.OW + 2 * opad) + ox + opad) * g.C +
+                           c) = o;
   }
 }
-int launch_maxpool16(const half_t* in, half_t* out, const PoolGeom& g, hipStream_t s) {
+int launch_maxpool16(const half_t* in, half_t* out, const PoolGeom& g, hipStream_t s, int opad) {
   if (g.B == 0) return 0;
   if (g.C % 8 != 0) {
     set_error("maxpool16: C=%d must be a multiple of 8", g.C);
     return -2;
   }
   const long long total = (long long)g.B * g.OH * g.OW * (g.C / 8);
-  hipLaunchKernelGGL(maxpool16_kernel, dim3((unsigned)grid_for(total)), dim3(256), 0, s, in, out, g, total);
+  hipLaunchKernelGGL(maxpool16_kernel, dim3((unsigned)grid_for(total)), dim3(256), 0, s, in, out, g, total, opad);
   return check16("maxpool16");
+}
+
+// ---- conv3x3_f16_patch_kernel (gemm_f16_patch.h): conv6/conv7 of the fp16 path
+constexpr int P16_BM = 192, P16_NPR = 320;
+constexpr bool P16_DEFAULT = false;
+
+// DNN_HIP_PATCH16=1 selects the patch kernel for eligible layers (default: on once measured faster
+// than gemm_f16_glds_kernel on the bench line)
+static bool patch16_enabled() {
+  const char* e = getenv("DNN_HIP_PATCH16");
+  return e ? e[0] == '1' : P16_DEFAULT;
+}
+
+bool conv_patch16_supported(int C, int OC, int H, int W, int OH, int OW, int kh, int kw, int sh, int sw, int pt,
+                            int pl) {
+  return kh == 3 && kw == 3 && sh == 1 && sw == 1 && pt == 1 && pl == 1 && OH == H && OW == W && C % 64 == 0 &&
+         OC % 256 == 0 && patch16_enabled();
+}
+
+// rows of the padded input one BM-row tile spans (tap offsets included)
+static int patch16_span(long long M, int H, int W) {
+  const int Wp = W + 2;
+  auto padded = [&](long long m) {
+    const long long b = m / (H * W), r = m - b * H * W, oy = r / W, ox = r - oy * W;
+    return (b * (H + 2) + oy + 1) * Wp + ox + 1;
+  };
+  long long mx = 0;
+  for (long long m0 = 0; m0 < M; m0 += P16_BM) {
+    const long long last = m0 + P16_BM - 1 < M ? m0 + P16_BM - 1 : M - 1;
+    const long long v = padded(last) - padded(m0) + 2 * (Wp + 1) + 1;
+    mx = v > mx ? v : mx;
+  }
+  return (int)(mx < 0x7fffffff ? mx : 0x7fffffff);
+}
+
+int launch_conv_patch16(const half_t* in_padded, const half_t* Bt, int ldb, half_t* out, int out_padded, long long M,
+                        int N, int K, int H, int W, int C, const EpiParams& epi, hipStream_t stream) {
+  if (M == 0 || N == 0) return 0;
+  const long long nimg = M / ((long long)H * W);
+  const long long in_bytes = nimg * (H + 2) * (W + 2) * (long long)C * 2;
+  if (M % ((long long)H * W) != 0 || K != 9 * C || C % 64 != 0 || N % 256 != 0 || ldb < K || ldb % 8 != 0 ||
+      in_bytes >= 0x80000000LL || M > 0x7fffffffLL || patch16_span(M, H, W) > P16_NPR) {
+    set_error("conv_patch16: unsupported shape M=%lld N=%d K=%d %dx%dx%d", M, N, K, H, W, C);
+    return -2;
+  }
+  const int tilesM = (int)((M + P16_BM - 1) / P16_BM), tilesN = N / 256;
+  hipLaunchKernelGGL((conv3x3_f16_patch_kernel<P16_BM, P16_NPR, half_t>), dim3(tilesM * tilesN), dim3(512), 0,
+                     stream, in_padded, Bt, ldb, out, (int)M, N, K, epi, tilesM, Patch16Geom{H, W, C, out_padded, getenv("DNN_HIP_P16DBG") ? atoi(getenv("DNN_HIP_P16DBG")) : 0},
+                     (unsigned)in_bytes);
+  return check16("conv_patch16");
 }
 
 }  // namespace dnnhip

@@ -85,8 +85,10 @@ static size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
 using namespace dnnhip;
 
-enum ConvMode : int { MODE_GEMM = 0, MODE_DIRECT_A = 1, MODE_IMPLICIT = 2, MODE_DIRECT = 3, MODE_PATCH = 4 };
-static const char* kModeName[] = {"gemm", "direct_a", "implicit", "direct", "patch"};
+// MODE_PATCH16: fp16 3x3 conv on a zero-bordered input (conv3x3_f16_patch_kernel; conv6/conv7)
+enum ConvMode : int { MODE_GEMM = 0, MODE_DIRECT_A = 1, MODE_IMPLICIT = 2, MODE_DIRECT = 3, MODE_PATCH = 4,
+                      MODE_PATCH16 = 5 };
+static const char* kModeName[] = {"gemm", "direct_a", "implicit", "direct", "patch", "patch16"};
 
 struct PlanLayer {
   int type = 0;  // 0 conv, 1 pool
@@ -98,6 +100,8 @@ struct PlanLayer {
   int K = 0, Kpad = 0, Npad = 0, cfg = 0, epi_flags = 0;
   int splits = 1;  // split-K partial count (> 1: GEMM writes partials, a reduce kernel finishes)
   bool pool = false;  // a 2x2/stride-2 max pool fused into this conv
+  bool out_padded = false;  // output written zero-bordered (the next layer is MODE_PATCH16)
+  int pad_region = 0;       // which of the two padded workspace regions it writes
   int PH = 0, PW = 0;
   size_t w_off = 0, epi_off = 0;  // float offsets in the weight arena
   bool have_host = false;
@@ -132,7 +136,7 @@ struct dnn_plan {
   float* ws = nullptr;
   size_t ws_floats = 0;
   bool own_ws = false;
-  size_t act_floats = 0, col_floats = 0, slab_floats = 0, ticket_floats = 0;
+  size_t act_floats = 0, col_floats = 0, slab_floats = 0, ticket_floats = 0, pad_floats = 0;
   static constexpr size_t kZeroFloats = 64;  // zero page: source of padding taps (implicit GEMM)
   // staging for dnn_plan_run_host
   float* h_in_dev = nullptr;
@@ -226,7 +230,17 @@ static void layout(dnn_plan* p) {
   p->col_floats = align_up(col * (size_t)p->batch, 64);
   p->slab_floats = align_up(std::max(slab * (size_t)p->batch, slab_fused), 64);
   p->ticket_floats = align_up(tickets, 64);  // unsigned tickets of the fused split-K layers
-  p->ws_floats = 2 * p->act_floats + p->col_floats + p->slab_floats + p->ticket_floats + dnn_plan::kZeroFloats;
+  // zero-bordered fp16 activations feeding MODE_PATCH16 layers: two regions, written alternately
+  size_t padh = 0;
+  int npad = 0;
+  for (auto& L : p->layers)
+    if (L.out_padded) {
+      padh = std::max(padh, (size_t)p->batch * (L.out_h() + 2) * (L.out_w() + 2) * L.OC);
+      L.pad_region = npad++ & 1;
+    }
+  p->pad_floats = align_up((padh + 1) / 2, 64);
+  p->ws_floats = 2 * p->act_floats + p->col_floats + p->slab_floats + p->ticket_floats + 2 * p->pad_floats +
+                 dnn_plan::kZeroFloats;
 }
 
 extern "C" {
@@ -264,6 +278,13 @@ void dnn_plan_destroy(dnn_plan* p) {
 
 static void set_cfg(dnn_plan* p, PlanLayer& L) {
   const long long M = (long long)p->batch * L.OH * L.OW;
+  if (p->fp16 && L.mode == MODE_PATCH16) {  // one config: 192x256 tiles, no split
+    L.cfg = 0;
+    L.Kpad = L.K;
+    L.Npad = (int)align_up(L.OC, 256);
+    L.splits = 1;
+    return;
+  }
   if (p->fp16) {  // fp16 MFMA configs: BK = 64 halves, split rule on (N, K) only
     L.cfg = choose_gemm16_cfg(M, L.OC, L.K);
     if (const char* e = getenv("DNN_HIP_CFG16")) {  // tuning experiments: "K:cfg,K:cfg,..."
@@ -356,6 +377,16 @@ int dnn_plan_add_conv(dnn_plan* p, int kh, int kw, int od, int stride_h, int str
     // fp16 path: 1x1 on the input, implicit GEMM (C % 8 == 0), or conv0's direct kernel (set
     // when its 2x2/s2 pool arrives); anything else is rejected at finalize
     L.mode = one_by_one ? MODE_DIRECT_A : (L.C % 8 == 0 && kh * kw <= 30) ? MODE_IMPLICIT : MODE_GEMM;
+    // 3x3 wide layers whose producer (a separate pool or another such conv) can write a
+    // zero-bordered output: the patch kernel (input staged once per 64-channel chunk)
+    if (L.mode == MODE_IMPLICIT && !p->layers.empty() &&
+        conv_patch16_supported(L.C, od, L.H, L.W, L.OH, L.OW, kh, kw, stride_h, stride_w, L.pt, L.pl)) {
+      PlanLayer& prev = p->layers.back();
+      if (prev.type == 1 || (prev.mode == MODE_PATCH16 && !prev.pool)) {
+        L.mode = MODE_PATCH16;
+        prev.out_padded = true;
+      }
+    }
   } else if (one_by_one)
     L.mode = MODE_DIRECT_A;
   else if (p->fuse && implicit_conv_supported(L.C, kh, kw) &&
@@ -498,7 +529,9 @@ static int upload_weights(dnn_plan* p) {
     } else {
       if (hipMemcpy(tmp, L.w.data(), wb, hipMemcpyHostToDevice) != hipSuccess) rc = -1;
       if (p->fp16) {
-        if (!rc) rc = launch_pack_weights(tmp, packed32, L.K, L.OC, L.Kpad, L.Npad, 0, L.kh, L.kw, L.C, 0);
+        if (!rc)
+          rc = launch_pack_weights(tmp, packed32, L.K, L.OC, L.Kpad, L.Npad, L.mode == MODE_PATCH16 ? 3 : 0, L.kh,
+                                   L.kw, L.C, 0);
         if (!rc)
           rc = launch_f32_to_f16(packed32, reinterpret_cast<half_t*>(p->weights + L.w_off),
                                  (long long)L.Npad * L.Kpad, 0);
@@ -552,6 +585,9 @@ int dnn_plan_finalize(dnn_plan* p, int device, void* weights, void* workspace) {
   }
   // zero page at the end of the workspace (padding taps of the implicit GEMM read it)
   DNN_HIP_TRY(hipMemset(p->ws + p->ws_floats - dnn_plan::kZeroFloats, 0, dnn_plan::kZeroFloats * sizeof(float)));
+  if (p->pad_floats)  // zero borders of the padded activations (interiors are rewritten every run)
+    DNN_HIP_TRY(hipMemset(p->ws + 2 * p->act_floats + p->col_floats + p->slab_floats + p->ticket_floats, 0,
+                          2 * p->pad_floats * sizeof(float)));
   if (p->ticket_floats)  // fused split-K tickets start at zero; every launch leaves them zero
     DNN_HIP_TRY(hipMemset(p->ws + 2 * p->act_floats + p->col_floats + p->slab_floats, 0,
                           p->ticket_floats * sizeof(float)));
@@ -597,9 +633,11 @@ static int run_fp16(dnn_plan* p, int n, const float* d_in, float* d_out, hipStre
     if ((rc = launch_f32_to_f16(d_in, act[1], (long long)n * p->in_h * p->in_w * p->in_c, s))) return rc;
     cur = act[1];
   }
+  half_t* padr = reinterpret_cast<half_t*>(p->ws + 2 * p->act_floats + p->col_floats + p->slab_floats +
+                                            p->ticket_floats);
   for (int i = 0; i < nl; ++i) {
     PlanLayer& L = p->layers[i];
-    half_t* dst = act[i & 1];
+    half_t* dst = L.out_padded ? padr + (size_t)L.pad_region * p->pad_floats * 2 : act[i & 1];
     int k = L.kernel_idx;
     if (L.type == 0) {
       const float* e = p->weights + L.epi_off;
@@ -624,6 +662,9 @@ static int run_fp16(dnn_plan* p, int n, const float* d_in, float* d_out, hipStre
           rc = launch_gemm16(L.cfg, GEMM_DENSE, cur, L.C, ImplicitConv{}, wt, L.Kpad, dst, L.OC, Mc, L.OC, L.Kpad,
                              epi, s, L.splits, slab, tickets);
           break;
+        case MODE_PATCH16:
+          rc = launch_conv_patch16(cur, wt, L.Kpad, dst, L.out_padded ? 1 : 0, Mc, L.OC, L.K, L.H, L.W, L.C, epi, s);
+          break;
         case MODE_IMPLICIT: {
           ImplicitConv ic{zero, L.H, L.W, L.C, L.OH, L.OW, L.PH, L.PW, L.kh, L.kw, L.sh, L.sw, L.pt, L.pl,
                           L.pool ? 1 : 0};
@@ -644,7 +685,7 @@ static int run_fp16(dnn_plan* p, int n, const float* d_in, float* d_out, hipStre
     } else {
       PoolGeom g{n, L.H, L.W, L.C, L.OH, L.OW, L.kh, L.kw, L.sh, L.sw, L.pt, L.pl, 0};
       if ((rc = record(p, k, s))) return rc;
-      if ((rc = launch_maxpool16(cur, dst, g, s))) return rc;
+      if ((rc = launch_maxpool16(cur, dst, g, s, L.out_padded ? 1 : 0))) return rc;
     }
     cur = dst;
   }

@@ -978,3 +978,53 @@ def golden_frames_0():
     import os
     from conftest import GOLDEN
     return np.load(os.path.join(GOLDEN, "net_frame0.npy"))
+
+
+PATCH16_CASES = [
+    # B, H, W, C, od1, od2: pool (2x2 s1) -> conv3x3 C->od1 -> conv3x3 od1->od2, both on the fp16
+    # patch kernel (zero-bordered activations written by the pool and by the first conv)
+    (64, 13, 13, 256, 512, 512),   # conv6-like at batch 64 (57 tiles of 192 rows)
+    (3, 13, 13, 128, 256, 256),    # few rows: one partial tile per N panel
+    (2, 9, 11, 64, 256, 512),      # non-square frame, 2 x 99 rows
+]
+
+
+@pytest.mark.parametrize("case", PATCH16_CASES)
+def test_fp16_patch_conv_vs_oracle(monkeypatch, case):
+    """conv3x3_f16_patch_kernel (input staged once per 64-channel chunk for all 9 taps, weights
+    straight to registers): whole chain within the fp16 layer tolerance of the fp32 oracle,
+    both convs on mode patch16, and batch rows independent of the batch (row 0 alone == row 0
+    of the batch, bit for bit)."""
+    B, H, W, C, od1, od2 = case
+    rng = np.random.default_rng(B + C + od1)
+    x = rng.standard_normal((B, H, W, C)).astype(np.float32)
+    k1 = (rng.standard_normal((3, 3, C, od1)) * np.sqrt(2.0 / (9 * C))).astype(np.float32)
+    k2 = (rng.standard_normal((3, 3, od1, od2)) * np.sqrt(2.0 / (9 * od1))).astype(np.float32)
+    bn = lambda n: (rng.standard_normal(n).astype(np.float32) * 0.1, rng.uniform(0.5, 1.5, n).astype(np.float32),
+                    rng.uniform(0.5, 1.5, n).astype(np.float32))
+    b1, bn1 = rng.standard_normal(od1).astype(np.float32) * 0.1, bn(od1)
+    b2, bn2 = rng.standard_normal(od2).astype(np.float32) * 0.1, bn(od2)
+
+    def graph(shape):
+        g = dnn_hip.DnnGraphBuilder()
+        y = g.create_input(list(shape))
+        y = g.create_max_pool2d(y, [1, 2, 2, 1], [1, 1, 1, 1], "SAME")
+        for k, b, n in ((k1, b1, bn1), (k2, b2, bn2)):
+            y = g.create_conv2d(y, k, [1, 1, 1, 1], "SAME")
+            y = g.create_bias_add(y, b)
+            y = g.create_batch_norm(y, *n, 1e-5)
+            y = g.create_leaky_relu(y)
+        g.set_out_node(y)
+        return g
+
+    monkeypatch.setenv("DNN_HIP_PATCH16", "1")
+    eng = dnn_hip.DnnInferenceEngine(graph(x.shape), False, precision="fp16")
+    assert eng.plan().describe().count("mode=patch16") == 2
+    y = eng.run(x)
+    ref = R.max_pool2d(x, [1, 2, 2, 1], [1, 1, 1, 1], "SAME")
+    for k, b, n in ((k1, b1, bn1), (k2, b2, bn2)):
+        ref = R.leaky_relu(R.batch_norm(R.bias_add(R.conv2d(ref, k), b), *n, 1e-5))
+    assert R.normwise_err(y, ref) < 2 * FP16_LAYER_TOL
+    y0 = dnn_hip.DnnInferenceEngine(graph((1,) + x.shape[1:]), False, precision="fp16").run(x[:1])
+    assert np.array_equal(y0, y[:1])
+    assert np.array_equal(eng.run(x), y)
