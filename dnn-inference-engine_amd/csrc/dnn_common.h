@@ -131,7 +131,8 @@ int choose_splitk(int N, int K, bool combine = false);
 // Latency plans (dnn_plan_set_latency_mode): tile config and split count of a small-M layer so
 // that its work units fill the chip (depends on M: batch-1 results are not bit-equal to a
 // batch plan's rows).  In: the batch rule's (cfg, splits); kept when they fill the chip.
-void choose_latency_plan(long long M, int N, int K, int* cfg, int* splits);
+void choose_latency_plan(long long M, int N, int K, int* cfg, int* splits, bool pool);
+bool generic_combine_cfg(int cfg);
 // tile order of a GEMM launch (SplitK::nmajor): 1 = N-major
 int nmajor_order(int N, int tilesN);
 // Persistent implicit GEMM for unsplit short-K layers (gemm_persist.h; DNN_HIP_PERSIST=0 off):

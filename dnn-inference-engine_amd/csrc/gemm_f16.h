@@ -62,8 +62,8 @@ gemm_f16_glds_kernel(const half_t* __restrict__ A, int lda, const half_t* __rest
     K = sk.steps * BK;
     if (!sk.tickets) slab += split_idx * sk.slab;
   }
-  int tm_, tn_;
-  tile_coords(tile, tilesN, sk, tm_, tn_);
+  const int2 tc = tile_coords(tile, tilesN, sk);
+  const int tm_ = tc.x, tn_ = tc.y;
   const int m0 = tm_ * BM, n0 = tn_ * BN;
   const int lane = threadIdx.x & 63;
   const int wid = wave_uniform(threadIdx.x >> 6);

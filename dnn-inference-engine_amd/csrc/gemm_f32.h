@@ -420,15 +420,11 @@ struct SplitK {
 
 // tile index -> (M tile, N tile): M-major (consecutive tiles walk N) or N-major (an XCD's
 // contiguous range of tiles shares one weight panel, which then stays in its L2)
-__device__ __forceinline__ void tile_coords(int tile, int tilesN, const SplitK& sk, int& tm, int& tn) {
-  if (sk.nmajor) {
-    const int tilesM = sk.ntile / tilesN;
-    tn = tile / tilesM;
-    tm = tile - tn * tilesM;
-  } else {
-    tm = tile / tilesN;
-    tn = tile - tm * tilesN;
-  }
+__device__ __forceinline__ int2 tile_coords(int tile, int tilesN, const SplitK& sk) {  // (tm, tn), by value:
+  // results through references made the compiler spill them to scratch
+  const int tilesM = sk.ntile / tilesN;
+  const int a = sk.nmajor ? tile / tilesM : tile / tilesN;
+  return sk.nmajor ? make_int2(tile - a * tilesM, a) : make_int2(a, tile - a * tilesN);
 }
 
 // Sum of the split-K partials in split order, ((p0 + p1) + p2) ..., then the fused epilogue.
@@ -596,7 +592,7 @@ __device__ __forceinline__ bool splitk_sum(typename Mfma<MF>::acc_t (&acc)[TM][T
   }
   __syncthreads();
   if (!*lds_word) return false;
-  // partials of up to 8 splits in flight at once (uniform branches, no wait between the
+  // partials of up to 4 splits in flight at once (uniform branches, no wait between the
   // loads), then added in split order
 #pragma unroll
   for (int i = 0; i < TM; ++i)
@@ -606,10 +602,10 @@ __device__ __forceinline__ bool splitk_sum(typename Mfma<MF>::acc_t (&acc)[TM][T
 #pragma unroll
       for (int q = 0; q < Q; ++q)
         own_v[q] = f32x4{acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]};
-      for (int s0 = 0; s0 < S; s0 += 8) {
-        f32x4 p[8][Q];
+      for (int s0 = 0; s0 < S; s0 += 4) {
+        f32x4 p[4][Q];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
+        for (int u = 0; u < 4; ++u) {
           const int ss = s0 + u;
           if (ss < S && ss != s) {
             const float* src = slab + ((long long)ss * sk.ntile + tile) * TILE_F;
@@ -618,7 +614,7 @@ __device__ __forceinline__ bool splitk_sum(typename Mfma<MF>::acc_t (&acc)[TM][T
           }
         }
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
+        for (int u = 0; u < 4; ++u) {
           const int ss = s0 + u;
           if (ss < S) {
 #pragma unroll
@@ -655,7 +651,9 @@ __device__ __forceinline__ void lds_dma16_buf(__amdgpu_buffer_rsrc_t r, unsigned
 }
 
 // MODE 0: dense A (col buffer or 1x1 input), MODE 1: implicit conv, MODE 2: implicit + pool.
-template <int BM, int BN, int WM, int WN, int MF, int NS, int MODE, bool ABUF = false>
+// GEN: the any-split / pool-split combine (latency plans) compiled in; a separate
+// instantiation, since its registers would cost the batch configs their occupancy
+template <int BM, int BN, int WM, int WN, int MF, int NS, int MODE, bool ABUF = false, bool GEN = false>
 __global__ void __launch_bounds__(WM* WN * 64)
 gemm_f32_glds_kernel(const float* __restrict__ A, int lda, const float* __restrict__ Bt, int ldb,
                      float* __restrict__ C, int ldc, int M, int N, int K, EpiParams epi, int tilesN,
@@ -686,9 +684,8 @@ gemm_f32_glds_kernel(const float* __restrict__ A, int lda, const float* __restri
     if (!sk.tickets) C += split * sk.slab;
     epi.flags = 0;  // raw partial sums; the reduce kernel / the combine applies the epilogue
   }
-  int tm_, tn_;
-  tile_coords(tile, tilesN, sk, tm_, tn_);
-  const int m0 = tm_ * BM, n0 = tn_ * BN;
+  const int2 tc = tile_coords(tile, tilesN, sk);
+  const int m0 = tc.x * BM, n0 = tc.y * BN;
   const int lane = threadIdx.x & 63;
   const int wid = wave_uniform(threadIdx.x >> 6);
   const int wm = wid / WN, wn = wid - (wid / WN) * WN;
@@ -877,13 +874,16 @@ gemm_f32_glds_kernel(const float* __restrict__ A, int lda, const float* __restri
     wait_lgkm0();
     stage = stage + 1 == NS ? 0 : stage + 1;
   }
-  if (sk.steps > 0 && sk.tickets && (MODE == 2 || sk.splits > 3)) {
-    // latency plans (any split count) and pool-fused split layers: the last split sums, then
-    // the normal store path below runs with the real epilogue
-    if (!splitk_sum<MF, TM, TN, NW>(acc, C, sk, split, tile, wid, lane, reinterpret_cast<unsigned*>(smem))) return;
-    epi.flags = sk.flags;
-    C = sk.out;
-    ldc = sk.ldo;
+  if constexpr (GEN) {  // the launcher picks this instantiation for > 3 splits or a pool-fused split
+    static_assert(TM * TN * MM::REGS <= 32, "the any-split combine is for small wave tiles");
+    if (sk.steps > 0 && sk.tickets && (MODE == 2 || sk.splits > 3)) {
+      // latency plans (any split count) and pool-fused split layers: the last split sums, then
+      // the normal store path below runs with the real epilogue
+      if (!splitk_sum<MF, TM, TN, NW>(acc, C, sk, split, tile, wid, lane, reinterpret_cast<unsigned*>(smem))) return;
+      epi.flags = sk.flags;
+      C = sk.out;
+      ldc = sk.ldo;
+    }
   }
   if constexpr (MODE == 2) {
     store_tile_pool<MF, TM, TN, WTM, WTN>(acc, C, ldc, M, N, m0, n0, wm, wn, lane, epi, ic);

@@ -347,7 +347,7 @@ int choose_splitk(int N, int K, bool combine) {
 // units), conv5 -> x 9, conv4 -> x 4, conv3 -> x 3, conv8 -> 32x64 x 4 (tools/lat_cfg_sweep_job.sh:
 // every tile/split choice of conv7 lands within 0.050-0.060 ms; the split-K combine's chain of
 // memory round trips costs ~5 us per layer).
-void choose_latency_plan(long long M, int N, int K, int* cfg, int* splits) {
+void choose_latency_plan(long long M, int N, int K, int* cfg, int* splits, bool pool) {
   if (*cfg < GEMM_128x128_K32) return;
   const char* e = getenv("DNN_HIP_LAT_UNITS");
   const long long target = e && atoi(e) > 0 ? atoi(e) : 256;
@@ -366,10 +366,11 @@ void choose_latency_plan(long long M, int N, int K, int* cfg, int* splits) {
   int best_cfg = *cfg, best_s = *splits;
   for (int c : cand) {
     if (c < 0 || K % kCfgs[c].bk != 0) continue;
+    const bool any_split = generic_combine_cfg(c);  // else only the batch combine's 2..3 splits
     const int nk = K / kCfgs[c].bk;
     const long long tiles = splitk_tiles(c, M, N);
     for (int sp = 1; sp <= 32; ++sp) {
-      if (nk % sp != 0 || (sp > 1 && nk / sp < minsteps)) continue;
+      if (nk % sp != 0 || (sp > 1 && nk / sp < minsteps) || (!any_split && (sp > 3 || pool))) continue;
       const long long units = tiles * sp;
       const double eff = (double)units / (double)(target * ((units + target - 1) / target));
       if (eff > best_eff + 1e-9 ||
@@ -391,6 +392,24 @@ template <int MODE, bool ABUF>
 static int launch_glds_t(int cfg, const float* A, int lda, const float* Bt, int ldb, float* C, int ldc, int m, int N,
                          int Kpad, const EpiParams& epi, int tilesN, const ImplicitConv& ic, const SplitK& sk,
                          const BufDesc& bd, dim3 grid, hipStream_t stream) {
+  const bool gen = sk.steps > 0 && sk.tickets && (MODE == 2 || sk.splits > 3);
+  if (gen) {  // latency plans: the any-split / pool-split combine (small-wave-tile configs only)
+#define DNN_GLDS_GEN(BM_, BN_, WM_, WN_, MF_, NS_)                                                                   \
+  hipLaunchKernelGGL((gemm_f32_glds_kernel<BM_, BN_, WM_, WN_, MF_, NS_, MODE, ABUF, true>), grid, dim3(WM_ * WN_ * 64), \
+                     0, stream, A, lda, Bt, ldb, C, ldc, m, N, Kpad, epi, tilesN, ic, sk, bd)
+    switch (cfg) {
+      case GEMM_64x128_K32: DNN_GLDS_GEN(64, 128, 2, 2, 32, 2); break;
+      case GEMM_G64x32_K32: DNN_GLDS_GEN(64, 32, 4, 1, 16, 2); break;
+      case GEMM_G32x128_NS4: DNN_GLDS_GEN(32, 128, 1, 4, 32, 4); break;
+      case GEMM_G32x64_NS4: DNN_GLDS_GEN(32, 64, 1, 2, 32, 4); break;
+      case GEMM_64x128_NS3: DNN_GLDS_GEN(64, 128, 2, 2, 32, 3); break;
+      default:
+        set_error("gemm: cfg %d has no any-split combine", cfg);
+        return -2;
+    }
+#undef DNN_GLDS_GEN
+    return check_launch("gemm_glds_gen");
+  }
 #define DNN_GLDS(BM_, BN_, WM_, WN_, MF_, NS_)                                                                      \
   hipLaunchKernelGGL((gemm_f32_glds_kernel<BM_, BN_, WM_, WN_, MF_, NS_, MODE, ABUF>), grid, dim3(WM_ * WN_ * 64), 0, \
                      stream, A, lda, Bt, ldb, C, ldc, m, N, Kpad, epi, tilesN, ic, sk, bd)
@@ -444,6 +463,13 @@ int nmajor_order(int N, int tilesN) {
   return (e && e[0] == '1' && tilesN > 1) ? 1 : 0;
 }
 
+// configs whose waves hold <= 32 accumulator registers: the only ones with the any-split /
+// pool-split combine compiled in (gemm_f32_glds_kernel)
+bool generic_combine_cfg(int cfg) {
+  return cfg == GEMM_G32x128_NS4 || cfg == GEMM_G32x64_NS4 || cfg == GEMM_64x128_K32 || cfg == GEMM_G64x32_K32 ||
+         cfg == GEMM_64x128_NS3;
+}
+
 // grid and SplitK descriptor for `splits` (> 1: the kernel writes raw partials to `slab`;
 // with `tickets` it also combines them itself into C)
 static int split_setup(int cfg, long long M, int N, int Kpad, int splits, float* slab, unsigned* tickets, float* C,
@@ -459,6 +485,10 @@ static int split_setup(int cfg, long long M, int N, int Kpad, int splits, float*
       return -2;
     }
     *sk = SplitK{Kpad / 32 / splits, *grid, M * (long long)N};
+    if (tickets && splits > 3 && !generic_combine_cfg(cfg)) {
+      set_error("gemm: %d-way split combine needs a small-wave-tile config (cfg %d)", splits, cfg);
+      return -2;
+    }
     if (tickets) {
       if (splits > 32) {
         set_error("gemm: fused split-K combine supports 2..32 splits (got %d)", splits);
@@ -534,7 +564,7 @@ int launch_gemm_implicit(int cfg, int mode, const float* in, const ImplicitConv&
   }
   const CfgInfo ci = kCfgs[cfg];
   if (Kpad % ci.bk != 0 || !implicit_conv_supported(ic.C, ic.kh, ic.kw) || M > 0x7fffffffLL || !ic.zero ||
-      (mode == GEMM_IMPLICIT_POOL && (M % 4 != 0 || (splits > 1 && !tickets)))) {
+      (mode == GEMM_IMPLICIT_POOL && (M % 4 != 0 || (splits > 1 && (!tickets || !generic_combine_cfg(cfg)))))) {
     set_error("gemm_implicit: unsupported shape M=%lld C=%d Kpad=%d splits=%d", M, ic.C, Kpad, splits);
     return -2;
   }
@@ -598,7 +628,14 @@ static int launch_persist_t(const float* Bt, int ldb, float* C, int ldc, int M, 
   return check_launch("gemm_persist");
 }
 
-bool persist_enabled() { return !getenv_flag_off("DNN_HIP_PERSIST"); }
+// DNN_HIP_PERSIST: 0 off, 1 (default) on the configs where it measured faster (256x64: conv2
+// 0.236 -> 0.228 ms; on 64x128 the static tile split lost to the hardware's dynamic one, conv3
+// 0.214 -> 0.224), 2 on every covered config (tests, experiments)
+static int persist_level() {
+  const char* e = getenv("DNN_HIP_PERSIST");
+  return e ? atoi(e) : 1;
+}
+bool persist_enabled() { return persist_level() > 0; }
 
 // Persistent launch of an unsplit implicit conv on the batch configs conv2-conv4 use;
 // returns -3 (caller falls back to launch_gemm_implicit) when the shape or config is not one
@@ -626,12 +663,18 @@ int launch_gemm_persist(int cfg, int mode, const float* in, const ImplicitConv& 
   const BufDesc bd{in - (size_t)(ic.W + 1) * ic.C, (unsigned)a_bytes, (unsigned)b_bytes};
   const int m = (int)M, nt = (int)ntiles;
   const unsigned ob = (unsigned)o_bytes;
-#define DNN_PERSIST(BM_, BN_, WM_, WN_, MF_, NS_)                                                                      \
+#define DNN_PERSIST_N(BM_, BN_, WM_, WN_, MF_, NS_, NTN_)                                                              \
   return mode == GEMM_IMPLICIT                                                                                        \
-             ? launch_persist_t<BM_, BN_, WM_, WN_, MF_, NS_, 1, 2>(Bt, ldb, C, ldc, m, N, Kpad, epi, tilesN, nt, ic, bd, \
-                                                                    ob, stream)                                       \
-             : launch_persist_t<BM_, BN_, WM_, WN_, MF_, NS_, 2, 2>(Bt, ldb, C, ldc, m, N, Kpad, epi, tilesN, nt, ic, bd, \
-                                                                    ob, stream)
+             ? launch_persist_t<BM_, BN_, WM_, WN_, MF_, NS_, 1, NTN_>(Bt, ldb, C, ldc, m, N, Kpad, epi, tilesN, nt, ic,  \
+                                                                       bd, ob, stream)                                \
+             : launch_persist_t<BM_, BN_, WM_, WN_, MF_, NS_, 2, NTN_>(Bt, ldb, C, ldc, m, N, Kpad, epi, tilesN, nt, ic,  \
+                                                                       bd, ob, stream)
+#define DNN_PERSIST(BM_, BN_, WM_, WN_, MF_, NS_)                                                                      \
+  if (tilesN == 1) {                                                                                                  \
+    DNN_PERSIST_N(BM_, BN_, WM_, WN_, MF_, NS_, 1);                                                                   \
+  }                                                                                                                   \
+  DNN_PERSIST_N(BM_, BN_, WM_, WN_, MF_, NS_, 2)
+  if (cfg != GEMM_G256x64_K32 && persist_level() < 2) return -3;
   switch (cfg) {
     case GEMM_G256x64_K32: DNN_PERSIST(256, 64, 4, 2, 32, 2);
     case GEMM_64x128_K32: DNN_PERSIST(64, 128, 2, 2, 32, 2);
@@ -639,6 +682,7 @@ int launch_gemm_persist(int cfg, int mode, const float* in, const ImplicitConv& 
     default: return -3;
   }
 #undef DNN_PERSIST
+#undef DNN_PERSIST_N
 }
 
 int launch_splitk_reduce(const float* slab, int splits, long long M, int N, float* C, int ldc,

@@ -317,7 +317,7 @@ static void set_cfg(dnn_plan* p, PlanLayer& L) {
   if (p->latency && fused_splitk(p) && L.Kpad == L.K) {
     // a tile config and split for this M when the batch rule leaves the chip idle
     int cfg = L.cfg, sp = L.splits;
-    choose_latency_plan(M, L.OC, L.K, &cfg, &sp);
+    choose_latency_plan(M, L.OC, L.K, &cfg, &sp, false);
     if (const char* e = getenv("DNN_HIP_SPLIT")) {  // tuning experiments: "K:splits,..."
       for (const char* q = e; *q;) {
         int k = 0, v = 0, n = 0;
@@ -459,7 +459,8 @@ int dnn_plan_add_max_pool(dnn_plan* p, int kh, int kw, int stride_h, int stride_
     PlanLayer& prev = p->layers.back();
     // (latency plans: a split implicit conv keeps its split, the combine pools)
     if (prev.type == 0 && !prev.pool &&
-        (prev.splits == 1 || (prev.mode == MODE_IMPLICIT && !p->fp16 && fused_splitk(p)))) {
+        (prev.splits == 1 ||
+         (prev.mode == MODE_IMPLICIT && !p->fp16 && fused_splitk(p) && generic_combine_cfg(prev.cfg)))) {
       bool ok = false;
       if (prev.mode == MODE_IMPLICIT) {
         ok = true;

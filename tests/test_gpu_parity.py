@@ -940,7 +940,7 @@ def test_persistent_gemm_equals_tile_kernel(monkeypatch, case):
     if C == 128:
         monkeypatch.setenv("DNN_HIP_CFG", "1152:4")  # 64x128: 1352 tiles, per-N-tile epilogue params
     for on in ("1", "0"):
-        monkeypatch.setenv("DNN_HIP_PERSIST", on)
+        monkeypatch.setenv("DNN_HIP_PERSIST", "2" if on == "1" else "0")  # 2: every covered config
         eng = dnn_hip.DnnInferenceEngine(_chain(x.shape, k, **kw), False)
         outs[on] = eng.run(x)
         outs[on + "b"] = eng.run(x)
