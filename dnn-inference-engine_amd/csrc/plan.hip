@@ -144,6 +144,7 @@ struct dnn_plan {
   // timing
   bool timing = false;
   int ev_cap = 0, ev_used = 0;
+  int timing_only = -1;  // >= 0: events only around that kernel (dnn_plan_timing_begin_only)
   std::vector<hipEvent_t> ev;
   std::vector<int> ev_kernel;
   // captured forward (dnn_plan_run_graph)
@@ -613,6 +614,11 @@ int dnn_plan_weight_buffer(const dnn_plan* p, void** ptr, size_t* bytes) {
 
 static int record(dnn_plan* p, int kernel, hipStream_t s) {
   if (!p->timing) return 0;
+  if (p->timing_only >= 0) {  // one kernel: its opening event and the next one (which closes it)
+    const bool closes = p->ev_used > 0 && p->ev_kernel[p->ev_used - 1] == p->timing_only;
+    if (kernel != p->timing_only && !closes) return 0;
+    if (kernel != p->timing_only) kernel = -1;  // a pure closer opens nothing
+  }
   if (p->ev_used + 1 >= p->ev_cap) return 0;  // capacity exhausted: stop recording silently
   DNN_HIP_TRY(hipEventRecord(p->ev[p->ev_used], s));
   p->ev_kernel[p->ev_used] = kernel;
@@ -878,7 +884,17 @@ int dnn_plan_timing_begin(dnn_plan* p, int max_runs) {
   p->ev_kernel.assign(p->ev.size(), -1);
   p->ev_cap = (int)p->ev.size();
   p->ev_used = 0;
+  p->timing_only = -1;
   p->timing = true;
+  return 0;
+}
+
+int dnn_plan_timing_begin_only(dnn_plan* p, int max_runs, int kernel_idx) {
+  DNN_REQUIRE(p && kernel_idx >= 0 && kernel_idx < (int)p->kernels.size(),
+              "dnn_plan_timing_begin_only: bad kernel index %d", kernel_idx);
+  int rc = dnn_plan_timing_begin(p, max_runs);
+  if (rc) return rc;
+  p->timing_only = kernel_idx;
   return 0;
 }
 

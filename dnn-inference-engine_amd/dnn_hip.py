@@ -69,6 +69,7 @@ def _bind_plan_api(lib):
         "dnn_plan_num_kernels": (i, [vp]),
         "dnn_plan_kernel_info": (i, [vp, i, ctypes.c_char_p, i, P(ctypes.c_double), P(ctypes.c_double)]),
         "dnn_plan_timing_begin": (i, [vp, i]),
+        "dnn_plan_timing_begin_only": (i, [vp, i, i]),
         "dnn_plan_timing_end": (i, [vp, P(ctypes.c_double), P(ctypes.c_longlong)]),
     }
     for name, (res, args) in sig.items():
@@ -630,8 +631,14 @@ class Plan(object):
             out.append({"name": name.value.decode(), "flops": fl.value, "bytes": by.value})
         return out
 
-    def timing_begin(self, max_runs):
-        _check(self.lib.dnn_plan_timing_begin(self.h, int(max_runs)), "timing_begin", self.lib)
+    def timing_begin(self, max_runs, only=None):
+        """Per-kernel HIP events over the next runs; `only` = a kernel name: events around that
+        kernel alone (dnn_plan_timing_begin_only)."""
+        if only is None:
+            _check(self.lib.dnn_plan_timing_begin(self.h, int(max_runs)), "timing_begin", self.lib)
+            return
+        idx = [k["name"] for k in self.kernels()].index(only)
+        _check(self.lib.dnn_plan_timing_begin_only(self.h, int(max_runs), idx), "timing_begin_only", self.lib)
 
     def timing_end(self):
         nk = self.lib.dnn_plan_num_kernels(self.h)

@@ -113,6 +113,10 @@ int dnn_plan_num_kernels(const dnn_plan* plan);
 int dnn_plan_kernel_info(const dnn_plan* plan, int idx, char* name, int name_len, double* flops,
                          double* bytes);
 int dnn_plan_timing_begin(dnn_plan* plan, int max_runs);
+/* As dnn_plan_timing_begin, but events are recorded only around kernel `kernel_idx` (two per
+ * forward instead of one per kernel: no event packets between the other kernels); the other
+ * kernels report 0 launches at dnn_plan_timing_end. */
+int dnn_plan_timing_begin_only(dnn_plan* plan, int max_runs, int kernel_idx);
 int dnn_plan_timing_end(dnn_plan* plan, double* ms_sum, long long* launches);
 
 #pragma GCC visibility pop

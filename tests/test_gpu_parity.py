@@ -460,6 +460,15 @@ def test_plan_timing_api(yolo_b1):
     assert len(ms) == len(ks) == 10  # 10 plan kernels: conv5/6/7 combine their split-K partials in the GEMM
     assert all(c == 3 for c in cnt)
     assert all(m > 0 for m in ms)
+    # events around one kernel only (the bench's timed region): the others report no launches
+    for only in ("conv7.gemm", "conv8.gemm", "conv0.direct"):
+        plan.timing_begin(3, only=only)
+        for _ in range(3):
+            plan.run_host(x)
+        ms1, cnt1 = plan.timing_end()
+        names = [k["name"] for k in ks]
+        assert [c for n, c in zip(names, cnt1) if n != only] == [0] * 9
+        assert cnt1[names.index(only)] == 3 and ms1[names.index(only)] > 0
 
 
 # ------------------------------------------------------------------ on-GPU postprocessing
