@@ -220,6 +220,7 @@ int launch_maxpool16(const half_t* in, half_t* out, const PoolGeom& g, hipStream
 // output zero-bordered too (gemm_f16_patch.h)
 bool conv_patch16_supported(int C, int OC, int H, int W, int OH, int OW, int kh, int kw, int sh, int sw, int pt,
                             int pl);
+int patch16_pack_order();  // launch_pack_weights order of the patch kernel's MFMA shape (3 or 4)
 int launch_conv_patch16(const half_t* in_padded, const half_t* Bt, int ldb, half_t* out, int out_padded, long long M,
                         int N, int K, int H, int W, int C, const EpiParams& epi, hipStream_t stream);
 // conv0 direct kernel with an fp16 output (fp32 input frames)

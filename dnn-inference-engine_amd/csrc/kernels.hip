@@ -819,10 +819,14 @@ __global__ void pack_weights_kernel(const float* __restrict__ w, float* __restri
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
     int n = (int)(i / Kpad), k = (int)(i % Kpad);
-    if (order == 3) {  // MFMA fragment order of the order-2 K (conv_patch16): [n/32][k/16][lane][8]
+    if (order == 3) {  // MFMA fragment order of the order-2 K (conv_patch16, 32x32x16): [n/32][k/16][lane][8]
       const long long e = i & 7, lane = (i >> 3) & 63, kq = (i >> 9) % (Kpad / 16), nb = (i >> 9) / (Kpad / 16);
       n = (int)(nb * 32 + (lane & 31));
       k = (int)(kq * 16 + 8 * (lane >> 5) + e);
+    } else if (order == 4) {  // ... for 16x16x32: [n/16][k/32][lane][8]
+      const long long e = i & 7, lane = (i >> 3) & 63, kq = (i >> 9) % (Kpad / 32), nb = (i >> 9) / (Kpad / 32);
+      n = (int)(nb * 16 + (lane & 15));
+      k = (int)(kq * 32 + 8 * (lane >> 4) + e);
     }
     float v = 0.f;
     if (n < N && k < K) {

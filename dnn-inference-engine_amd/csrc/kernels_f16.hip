@@ -266,7 +266,16 @@ int launch_maxpool16(const half_t* in, half_t* out, const PoolGeom& g, hipStream
 }
 
 // ---- conv3x3_f16_patch_kernel (gemm_f16_patch.h): conv6/conv7 of the fp16 path
-constexpr int P16_BM = 192, P16_NPR = 320;
+// MFMA shape of the patch kernel: 16 (v_mfma_f32_16x16x32_f16, 176-row tiles) or 32
+// (32x32x16, 192-row tiles); DNN_HIP_P16MF overrides (experiments).  The weight packing order
+// follows it (patch16_pack_order).
+constexpr int P16_NPR = 320;
+static int p16_mf() {
+  const char* e = getenv("DNN_HIP_P16MF");
+  return e && atoi(e) == 32 ? 32 : 16;
+}
+static int p16_bm() { return p16_mf() == 32 ? 192 : 176; }
+int patch16_pack_order() { return p16_mf() == 32 ? 3 : 4; }
 constexpr bool P16_DEFAULT = true;  // measured: conv6 0.1415 -> 0.1286 ms, conv7 equal (batch 64)
 
 // DNN_HIP_PATCH16=0/1 overrides the default choice of the patch kernel for eligible layers
@@ -289,8 +298,9 @@ static int patch16_span(long long M, int H, int W) {
     return (b * (H + 2) + oy + 1) * Wp + ox + 1;
   };
   long long mx = 0;
-  for (long long m0 = 0; m0 < M; m0 += P16_BM) {
-    const long long last = m0 + P16_BM - 1 < M ? m0 + P16_BM - 1 : M - 1;
+  const int bm = p16_bm();
+  for (long long m0 = 0; m0 < M; m0 += bm) {
+    const long long last = m0 + bm - 1 < M ? m0 + bm - 1 : M - 1;
     const long long v = padded(last) - padded(m0) + 2 * (Wp + 1) + 1;
     mx = v > mx ? v : mx;
   }
@@ -307,10 +317,15 @@ int launch_conv_patch16(const half_t* in_padded, const half_t* Bt, int ldb, half
     set_error("conv_patch16: unsupported shape M=%lld N=%d K=%d %dx%dx%d", M, N, K, H, W, C);
     return -2;
   }
-  const int tilesM = (int)((M + P16_BM - 1) / P16_BM), tilesN = N / 256;
-  hipLaunchKernelGGL((conv3x3_f16_patch_kernel<P16_BM, P16_NPR, half_t>), dim3(tilesM * tilesN), dim3(512), 0,
-                     stream, in_padded, Bt, ldb, out, (int)M, N, K, epi, tilesM, Patch16Geom{H, W, C, out_padded, getenv("DNN_HIP_P16DBG") ? atoi(getenv("DNN_HIP_P16DBG")) : 0},
-                     (unsigned)in_bytes);
+  const int bm = p16_bm();
+  const int tilesM = (int)((M + bm - 1) / bm), tilesN = N / 256;
+  const Patch16Geom pg{H, W, C, out_padded};
+  if (bm == 176)
+    hipLaunchKernelGGL((conv3x3_f16_patch_kernel<176, P16_NPR, half_t, 16>), dim3(tilesM * tilesN), dim3(512), 0,
+                       stream, in_padded, Bt, ldb, out, (int)M, N, K, epi, tilesM, pg, (unsigned)in_bytes);
+  else
+    hipLaunchKernelGGL((conv3x3_f16_patch_kernel<192, P16_NPR, half_t, 32>), dim3(tilesM * tilesN), dim3(512), 0,
+                       stream, in_padded, Bt, ldb, out, (int)M, N, K, epi, tilesM, pg, (unsigned)in_bytes);
   return check16("conv_patch16");
 }
 

@@ -532,7 +532,7 @@ static int upload_weights(dnn_plan* p) {
       if (hipMemcpy(tmp, L.w.data(), wb, hipMemcpyHostToDevice) != hipSuccess) rc = -1;
       if (p->fp16) {
         if (!rc)
-          rc = launch_pack_weights(tmp, packed32, L.K, L.OC, L.Kpad, L.Npad, L.mode == MODE_PATCH16 ? 3 : 0, L.kh,
+          rc = launch_pack_weights(tmp, packed32, L.K, L.OC, L.Kpad, L.Npad, L.mode == MODE_PATCH16 ? patch16_pack_order() : 0, L.kh,
                                    L.kw, L.C, 0);
         if (!rc)
           rc = launch_f32_to_f16(packed32, reinterpret_cast<half_t*>(p->weights + L.w_off),
