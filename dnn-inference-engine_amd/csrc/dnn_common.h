@@ -220,6 +220,15 @@ int launch_maxpool16(const half_t* in, half_t* out, const PoolGeom& g, hipStream
 // output zero-bordered too (gemm_f16_patch.h)
 bool conv_patch16_supported(int C, int OC, int H, int W, int OH, int OW, int kh, int kw, int sh, int sw, int pt,
                             int pl);
+// fp32 path "x3" conv (kernels_x3.hip, gemm_x3_patch.h): fp32 operands split exactly into three
+// bf16 pieces, six bf16 MFMA products, fp32 accumulation; activations in split planes
+// [B][H+2][W+2][C/32][3][32] bf16 (zero-bordered), weights packed by launch_pack_weights_x3
+bool conv_x3_supported(int C, int OC, int H, int W, int OH, int OW, int kh, int kw, int sh, int sw, int pt, int pl);
+size_t x3_act_bytes(long long nimg, int H, int W, int C);
+int launch_maxpool_x3(const float* in, unsigned short* out, const PoolGeom& g, hipStream_t s);
+int launch_pack_weights_x3(const float* w, unsigned short* out, int K, int N, int Npad, int C, hipStream_t s);
+int launch_conv_x3(const unsigned short* in_split, const unsigned short* Bt, float* out, unsigned short* out_split,
+                   long long M, int N, int Npad, int K, int H, int W, int C, const EpiParams& epi, hipStream_t stream);
 int patch16_pack_order();  // launch_pack_weights order of the patch kernel's MFMA shape (3 or 4)
 int launch_conv_patch16(const half_t* in_padded, const half_t* Bt, int ldb, half_t* out, int out_padded, long long M,
                         int N, int K, int H, int W, int C, const EpiParams& epi, hipStream_t stream);

@@ -1,0 +1,251 @@
+// fp32 3x3 conv on the bf16 MFMA with exact three-way operand splits ("x3"), for the long-K,
+// wide-N layers of the fp32 path (conv6/conv7 of YOLOv2-tiny), device code only.
+//
+// Why: the fp32 MFMA (v_mfma_f32_32x32x2f32) peaks at 157 TFLOP/s, the bf16 one at 2.5 PF.
+// Every finite fp32 x with |x| >= 2^-100 is EXACTLY x0 + x1 + x2 with x0 = bf16(x), x1 =
+// bf16(x - x0), x2 = bf16(x - x0 - x1) (round-to-nearest: 8 + 8 + 8 significand bits cover
+// 24, and every difference is exact).  A product a*b is then the sum of the nine a_i*b_j; the
+// six with i + j <= 2 are formed (each exact in the fp32 accumulator's input), the three
+// dropped ones are <= 2^-24 |a b| together with rounding.  tools/bf16x6_probe.hip measured the
+// result against float64 at K = 288 / 2304 / 9216: max |err| / sum|a b| 1.7e-7 - 3.4e-7,
+// the fp32 MFMA (which reproduces a sequential fp32 FMA chain) 2.1e-7 - 3.0e-7: the same
+// accuracy class as fp32, 6 bf16 MFMAs per fp32 product instead of 1/16 of the rate.
+//
+// Layout (written by the producers: maxpool_x3_kernel, this kernel's own epilogue):
+// activations zero-bordered [B][H+2][W+2] rows, each row C/32 chunks of [3 pieces][32 ch]
+// bf16 (192 B per chunk).  Weights (pack_weights_x3_kernel): [n/16][step][piece][lane][8]
+// with step = chunk * 9 + tap over 32-channel chunks, i.e. MFMA fragment order of
+// v_mfma_f32_16x16x32_bf16 (n = 16 nb + (lane & 15), k = 8 (lane >> 4) + e).
+// Per output and 32-channel step: the corrections a2b0 + a1b1 + a0b2 + a1b0 + a0b1 summed from
+// zero, then (acc + a0b0) + corrections; steps chunk-major, tap-minor.  The order depends on
+// (N, K) only, so batch rows are bit-identical to batch-1 runs; it is not the fp32 MFMA
+// path's order (DNN_HIP_X3=0 selects that path).
+//
+// Structure (as conv3x3_f16_patch_kernel, MF = 16): BM x 256 tiles, 8 waves of BM x 32; a tile
+// of BM consecutive output pixels reads one contiguous run of <= NPR padded rows per chunk,
+// staged once into a double-buffered LDS patch (NPR x 192 B) and reused by all 9 taps; the
+// weight fragments go straight from L2 to registers two taps ahead.
+#pragma once
+#include "gemm_f16.h"
+
+namespace dnnhip {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned short bf16_bits;
+
+struct X3Geom {
+  int H, W, C;     // conv input = output spatial size (3x3, stride 1, SAME), channels
+  int out_split;   // 1: write split planes into a zero-bordered [B][H+2][W+2] buffer (next x3 layer)
+};
+
+__device__ __forceinline__ unsigned short bf16_rn(float x) { return __builtin_bit_cast(unsigned short, (__bf16)x); }
+__device__ __forceinline__ float bf16_f(unsigned short h) { return __builtin_bit_cast(float, (unsigned)h << 16); }
+// x = bf16_f(s0) + bf16_f(s1) + bf16_f(s2) exactly (finite x, |x| >= 2^-100)
+__device__ __forceinline__ void split3(float x, unsigned short& s0, unsigned short& s1, unsigned short& s2) {
+  s0 = bf16_rn(x);
+  const float r1 = x - bf16_f(s0);
+  s1 = bf16_rn(r1);
+  s2 = bf16_rn(r1 - bf16_f(s1));
+}
+
+__device__ __forceinline__ f32x4 mfma16_bf16(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+template <int BM, int NPR>
+__global__ void __launch_bounds__(512, 1)
+conv3x3_x3_patch_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __restrict__ Bt, float* __restrict__ out,
+                        bf16_bits* __restrict__ out_split, int M, int N, int K, EpiParams epi, int tilesM, X3Geom g,
+                        unsigned in_bytes, unsigned b_bytes) {
+  constexpr int BN = 256, TM = BM / 16, RB = 192;  // 8 waves of BM x 32; patch row bytes
+  constexpr int SR = 32, PPT = NPR / SR;           // staging: 384 threads = 32 rows x 12 slots
+  static_assert(BM % 16 == 0 && NPR % SR == 0 && PPT >= 1 && PPT <= 16, "shape");
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * NPR * RB];
+
+  const int lane = threadIdx.x & 63;
+  const int wid = wave_uniform(threadIdx.x >> 6);
+  // tiles N-major inside each XCD's contiguous range: the XCD's CUs share one weight panel
+  const int tile = xcd_tile(blockIdx.x, gridDim.x);
+  const int tn = tile / tilesM, tm = tile - tn * tilesM;
+  const int m0 = tm * BM, n0 = tn * BN + wid * 32;  // this wave's 32 columns
+  const int Wp = g.W + 2, HWo = g.H * g.W;
+  auto padded = [&](int m) {
+    const int b = m / HWo, r = m - b * HWo, oy = r / g.W, ox = r - oy * g.W;
+    return (b * (g.H + 2) + oy + 1) * Wp + ox + 1;
+  };
+  const int P0 = padded(m0) - (Wp + 1);  // first patch row (>= 0: p(0) = Wp + 1)
+
+  // A fragment of row-block i: lane's output row 16 i + fr -> patch row of tap (1, 1); its k
+  // slot fq (8 channels) of piece p sits at row*192 + 64 p + 16 (fq ^ ((row >> 2) & 3))
+  // (16 consecutive rows hit 16 distinct 16-B bank groups)
+  const int fr = lane & 15, fq = lane >> 4;
+  int prow[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    int m = m0 + 16 * i + fr;
+    m = m < M ? m : M - 1;
+    prow[i] = padded(m) - P0;
+  }
+
+  // patch staging: thread (tid % 384) owns slot ss = t % 12 of rows t / 12 + 32 u (waves 6, 7
+  // repeat waves 0, 1: no branch, same bytes to the same LDS address)
+  const int st = threadIdx.x % 384, srow = st / 12, ss = st - srow * 12;
+  const int rowB = 6 * g.C;  // bytes per padded row (all chunks)
+  const unsigned pvo = (unsigned)((P0 + srow) * rowB + ss * 16);
+  const int pdst = srow * RB + (ss >> 2) * 64 + 16 * ((ss & 3) ^ ((srow >> 2) & 3));
+  const auto rsA = __builtin_amdgcn_make_buffer_rsrc((void*)in, 0, (int)in_bytes, 0x00020000);
+  u32x4 pst[PPT];
+  auto load_piece = [&](int chunk, int u) {
+    pst[u] = __builtin_amdgcn_raw_buffer_load_b128(rsA, pvo, chunk * RB + u * SR * rowB, 0);
+  };
+  auto store_piece = [&](int buf, int u) {
+    *reinterpret_cast<u32x4*>(smem + buf * NPR * RB + pdst + u * SR * RB) = pst[u];
+  };
+
+  // weight fragments: per (16-column block, step) 3 pieces x 1 KiB, two taps ahead
+  const int nk = K / 32, nch = nk / 9;
+  const unsigned bvo = (unsigned)((n0 / 16) * nk * 3072 + lane * 16);
+  const int bjs = nk * 3072;  // second 16-column block of the wave
+  const auto rsB = __builtin_amdgcn_make_buffer_rsrc((void*)Bt, 0, (int)b_bytes, 0x00020000);
+  bf16x8 bq[3][3][2];  // [step % 3][piece][column block]
+#pragma unroll
+  for (int a = 0; a < 3; ++a)
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bq[a][p][j] = bf16x8{};
+  // unconditional (past the last step: the descriptor's zeros or another panel, never used):
+  // a conditional load would leave every later wait to drain the fresh loads too
+  auto load_b = [&](int s, bf16x8 (&dst)[3][2]) {
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        dst[p][j] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rsB, bvo, s * 3072 + p * 1024 + j * bjs, 0));
+  };
+
+  f32x4 acc[TM][2];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int u = 0; u < PPT; ++u) load_piece(0, u);
+  load_b(0, bq[0]);
+  load_b(1, bq[1]);
+#pragma unroll
+  for (int u = 0; u < PPT; ++u) store_piece(0, u);
+  wait_lgkm0();
+  __syncthreads();
+
+  // piece u of patch j+1: loaded at tap L(u) = 8u / PPT of chunk j, written at tap L(u) + 1
+  auto frag = [&](const unsigned char* P, int i, int toff, bf16x8 (&a)[3]) {
+    int pr = prow[i];
+    asm volatile("" : "+v"(pr));  // keep the taps' addresses from being hoisted
+    const int row = pr + toff;
+    const unsigned char* q = P + row * RB + 16 * (fq ^ ((row >> 2) & 3));
+#pragma unroll
+    for (int p = 0; p < 3; ++p) a[p] = *reinterpret_cast<const bf16x8*>(q + 64 * p);
+  };
+  for (int j = 0; j < nch; ++j) {
+    const unsigned char* P = smem + (j & 1) * NPR * RB;
+    bf16x8 af[2][3];
+    frag(P, 0, -(Wp + 1), af[0]);
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int s = 9 * j + t;
+      const int toff = (t / 3 - 1) * Wp + (t % 3 - 1);
+      const int toff_next = ((t + 1) / 3 - 1) * Wp + ((t + 1) % 3 - 1);
+      // taps are scheduling regions (the scheduler would sink a piece's load to its store)
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int u = 0; u < PPT; ++u)
+        if ((8 * u) / PPT == t) load_piece(j + 1, u);
+      load_b(s + 2, bq[(t + 2) % 3]);
+#pragma unroll
+      for (int u = 0; u < PPT; ++u)
+        if ((8 * u) / PPT + 1 == t) store_piece((j + 1) & 1, u);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int cur = i & 1, nxt = cur ^ 1;
+        // the next fragment (row-block i + 1 of this tap, or row-block 0 of the next tap) is
+        // read while this one's 12 MFMAs run
+        if (i + 1 < TM)
+          frag(P, i + 1, toff, af[nxt]);
+        else if (t < 8)
+          frag(P, 0, toff_next, af[nxt]);
+        const bf16x8(&b)[3][2] = bq[t % 3];
+        // the five correction products (<= 2^-7 of the main one) summed from zero in their own
+        // chain, then one add: the accumulator sees two roundings per step instead of six
+        // (tests/test_gpu_parity.py::test_x3_conv_vs_oracle; the bf16 MFMA's internal sum is
+        // not round-to-nearest at the accumulator's magnitude)
+#pragma unroll
+        for (int jb = 0; jb < 2; ++jb) {
+          f32x4 c = mfma16_bf16(af[cur][2], b[0][jb], f32x4{0.f, 0.f, 0.f, 0.f});
+          c = mfma16_bf16(af[cur][1], b[1][jb], c);
+          c = mfma16_bf16(af[cur][0], b[2][jb], c);
+          c = mfma16_bf16(af[cur][1], b[0][jb], c);
+          c = mfma16_bf16(af[cur][0], b[1][jb], c);
+          const f32x4 m = mfma16_bf16(af[cur][0], b[0][jb], acc[i][jb]);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[i][jb][r] = m[r] + c[r];
+        }
+        // row-block boundaries are scheduling regions: only one block's correction chains
+        // live at a time (the other wave on the SIMD covers the adds' wait for the MFMAs)
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      // TM is odd: the tap's last fragment set lands in af[TM & 1]; re-home it for the next tap
+      if constexpr (TM & 1) {
+        if (t < 8) {
+#pragma unroll
+          for (int p = 0; p < 3; ++p) af[0][p] = af[1][p];
+        }
+      }
+    }
+    if (j + 1 < nch) {  // patch j+1 written by every wave; every wave done reading patch j
+      wait_lgkm0();
+      raw_barrier();
+    }
+  }
+
+  // epilogue: the reference's fp32 epilogue, then fp32 [M][N] or the split planes of the next
+  // x3 layer's zero-bordered input; output row indices tabulated once in LDS
+  int* orow = reinterpret_cast<int*>(smem);
+  __syncthreads();  // every wave is done with the patches
+  if (threadIdx.x < BM) {
+    const int m = m0 + threadIdx.x;
+    orow[threadIdx.x] = m >= M ? -1 : (g.out_split ? padded(m) : m);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int jb = 0; jb < 2; ++jb) {
+    const int n = n0 + 16 * jb + fr;
+    const float pb = (epi.flags & EPI_BIAS) ? epi.bias[n] : 0.f;
+    const float pm = (epi.flags & (EPI_BN | EPI_BN_AB)) ? epi.mean[n] : 0.f;
+    const float ps = (epi.flags & (EPI_BN | EPI_BN_AB)) ? epi.sq[n] : 1.f;
+    const float pg = (epi.flags & EPI_BN) ? epi.gamma[n] : 1.f;
+    if (n >= N) continue;
+    const int cofs = (n >> 5) * 96 + (n & 31);  // bf16 offset of piece 0 inside a padded row
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int o = orow[16 * i + 4 * fq + r];
+        if (o < 0) continue;
+        const float v = apply_epilogue(acc[i][jb][r], pb, pm, ps, pg, epi.flags);
+        if (g.out_split) {
+          unsigned short s0, s1, s2;
+          split3(v, s0, s1, s2);
+          bf16_bits* d = out_split + (size_t)o * (3 * N) + cofs;
+          d[0] = s0;
+          d[32] = s1;
+          d[64] = s2;
+        } else {
+          out[(size_t)o * N + n] = v;
+        }
+      }
+  }
+}
+
+}  // namespace dnnhip

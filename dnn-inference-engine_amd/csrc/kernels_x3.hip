@@ -1,0 +1,172 @@
+// fp32 path, "x3" conv (gemm_x3_patch.h): exact three-way bf16 splits of fp32 operands on the
+// bf16 MFMA for the 3x3 wide layers (conv6/conv7 of YOLOv2-tiny), its producers (the split
+// max pool that feeds it) and its weight packing.
+#include "dnn_common.h"
+#include "gemm_x3_patch.h"
+
+#include <cfloat>
+#include <cstdlib>
+
+namespace dnnhip {
+
+static int check_x3(const char* what) {
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    set_error("%s: launch failed: %s", what, hipGetErrorString(e));
+    return -1;
+  }
+  return 0;
+}
+
+static unsigned grid_x3(long long n) {
+  const long long b = (n + 255) / 256;
+  return (unsigned)(b < 65535 * 8 ? (b > 0 ? b : 1) : 65535 * 8);
+}
+
+// ---- max pool (fp32 in, the reference's window order and `m >= x ? m : x`, pad cells skipped
+// as in maxpool_nhwc_kernel) into the split planes of a zero-bordered x3 input; 8 channels per
+// thread, one 16-B store per piece
+__global__ void maxpool_x3_kernel(const float* __restrict__ in, bf16_bits* __restrict__ out, PoolGeom g,
+                                  long long total) {
+  const int cq = g.C / 8;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % cq) * 8;
+    long long t = i / cq;
+    const int ox = (int)(t % g.OW);
+    t /= g.OW;
+    const int oy = (int)(t % g.OH);
+    const int b = (int)(t / g.OH);
+    float m[8];
+    bool first = true;
+    for (int dy = 0; dy < g.kh; ++dy)
+      for (int dx = 0; dx < g.kw; ++dx) {
+        const int iy = oy * g.sh - g.pt + dy, ix = ox * g.sw - g.pl + dx;
+        float v[8];
+        if ((unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W) {
+          const float* src = in + (((size_t)b * g.H + iy) * g.W + ix) * g.C + c;
+          const float4 x0 = *reinterpret_cast<const float4*>(src), x1 = *reinterpret_cast<const float4*>(src + 4);
+          v[0] = x0.x, v[1] = x0.y, v[2] = x0.z, v[3] = x0.w, v[4] = x1.x, v[5] = x1.y, v[6] = x1.z, v[7] = x1.w;
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = -FLT_MAX;
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) m[e] = first ? v[e] : (m[e] >= v[e] ? m[e] : v[e]);
+        first = false;
+      }
+    typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
+    u16x8 s0, s1, s2;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      unsigned short a, b2, c2;
+      split3(m[e], a, b2, c2);
+      s0[e] = a, s1[e] = b2, s2[e] = c2;
+    }
+    const size_t row = ((size_t)b * (g.OH + 2) + oy + 1) * (g.OW + 2) + ox + 1;
+    bf16_bits* d = out + row * (3 * (size_t)g.C) + (c >> 5) * 96 + (c & 31);
+    *reinterpret_cast<u16x8*>(d) = s0;
+    *reinterpret_cast<u16x8*>(d + 32) = s1;
+    *reinterpret_cast<u16x8*>(d + 64) = s2;
+  }
+}
+
+int launch_maxpool_x3(const float* in, bf16_bits* out, const PoolGeom& g, hipStream_t s) {
+  if (g.B == 0) return 0;
+  if (g.C % 32 != 0) {
+    set_error("maxpool_x3: C=%d must be a multiple of 32", g.C);
+    return -2;
+  }
+  const long long total = (long long)g.B * g.OH * g.OW * (g.C / 8);
+  hipLaunchKernelGGL(maxpool_x3_kernel, dim3(grid_x3(total)), dim3(256), 0, s, in, out, g, total);
+  return check_x3("maxpool_x3");
+}
+
+// ---- weights: HWIO fp32 [K = tap * C + c][N] -> split pieces in the kernel's fragment order
+// [n/16][step = chunk * 9 + tap][piece][lane][8], k inside a step = 8 (lane >> 4) + e
+__global__ void pack_weights_x3_kernel(const float* __restrict__ w, bf16_bits* __restrict__ out, int K, int N, int Npad,
+                                       int C) {
+  const int nk = K / 32;
+  const long long total = (long long)(Npad / 16) * nk * 3 * 512;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int e = (int)(i & 7), lane = (int)((i >> 3) & 63);
+    const long long q = i >> 9;
+    const int p = (int)(q % 3);
+    const long long r = q / 3;
+    const int s = (int)(r % nk), nb = (int)(r / nk);
+    const int n = nb * 16 + (lane & 15);
+    const int chunk = s / 9, tap = s - chunk * 9, c = chunk * 32 + 8 * (lane >> 4) + e;
+    const float v = n < N ? w[((size_t)tap * C + c) * N + n] : 0.f;
+    unsigned short s0, s1, s2;
+    split3(v, s0, s1, s2);
+    out[i] = p == 0 ? s0 : p == 1 ? s1 : s2;
+  }
+}
+
+int launch_pack_weights_x3(const float* w, bf16_bits* out, int K, int N, int Npad, int C, hipStream_t s) {
+  if (K != 9 * C || C % 32 != 0 || Npad % 256 != 0 || Npad < N) {
+    set_error("pack_weights_x3: unsupported K=%d N=%d Npad=%d C=%d", K, N, Npad, C);
+    return -2;
+  }
+  const long long total = (long long)(Npad / 16) * (K / 32) * 3 * 512;
+  hipLaunchKernelGGL(pack_weights_x3_kernel, dim3(grid_x3(total)), dim3(256), 0, s, w, out, K, N, Npad, C);
+  return check_x3("pack_weights_x3");
+}
+
+// ---- the conv
+constexpr int X3_BM = 176, X3_NPR = 320;
+
+// DNN_HIP_X3=0 keeps these layers on the fp32 MFMA (implicit GEMM)
+static bool x3_enabled() {
+  const char* e = getenv("DNN_HIP_X3");
+  return !(e && e[0] == '0');
+}
+
+// rows of the padded input one BM-row tile spans (tap offsets included)
+static long long x3_span(long long M, int H, int W) {
+  const int Wp = W + 2;
+  auto padded = [&](long long m) {
+    const long long b = m / (H * W), r = m - b * H * W, oy = r / W, ox = r - oy * W;
+    return (b * (H + 2) + oy + 1) * Wp + ox + 1;
+  };
+  long long mx = 0;
+  for (long long m0 = 0; m0 < M; m0 += X3_BM) {
+    const long long last = m0 + X3_BM - 1 < M ? m0 + X3_BM - 1 : M - 1;
+    const long long v = padded(last) - padded(m0) + 2 * (Wp + 1) + 1;
+    mx = v > mx ? v : mx;
+  }
+  return mx;
+}
+
+bool conv_x3_supported(int C, int OC, int H, int W, int OH, int OW, int kh, int kw, int sh, int sw, int pt, int pl) {
+  if (!(kh == 3 && kw == 3 && sh == 1 && sw == 1 && pt == 1 && pl == 1 && OH == H && OW == W && C % 32 == 0 &&
+        OC % 256 == 0 && x3_enabled()))
+    return false;
+  // a tile must fit the patch for any batch: spans grow with M only until a tile crosses whole
+  // images, so two images' worth of rows decides it
+  return x3_span(2LL * H * W + X3_BM, H, W) <= X3_NPR;
+}
+
+size_t x3_act_bytes(long long nimg, int H, int W, int C) { return (size_t)nimg * (H + 2) * (W + 2) * C * 6; }
+
+int launch_conv_x3(const bf16_bits* in_split, const bf16_bits* Bt, float* out, bf16_bits* out_split, long long M,
+                   int N, int Npad, int K, int H, int W, int C, const EpiParams& epi, hipStream_t stream) {
+  if (M == 0 || N == 0) return 0;
+  const long long nimg = M / ((long long)H * W);
+  const long long in_bytes = (long long)x3_act_bytes(nimg, H, W, C);
+  const long long b_bytes = (long long)(Npad / 16) * (K / 32) * 3072;
+  if (M % ((long long)H * W) != 0 || K != 9 * C || C % 32 != 0 || N % 256 != 0 || Npad != N ||
+      in_bytes >= 0x80000000LL || b_bytes >= 0x80000000LL || M > 0x7fffffffLL || x3_span(M, H, W) > X3_NPR ||
+      (out_split == nullptr) == (out == nullptr)) {
+    set_error("conv_x3: unsupported shape M=%lld N=%d K=%d %dx%dx%d", M, N, K, H, W, C);
+    return -2;
+  }
+  const int tilesM = (int)((M + X3_BM - 1) / X3_BM), tilesN = N / 256;
+  const X3Geom xg{H, W, C, out_split ? 1 : 0};
+  hipLaunchKernelGGL((conv3x3_x3_patch_kernel<X3_BM, X3_NPR>), dim3(tilesM * tilesN), dim3(512), 0, stream, in_split,
+                     Bt, out, out_split, (int)M, N, K, epi, tilesM, xg, (unsigned)in_bytes, (unsigned)b_bytes);
+  return check_x3("conv_x3");
+}
+
+}  // namespace dnnhip

@@ -86,9 +86,11 @@ static size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 using namespace dnnhip;
 
 // MODE_PATCH16: fp16 3x3 conv on a zero-bordered input (conv3x3_f16_patch_kernel; conv6/conv7)
+// MODE_X3: fp32 3x3 conv on the bf16 MFMA with exact 3-way splits, split zero-bordered input
+// (conv3x3_x3_patch_kernel; conv6/conv7 of the fp32 path)
 enum ConvMode : int { MODE_GEMM = 0, MODE_DIRECT_A = 1, MODE_IMPLICIT = 2, MODE_DIRECT = 3, MODE_PATCH = 4,
-                      MODE_PATCH16 = 5 };
-static const char* kModeName[] = {"gemm", "direct_a", "implicit", "direct", "patch", "patch16"};
+                      MODE_PATCH16 = 5, MODE_X3 = 6 };
+static const char* kModeName[] = {"gemm", "direct_a", "implicit", "direct", "patch", "patch16", "patch_x3"};
 
 struct PlanLayer {
   int type = 0;  // 0 conv, 1 pool
@@ -100,7 +102,8 @@ struct PlanLayer {
   int K = 0, Kpad = 0, Npad = 0, cfg = 0, epi_flags = 0;
   int splits = 1;  // split-K partial count (> 1: GEMM writes partials, a reduce kernel finishes)
   bool pool = false;  // a 2x2/stride-2 max pool fused into this conv
-  bool out_padded = false;  // output written zero-bordered (the next layer is MODE_PATCH16)
+  bool out_padded = false;  // output written zero-bordered (the next layer is MODE_PATCH16 / MODE_X3;
+                            // fp32 plans: as x3 split planes)
   int pad_region = 0;       // which of the two padded workspace regions it writes
   int PH = 0, PW = 0;
   size_t w_off = 0, epi_off = 0;  // float offsets in the weight arena
@@ -181,7 +184,10 @@ static void layout(dnn_plan* p) {
       L.w_off = off;
       // fp16 GEMM layers hold Bt in halves (2 per float slot); conv0's direct kernel reads fp32
       const bool half_w = p->fp16 && L.mode != MODE_DIRECT;
-      off = align_up(off + ((size_t)L.Npad * L.Kpad + (half_w ? 1 : 0)) / (half_w ? 2 : 1), 64);
+      if (L.mode == MODE_X3)  // three bf16 pieces per weight
+        off = align_up(off + (size_t)L.Npad * L.Kpad * 3 / 2, 64);
+      else
+        off = align_up(off + ((size_t)L.Npad * L.Kpad + (half_w ? 1 : 0)) / (half_w ? 2 : 1), 64);
       L.epi_off = off;
       off = align_up(off + 4 * (size_t)L.Npad, 64);
       const double flops = 2.0 * M * L.OC * L.K, w_b = 4.0 * L.K * L.OC;
@@ -231,7 +237,8 @@ static void layout(dnn_plan* p) {
   p->col_floats = align_up(col * (size_t)p->batch, 64);
   p->slab_floats = align_up(std::max(slab * (size_t)p->batch, slab_fused), 64);
   p->ticket_floats = align_up(tickets, 64);  // unsigned tickets of the fused split-K layers
-  // zero-bordered fp16 activations feeding MODE_PATCH16 layers: two regions, written alternately
+  // zero-bordered activations feeding MODE_PATCH16 (fp16) / MODE_X3 (3 bf16 pieces) layers: two
+  // regions, written alternately
   size_t padh = 0;
   int npad = 0;
   for (auto& L : p->layers)
@@ -239,7 +246,7 @@ static void layout(dnn_plan* p) {
       padh = std::max(padh, (size_t)p->batch * (L.out_h() + 2) * (L.out_w() + 2) * L.OC);
       L.pad_region = npad++ & 1;
     }
-  p->pad_floats = align_up((padh + 1) / 2, 64);
+  p->pad_floats = align_up(p->fp16 ? (padh + 1) / 2 : padh * 3 / 2, 64);
   p->ws_floats = 2 * p->act_floats + p->col_floats + p->slab_floats + p->ticket_floats + 2 * p->pad_floats +
                  dnn_plan::kZeroFloats;
 }
@@ -279,6 +286,13 @@ void dnn_plan_destroy(dnn_plan* p) {
 
 static void set_cfg(dnn_plan* p, PlanLayer& L) {
   const long long M = (long long)p->batch * L.OH * L.OW;
+  if (!p->fp16 && L.mode == MODE_X3) {  // one config: 176x256 tiles, no split
+    L.cfg = 0;
+    L.Kpad = L.K;
+    L.Npad = (int)align_up(L.OC, 256);
+    L.splits = 1;
+    return;
+  }
   if (p->fp16 && L.mode == MODE_PATCH16) {  // one config: 192x256 tiles, no split
     L.cfg = 0;
     L.Kpad = L.K;
@@ -395,6 +409,19 @@ int dnn_plan_add_conv(dnn_plan* p, int kh, int kw, int od, int stride_h, int str
     L.mode = MODE_IMPLICIT;
   else
     L.mode = MODE_GEMM;  // may become MODE_DIRECT when a 2x2/s2 pool follows (conv0)
+  // fp32 3x3 wide layers fed by a separate pool or another such conv: the x3 conv (its producer
+  // writes the split planes).  Batch plans choose it by the layer alone, so a batch-1 plan and a
+  // batch-64 plan run the same arithmetic; latency plans (with the in-GEMM split-K combine) only
+  // where its tiles fill half the chip (else split-K on the fp32 MFMA spreads the layer wider)
+  const long long x3_tiles = ((long long)p->batch * L.OH * L.OW + 175) / 176 * (od / 256);
+  if (!p->fp16 && (!p->latency || !fused_splitk(p) || x3_tiles >= 128) && L.mode == MODE_IMPLICIT && !p->layers.empty() &&
+      conv_x3_supported(L.C, od, L.H, L.W, L.OH, L.OW, kh, kw, stride_h, stride_w, L.pt, L.pl)) {
+    PlanLayer& prev = p->layers.back();
+    if ((prev.type == 1 && prev.C % 32 == 0) || (prev.type == 0 && prev.mode == MODE_X3 && !prev.pool)) {
+      L.mode = MODE_X3;
+      prev.out_padded = true;
+    }
+  }
   set_cfg(p, L);
   L.epi_flags = (biases ? EPI_BIAS : 0) | (mean ? EPI_BN : 0) |
                 (leaky == 1 ? EPI_LEAKY_F64 : leaky == 2 ? EPI_LEAKY_F32 : 0);
@@ -537,6 +564,9 @@ static int upload_weights(dnn_plan* p) {
         if (!rc)
           rc = launch_f32_to_f16(packed32, reinterpret_cast<half_t*>(p->weights + L.w_off),
                                  (long long)L.Npad * L.Kpad, 0);
+      } else if (!rc && L.mode == MODE_X3) {
+        rc = launch_pack_weights_x3(tmp, reinterpret_cast<unsigned short*>(p->weights + L.w_off), L.K, L.OC, L.Npad,
+                                    L.C, 0);
       } else if (!rc) {
         rc = launch_pack_weights(tmp, p->weights + L.w_off, L.K, L.OC, L.Kpad, L.Npad, 0, L.kh, L.kw, L.C, 0);
       }
@@ -715,9 +745,12 @@ int dnn_plan_run(dnn_plan* p, int n, const float* d_in, float* d_out, void* stre
   const float* zero = p->ws + p->ws_floats - dnn_plan::kZeroFloats;
   const float* cur = d_in;
   const int nl = (int)p->layers.size();
+  unsigned short* padr = reinterpret_cast<unsigned short*>(slab + p->slab_floats + p->ticket_floats);
   for (int i = 0; i < nl; ++i) {
     PlanLayer& L = p->layers[i];
     float* dst = (i == nl - 1) ? d_out : act[i & 1];
+    // output in x3 split planes (the next layer is MODE_X3)
+    unsigned short* dsplit = L.out_padded ? padr + (size_t)L.pad_region * p->pad_floats * 2 : nullptr;
     int k = L.kernel_idx;
     int rc = 0;
     if (L.type == 0) {
@@ -764,6 +797,14 @@ int dnn_plan_run(dnn_plan* p, int n, const float* d_in, float* d_out, void* stre
           rc = launch_conv3x3_patch_pool(cur, wt, L.Kpad, dst, g, L.C, L.OC, zero, epi, s);
           break;
         }
+        case MODE_X3:
+          rc = launch_conv_x3(reinterpret_cast<const unsigned short*>(cur),
+                              reinterpret_cast<const unsigned short*>(wt), dsplit ? nullptr : dst, dsplit, Mc, L.OC,
+                              L.Npad, L.K, L.H, L.W, L.C, epi, s);
+          break;
+        default:
+          set_error("dnn_plan_run: fp32 plan has an unsupported conv mode %d", L.mode);
+          return -2;
       }
       if (rc) return rc;
       if (L.splits > 1 && !tickets) {
@@ -773,9 +814,9 @@ int dnn_plan_run(dnn_plan* p, int n, const float* d_in, float* d_out, void* stre
     } else {
       PoolGeom g{n, L.H, L.W, L.C, L.OH, L.OW, L.kh, L.kw, L.sh, L.sw, L.pt, L.pl, 0};
       if ((rc = record(p, k, s))) return rc;
-      if ((rc = launch_maxpool(cur, dst, g, s))) return rc;
+      if ((rc = dsplit ? launch_maxpool_x3(cur, dsplit, g, s) : launch_maxpool(cur, dst, g, s))) return rc;
     }
-    cur = dst;
+    cur = dsplit ? reinterpret_cast<const float*>(dsplit) : dst;
   }
   return record(p, -1, s);
 }

@@ -107,8 +107,10 @@ def test_lowering_rejects_unfusable_graph():
 
 @pytest.mark.parametrize("fuse,splitk", [("1", "1"), ("0", "1"), ("1", "0")])
 def test_plan_shape_memory_and_flops_host_only(monkeypatch, fuse, splitk):
+    """The fp32-MFMA plan (DNN_HIP_X3=0; the x3 plan: test_plan_x3_structure_host_only)."""
     monkeypatch.setenv("DNN_HIP_FUSE", fuse)
     monkeypatch.setenv("DNN_HIP_SPLITK_FUSED", splitk)
+    monkeypatch.setenv("DNN_HIP_X3", "0")
     ws = synth.yolo_weights()
     g, _ = yolo_graph.build_graph(dnn_hip.DnnGraphBuilder, ws, in_shape=(64, 416, 416, 3))
     entries = dnn_hip.lower_graph(g)
@@ -174,6 +176,28 @@ def test_plan_shape_memory_and_flops_host_only(monkeypatch, fuse, splitk):
         assert desc.count(" combine") == (3 if splitk == "1" else 0)
     finally:
         lib.dnn_plan_destroy(h)
+
+
+def test_plan_x3_structure_host_only(monkeypatch):
+    """Default fp32 batch plan: conv6/conv7 on the x3 conv (exact 3-way bf16 splits, no split-K),
+    pool5 writing their split planes; weights of those layers in 3 bf16 pieces (6 B each)."""
+    monkeypatch.delenv("DNN_HIP_X3", raising=False)
+    ws = synth.yolo_weights()
+    g, _ = yolo_graph.build_graph(dnn_hip.DnnGraphBuilder, ws, in_shape=(64, 416, 416, 3))
+    entries = dnn_hip.lower_graph(g)
+    wb, sb = dnn_hip.Plan.memory(64, (416, 416, 3), entries)
+    nparams = sum(w["kernel"].size for w in ws)
+    x3params = 3 * 3 * 512 * 1024 + 3 * 3 * 1024 * 1024
+    assert wb >= 4 * nparams + 2 * x3params and wb < (4 * nparams + 2 * x3params) * 1.2
+    act2 = 2 * 64 * 208 * 208 * 16 * 4
+    pad = 2 * 64 * 15 * 15 * 1024 * 6  # two zero-bordered split-plane regions (conv6's output is the larger)
+    slab = 85 * 128 * 512 * 3 * 4  # conv5's fused split-K partials only
+    assert act2 + pad + slab <= sb < act2 + pad + slab + 8192
+    lines = _describe_yolo(64, False)
+    assert [ln for ln in lines if "patch_x3" in ln] == [lines[-3], lines[-2]]  # conv6, conv7
+    assert sum("splitK=3" in ln for ln in lines) == 1  # conv5
+    # latency plans keep the fp32 MFMA (split-K over the idle chip)
+    assert not any("patch_x3" in ln for ln in _describe_yolo(1, True))
 
 
 def test_plan_errors_are_reported():
@@ -289,9 +313,9 @@ def test_latency_plan_layout():
     for i in (4, 5, 6, 7, 8):
         assert " splitK=" in conv[i] and " combine" in conv[i], conv[i]
     assert "+pool2x2s2" in conv[4]
-    # the batch plan at batch 1: only the (N, K) rule's 3 splits of conv5-conv7
+    # the batch plan at batch 1: only the (N, K) rule's 3 splits of conv5, conv6/conv7 on the x3 conv
     assert [l for l in base if " splitK=" in l] == [l for l in base if " splitK=3 " in l] and \
-        sum(" splitK=3 " in l for l in base) == 3
+        sum(" splitK=3 " in l for l in base) == 1 and sum("patch_x3" in l for l in base) == 2
     assert sum(" splitK=16 " in l for l in conv) == 2  # conv6/conv7 at batch 1: 48 tiles x 16
     # batch 64: latency mode leaves the (N, K)-only rule in charge of every layer that fills the chip
     assert [l.replace(" latency", "") for l in _describe_yolo(64, True)] == _describe_yolo(64, False)

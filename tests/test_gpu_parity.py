@@ -1037,3 +1037,65 @@ def test_fp16_patch_conv_vs_oracle(monkeypatch, case):
     y0 = dnn_hip.DnnInferenceEngine(graph((1,) + x.shape[1:]), False, precision="fp16").run(x[:1])
     assert np.array_equal(y0, y[:1])
     assert np.array_equal(eng.run(x), y)
+
+
+X3_CASES = [
+    # B, H, W, C, od1, od2: pool (2x2 s1) -> conv3x3 C->od1 -> conv3x3 od1->od2, both on the fp32
+    # x3 conv (exact 3-way bf16 splits; split planes written by the pool and by the first conv)
+    (64, 13, 13, 512, 1024, 256),  # conv6-like at batch 64 (62 tiles of 176 rows), K = 4608 / 9216
+    (3, 13, 13, 128, 256, 256),    # few rows: one partial tile per N panel
+    (2, 9, 11, 32, 256, 512),      # non-square frame, one 32-channel chunk
+]
+
+
+@pytest.mark.parametrize("case", X3_CASES)
+def test_x3_conv_vs_oracle(monkeypatch, case):
+    """conv3x3_x3_patch_kernel: fp32 operands split exactly into three bf16 pieces, six bf16 MFMA
+    products into an fp32 accumulator.  Each layer within the fp32 LAYER_TOL of the float64
+    oracle (the x3 chain and the fp32-MFMA chain, DNN_HIP_X3=0, are held to the same bar, and the
+    x3 error is at most 1.25x the fp32 path's), both convs on mode patch_x3, batch rows
+    independent of the batch (bit for bit), repeat runs identical."""
+    B, H, W, C, od1, od2 = case
+    rng = np.random.default_rng(B + C + od1 + 7)
+    x = rng.standard_normal((B, H, W, C)).astype(np.float32)
+    k1 = (rng.standard_normal((3, 3, C, od1)) * np.sqrt(2.0 / (9 * C))).astype(np.float32)
+    k2 = (rng.standard_normal((3, 3, od1, od2)) * np.sqrt(2.0 / (9 * od1))).astype(np.float32)
+    bn = lambda n: (rng.standard_normal(n).astype(np.float32) * 0.1, rng.uniform(0.5, 1.5, n).astype(np.float32),
+                    rng.uniform(0.5, 1.5, n).astype(np.float32))
+    b1, bn1 = rng.standard_normal(od1).astype(np.float32) * 0.1, bn(od1)
+    b2, bn2 = rng.standard_normal(od2).astype(np.float32) * 0.1, bn(od2)
+
+    def graph(shape, layers):
+        g = dnn_hip.DnnGraphBuilder()
+        y = g.create_input(list(shape))
+        y = g.create_max_pool2d(y, [1, 2, 2, 1], [1, 1, 1, 1], "SAME")
+        for k, b, n in layers:
+            y = g.create_conv2d(y, k, [1, 1, 1, 1], "SAME")
+            y = g.create_bias_add(y, b)
+            y = g.create_batch_norm(y, *n, 1e-5)
+            y = g.create_leaky_relu(y)
+        g.set_out_node(y)
+        return g
+
+    L = [(k1, b1, bn1), (k2, b2, bn2)]
+    pooled = R.max_pool2d(x, [1, 2, 2, 1], [1, 1, 1, 1], "SAME")
+    ref1 = R.leaky_relu(R.batch_norm(R.bias_add(R.conv2d(pooled, k1), b1), *bn1, 1e-5))
+    ref2 = R.leaky_relu(R.batch_norm(R.bias_add(R.conv2d(ref1, k2), b2), *bn2, 1e-5))
+    errs = {}
+    for x3 in ("1", "0"):
+        monkeypatch.setenv("DNN_HIP_X3", x3)
+        e1 = dnn_hip.DnnInferenceEngine(graph(x.shape, L[:1]), False)
+        e2 = dnn_hip.DnnInferenceEngine(graph(x.shape, L), False)
+        assert e2.plan().describe().count("mode=patch_x3") == (2 if x3 == "1" else 0)
+        y1, y2 = e1.run(x), e2.run(x)
+        errs[x3] = (R.normwise_err(y1, ref1), R.normwise_err(y2, ref2))
+        print("x3=%s layer/chain normwise err %.3e %.3e" % (x3, errs[x3][0], errs[x3][1]))
+        if x3 == "1":
+            y0 = dnn_hip.DnnInferenceEngine(graph((1,) + x.shape[1:], L), False).run(x[:1])
+            assert np.array_equal(y0, y2[:1])
+            assert np.array_equal(e2.run(x), y2)
+    for x3 in ("0", "1"):
+        assert errs[x3][0] < LAYER_TOL and errs[x3][1] < 2 * LAYER_TOL, (x3, errs)
+    # measured: the x3 layer error is 0.4-0.95x the fp32 path's (its accumulator sees two
+    # roundings per 32-channel step, the fp32 MFMA chain one per 2 channels)
+    assert errs["1"][0] <= 1.25 * errs["0"][0] and errs["1"][1] <= 1.25 * errs["0"][1], errs
