@@ -62,6 +62,8 @@ enum EpiFlags : int {
   EPI_LEAKY_F64 = 4,   // v < 0 ? (float)(0.1 * (double)v) : v   (dnn_openblas.c:250)
   EPI_LEAKY_F32 = 8,   // max(v, 0.1f * v)                       (dnn_avx.c:540-542)
   EPI_BN_AB = 16,      // v * alpha - beta                       (dnn_avx.c:505-507)
+  EPI_OUT_X3 = 32,     // (pool-fused fp32 implicit GEMM) store the exact 3-way bf16 split of the
+                       // result into the zero-bordered split planes of an x3 conv's input
 };
 
 struct EpiParams {
@@ -227,8 +229,12 @@ bool conv_x3_supported(int C, int OC, int H, int W, int OH, int OW, int kh, int 
 size_t x3_act_bytes(long long nimg, int H, int W, int C);
 int launch_maxpool_x3(const float* in, unsigned short* out, const PoolGeom& g, hipStream_t s);
 int launch_pack_weights_x3(const float* w, unsigned short* out, int K, int N, int Npad, int C, hipStream_t s);
+int x3_splits(int N, int K);  // split-K of an x3 batch-plan layer: a function of (N, K) only
 int launch_conv_x3(const unsigned short* in_split, const unsigned short* Bt, float* out, unsigned short* out_split,
-                   long long M, int N, int Npad, int K, int H, int W, int C, const EpiParams& epi, hipStream_t stream);
+                   long long M, int N, int Npad, int K, int H, int W, int C, const EpiParams& epi, hipStream_t stream,
+                   int splits = 1);
+int launch_x3_combine(const float* part, int splits, long long slab, const EpiParams& epi, const PoolGeom& g,
+                      float* out, unsigned short* out_split, hipStream_t s);
 int patch16_pack_order();  // launch_pack_weights order of the patch kernel's MFMA shape (3 or 4)
 int launch_conv_patch16(const half_t* in_padded, const half_t* Bt, int ldb, half_t* out, int out_padded, long long M,
                         int N, int K, int H, int W, int C, const EpiParams& epi, hipStream_t stream);

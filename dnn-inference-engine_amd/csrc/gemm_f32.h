@@ -17,6 +17,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <cfloat>
+#include <type_traits>
 #include "dnn_common.h"
 
 namespace dnnhip {
@@ -46,6 +47,18 @@ __device__ __forceinline__ float div_rn(float x, float d) {
   const float q = (float)((double)x * y);
   if (__builtin_amdgcn_classf(q, 0x0F0)) return x / d;  // +-0, +-denormal
   return q;
+}
+
+// exact three-way bf16 split of fp32 (the x3 conv's operands, gemm_x3_patch.h)
+typedef unsigned short bf16_bits;
+__device__ __forceinline__ unsigned short bf16_rn(float x) { return __builtin_bit_cast(unsigned short, (__bf16)x); }
+__device__ __forceinline__ float bf16_f(unsigned short h) { return __builtin_bit_cast(float, (unsigned)h << 16); }
+// x = bf16_f(s0) + bf16_f(s1) + bf16_f(s2) exactly (finite x, |x| >= 2^-100)
+__device__ __forceinline__ void split3(float x, unsigned short& s0, unsigned short& s1, unsigned short& s2) {
+  s0 = bf16_rn(x);
+  const float r1 = x - bf16_f(s0);
+  s1 = bf16_rn(r1);
+  s2 = bf16_rn(r1 - bf16_f(s1));
 }
 
 __device__ __forceinline__ float apply_epilogue(float v, float bias, float mean, float sq, float gamma,
@@ -393,7 +406,21 @@ __device__ __forceinline__ void store_tile_pool(const typename Mfma<MF>::acc_t (
           if (!y1) v[2] = v[0];
           if (!(x1 && y1)) v[3] = v[0];
         }
-        store_out(C + (size_t)win * ldc + n, pool_then_epilogue(v, pb, pm, ps, pg, epi.flags));
+        const float val = pool_then_epilogue(v, pb, pm, ps, pg, epi.flags);
+        if constexpr (std::is_same<OutT, float>::value) {
+          if (epi.flags & EPI_OUT_X3) {  // pooled pixel -> interior row of the zero-bordered planes
+            const int b = win / (ic.PH * ic.PW), rr = win - b * (ic.PH * ic.PW), py = rr / ic.PW;
+            const size_t row = ((size_t)b * (ic.PH + 2) + py + 1) * (ic.PW + 2) + (rr - py * ic.PW) + 1;
+            unsigned short s0, s1, s2;
+            split3(val, s0, s1, s2);
+            bf16_bits* d = reinterpret_cast<bf16_bits*>(C) + row * (3 * (size_t)N) + (n >> 5) * 96 + (n & 31);
+            d[0] = s0;
+            d[32] = s1;
+            d[64] = s2;
+            continue;
+          }
+        }
+        store_out(C + (size_t)win * ldc + n, val);
       }
     }
   }

@@ -31,22 +31,14 @@
 namespace dnnhip {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef unsigned short bf16_bits;
 
 struct X3Geom {
   int H, W, C;     // conv input = output spatial size (3x3, stride 1, SAME), channels
-  int out_split;   // 1: write split planes into a zero-bordered [B][H+2][W+2] buffer (next x3 layer)
+  int out_mode;    // 0: fp32 [M][N] after the epilogue; 1: split planes into a zero-bordered
+                   // [B][H+2][W+2] buffer (next x3 layer); 2: raw fp32 partial of split-K slice
+                   // s at out + s*M*N (no epilogue; x3_combine_kernel finishes)
+  int splits;      // K split into this many contiguous chunk ranges (grid = tiles x splits)
 };
-
-__device__ __forceinline__ unsigned short bf16_rn(float x) { return __builtin_bit_cast(unsigned short, (__bf16)x); }
-__device__ __forceinline__ float bf16_f(unsigned short h) { return __builtin_bit_cast(float, (unsigned)h << 16); }
-// x = bf16_f(s0) + bf16_f(s1) + bf16_f(s2) exactly (finite x, |x| >= 2^-100)
-__device__ __forceinline__ void split3(float x, unsigned short& s0, unsigned short& s1, unsigned short& s2) {
-  s0 = bf16_rn(x);
-  const float r1 = x - bf16_f(s0);
-  s1 = bf16_rn(r1);
-  s2 = bf16_rn(r1 - bf16_f(s1));
-}
 
 __device__ __forceinline__ f32x4 mfma16_bf16(bf16x8 a, bf16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
@@ -65,7 +57,8 @@ conv3x3_x3_patch_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __res
   const int lane = threadIdx.x & 63;
   const int wid = wave_uniform(threadIdx.x >> 6);
   // tiles N-major inside each XCD's contiguous range: the XCD's CUs share one weight panel
-  const int tile = xcd_tile(blockIdx.x, gridDim.x);
+  const int tile_s = xcd_tile(blockIdx.x, gridDim.x), ntiles = gridDim.x / g.splits;
+  const int split = tile_s / ntiles, tile = tile_s - split * ntiles;
   const int tn = tile / tilesM, tm = tile - tn * tilesM;
   const int m0 = tm * BM, n0 = tn * BN + wid * 32;  // this wave's 32 columns
   const int Wp = g.W + 2, HWo = g.H * g.W;
@@ -94,9 +87,12 @@ conv3x3_x3_patch_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __res
 
   // patch staging: thread (tid % 384) owns slot ss = t % 12 of rows t / 12 + 32 u (waves 6, 7
   // repeat waves 0, 1: no branch, same bytes to the same LDS address)
+  // this split's chunks: [split * nch, (split + 1) * nch) of the K / 288 (the launcher checks
+  // that splits divides them); its first chunk folded into both per-lane offsets
+  const int nk = K / 32, nch = nk / 9 / g.splits, cb = split * nch;
   const int st = threadIdx.x % 384, srow = st / 12, ss = st - srow * 12;
   const int rowB = 6 * g.C;  // bytes per padded row (all chunks)
-  const unsigned pvo = (unsigned)((P0 + srow) * rowB + ss * 16);
+  const unsigned pvo = (unsigned)((P0 + srow) * rowB + ss * 16 + cb * RB);
   const int pdst = srow * RB + (ss >> 2) * 64 + 16 * ((ss & 3) ^ ((srow >> 1) & 2));
   const auto rsA = __builtin_amdgcn_make_buffer_rsrc((void*)in, 0, (int)in_bytes, 0x00020000);
   u32x4 pst[PPT];
@@ -108,8 +104,7 @@ conv3x3_x3_patch_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __res
   };
 
   // weight fragments: per (16-column block, step) 3 pieces x 1 KiB, two taps ahead
-  const int nk = K / 32, nch = nk / 9;
-  const unsigned bvo = (unsigned)((n0 / 16) * nk * 3072 + lane * 16);
+  const unsigned bvo = (unsigned)((n0 / 16) * nk * 3072 + lane * 16 + cb * 9 * 3072);
   const int bjs = nk * 3072;  // second 16-column block of the wave
   const auto rsB = __builtin_amdgcn_make_buffer_rsrc((void*)Bt, 0, (int)b_bytes, 0x00020000);
   bf16x8 bq[3][3][2];  // [step % 3][piece][column block]
@@ -224,7 +219,7 @@ conv3x3_x3_patch_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __res
   __syncthreads();  // every wave is done with the patches
   if (threadIdx.x < BM) {
     const int m = m0 + threadIdx.x;
-    orow[threadIdx.x] = m >= M ? -1 : (g.out_split ? padded(m) : m);
+    orow[threadIdx.x] = m >= M ? -1 : (g.out_mode == 1 ? padded(m) : m);
   }
   __syncthreads();
 #pragma unroll
@@ -241,8 +236,12 @@ conv3x3_x3_patch_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __res
       for (int r = 0; r < 4; ++r) {
         const int o = orow[16 * i + 4 * fq + r];
         if (o < 0) continue;
+        if (g.out_mode == 2) {
+          out[((size_t)split * M + o) * N + n] = acc[i][jb][r];
+          continue;
+        }
         const float v = apply_epilogue(acc[i][jb][r], pb, pm, ps, pg, epi.flags);
-        if (g.out_split) {
+        if (g.out_mode == 1) {
           unsigned short s0, s1, s2;
           split3(v, s0, s1, s2);
           bf16_bits* d = out_split + (size_t)o * (3 * N) + cofs;

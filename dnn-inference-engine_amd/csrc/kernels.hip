@@ -645,7 +645,7 @@ int launch_gemm_persist(int cfg, int mode, const float* in, const ImplicitConv& 
   if (M == 0 || N == 0) return 0;
   if (!persist_enabled() || (mode != GEMM_IMPLICIT && mode != GEMM_IMPLICIT_POOL) || ic_in.C % 32 != 0 ||
       M > 0x7fffffffLL || Kpad % 32 != 0 || !implicit_conv_supported(ic_in.C, ic_in.kh, ic_in.kw) ||
-      (mode == GEMM_IMPLICIT_POOL && M % 4 != 0))
+      (mode == GEMM_IMPLICIT_POOL && M % 4 != 0) || (epi.flags & EPI_OUT_X3))  // (split-plane output: tile kernel)
     return -3;
   ImplicitConv ic = ic_in;
   implicit_conv_magic(&ic);

@@ -52,7 +52,8 @@ __global__ void maxpool_x3_kernel(const float* __restrict__ in, bf16_bits* __res
           for (int e = 0; e < 8; ++e) v[e] = -FLT_MAX;
         }
 #pragma unroll
-        for (int e = 0; e < 8; ++e) m[e] = first ? v[e] : (m[e] >= v[e] ? m[e] : v[e]);
+        for (int e = 0; e < 8; ++e)
+          m[e] = first ? v[e] : (c + e < g.gt_below ? (m[e] > v[e] ? m[e] : v[e]) : (m[e] >= v[e] ? m[e] : v[e]));
         first = false;
       }
     typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
@@ -80,6 +81,166 @@ int launch_maxpool_x3(const float* in, bf16_bits* out, const PoolGeom& g, hipStr
   const long long total = (long long)g.B * g.OH * g.OW * (g.C / 8);
   hipLaunchKernelGGL(maxpool_x3_kernel, dim3(grid_x3(total)), dim3(256), 0, s, in, out, g, total);
   return check_x3("maxpool_x3");
+}
+
+// ---- split-K combine of the x3 conv: partials [splits][M][N] (raw fp32, `slab` floats apart)
+// summed in split order ((p0 + p1) + p2 ...), the conv's fp32 epilogue, then an optional max
+// pool in the reference's order (window cells in row order, `m >= x ? m : x`, pad cells
+// skipped; kh = kw = 1, stride 1: no pool), into fp32 NHWC or the split planes of the next x3
+// layer (out_split).  8 channels per thread, epilogue parameters loaded once per thread.
+template <int KH, int KW, int S>  // KH = 0: any window / split count (runtime loops)
+__global__ void x3_combine_kernel(const float* __restrict__ part, int splits, long long slab, EpiParams epi,
+                                  PoolGeom g, float* __restrict__ out, bf16_bits* __restrict__ out_split,
+                                  long long total) {
+  const int cq = g.C / 8;
+  // blocks in consecutive pixel order per XCD (xcd_tile): a window's other rows are read by
+  // blocks of the same XCD, from its L2, instead of by every XCD from HBM (stride-1 pools
+  // read each partial 4 times)
+  const long long i = (long long)xcd_tile(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
+  if (i < total) {
+    const int c = (int)(i % cq) * 8;
+    long long t = i / cq;
+    const int ox = (int)(t % g.OW);
+    t /= g.OW;
+    const int oy = (int)(t % g.OH);
+    const int b = (int)(t / g.OH);
+    // epilogue parameters of the 8 channels: two 16-B loads per array (c % 8 == 0; the plan's
+    // arrays hold Npad >= C floats), not 32 scalar loads
+    float pb[8], pm[8], ps[8], pg[8];
+    auto ld8 = [&](const float* a, float (&d)[8], float dflt, bool on) {
+      if (on) {
+        const float4 x0 = *reinterpret_cast<const float4*>(a + c), x1 = *reinterpret_cast<const float4*>(a + c + 4);
+        d[0] = x0.x, d[1] = x0.y, d[2] = x0.z, d[3] = x0.w, d[4] = x1.x, d[5] = x1.y, d[6] = x1.z, d[7] = x1.w;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) d[e] = dflt;
+      }
+    };
+    ld8(epi.bias, pb, 0.f, (epi.flags & EPI_BIAS) != 0);
+    ld8(epi.mean, pm, 0.f, (epi.flags & (EPI_BN | EPI_BN_AB)) != 0);
+    ld8(epi.sq, ps, 1.f, (epi.flags & (EPI_BN | EPI_BN_AB)) != 0);
+    ld8(epi.gamma, pg, 1.f, (epi.flags & EPI_BN) != 0);
+    float hi[8], lo[8];
+    if constexpr (KH > 0) {
+      // fixed window and split count: every load issued up front.  Window cells past the frame
+      // are clamped into it: a clamped row / column is the window's first or last in-frame
+      // one, so the cell repeats a window member and the max is unchanged
+      float v[KH * KW][8];
+#pragma unroll
+      for (int dy = 0; dy < KH; ++dy)
+#pragma unroll
+        for (int dx = 0; dx < KW; ++dx) {
+          int iy = oy * g.sh - g.pt + dy, ix = ox * g.sw - g.pl + dx;
+          iy = iy < 0 ? 0 : iy >= g.H ? g.H - 1 : iy;
+          ix = ix < 0 ? 0 : ix >= g.W ? g.W - 1 : ix;
+          const float* src = part + (((size_t)b * g.H + iy) * g.W + ix) * g.C + c;
+          float4 x[S][2];
+#pragma unroll
+          for (int sp = 0; sp < S; ++sp) {
+            x[sp][0] = *reinterpret_cast<const float4*>(src + sp * slab);
+            x[sp][1] = *reinterpret_cast<const float4*>(src + sp * slab + 4);
+          }
+          float* w = v[dy * KW + dx];
+          w[0] = x[0][0].x, w[1] = x[0][0].y, w[2] = x[0][0].z, w[3] = x[0][0].w;
+          w[4] = x[0][1].x, w[5] = x[0][1].y, w[6] = x[0][1].z, w[7] = x[0][1].w;
+#pragma unroll
+          for (int sp = 1; sp < S; ++sp) {  // split order ((p0 + p1) + p2 ...)
+            w[0] += x[sp][0].x, w[1] += x[sp][0].y, w[2] += x[sp][0].z, w[3] += x[sp][0].w;
+            w[4] += x[sp][1].x, w[5] += x[sp][1].y, w[6] += x[sp][1].z, w[7] += x[sp][1].w;
+          }
+        }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        hi[e] = lo[e] = v[0][e];
+#pragma unroll
+        for (int q = 1; q < KH * KW; ++q) {
+          hi[e] = __builtin_fmaxf(hi[e], v[q][e]);
+          lo[e] = __builtin_fminf(lo[e], v[q][e]);
+        }
+      }
+    } else {
+    bool first = true;
+    for (int dy = 0; dy < g.kh; ++dy)
+      for (int dx = 0; dx < g.kw; ++dx) {
+        const int iy = oy * g.sh - g.pt + dy, ix = ox * g.sw - g.pl + dx;
+        if ((unsigned)iy >= (unsigned)g.H || (unsigned)ix >= (unsigned)g.W) continue;  // -FLT_MAX pad cell
+        const float* src = part + (((size_t)b * g.H + iy) * g.W + ix) * g.C + c;
+        float v[8];
+        {
+          const float4 x0 = *reinterpret_cast<const float4*>(src), x1 = *reinterpret_cast<const float4*>(src + 4);
+          v[0] = x0.x, v[1] = x0.y, v[2] = x0.z, v[3] = x0.w, v[4] = x1.x, v[5] = x1.y, v[6] = x1.z, v[7] = x1.w;
+        }
+        for (int sp = 1; sp < splits; ++sp) {
+          const float* q = src + sp * slab;
+          const float4 x0 = *reinterpret_cast<const float4*>(q), x1 = *reinterpret_cast<const float4*>(q + 4);
+          v[0] += x0.x, v[1] += x0.y, v[2] += x0.z, v[3] += x0.w, v[4] += x1.x, v[5] += x1.y, v[6] += x1.z,
+              v[7] += x1.w;
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          hi[e] = first ? v[e] : __builtin_fmaxf(hi[e], v[e]);
+          lo[e] = first ? v[e] : __builtin_fminf(lo[e], v[e]);
+        }
+        first = false;
+      }
+    }
+    // pool before the epilogue, as the GEMMs' fused pools (pool_then_epilogue):
+    // the epilogue is a chain of IEEE-monotone steps, so max f(v_i) = f(max v_i) (min for a
+    // decreasing channel) -- one exact-division epilogue per output instead of one per cell
+    float m[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const bool dec = ((epi.flags & EPI_BN) && pg[e] < 0.f) || ((epi.flags & EPI_BN_AB) && pm[e] < 0.f);
+      m[e] = apply_epilogue(dec ? lo[e] : hi[e], pb[e], pm[e], ps[e], pg[e], epi.flags);
+    }
+    if (out_split) {
+      typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
+      u16x8 s0, s1, s2;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        unsigned short a, b2, c2;
+        split3(m[e], a, b2, c2);
+        s0[e] = a, s1[e] = b2, s2[e] = c2;
+      }
+      const size_t row = ((size_t)b * (g.OH + 2) + oy + 1) * (g.OW + 2) + ox + 1;
+      bf16_bits* d = out_split + row * (3 * (size_t)g.C) + (c >> 5) * 96 + (c & 31);
+      *reinterpret_cast<u16x8*>(d) = s0;
+      *reinterpret_cast<u16x8*>(d + 32) = s1;
+      *reinterpret_cast<u16x8*>(d + 64) = s2;
+    } else {
+      float* d = out + (((size_t)b * g.OH + oy) * g.OW + ox) * g.C + c;
+      *reinterpret_cast<float4*>(d) = make_float4(m[0], m[1], m[2], m[3]);
+      *reinterpret_cast<float4*>(d + 4) = make_float4(m[4], m[5], m[6], m[7]);
+    }
+  }
+}
+
+int launch_x3_combine(const float* part, int splits, long long slab, const EpiParams& epi, const PoolGeom& g,
+                      float* out, bf16_bits* out_split, hipStream_t s) {
+  if (g.B == 0) return 0;
+  if (g.C % 32 != 0 || splits < 1 || (out == nullptr) == (out_split == nullptr)) {
+    set_error("x3_combine: unsupported C=%d splits=%d", g.C, splits);
+    return -2;
+  }
+  const long long total = (long long)g.B * g.OH * g.OW * (g.C / 8);
+  if ((total + 255) / 256 > 0x7fffffffLL) {
+    set_error("x3_combine: %lld outputs", total);
+    return -2;
+  }
+  const dim3 grid((unsigned)((total + 255) / 256));
+#define X3C(KH, KW, S) \
+  hipLaunchKernelGGL((x3_combine_kernel<KH, KW, S>), grid, dim3(256), 0, s, part, splits, slab, epi, g, out, out_split, total)
+  const int win = g.kh == 2 && g.kw == 2 ? 2 : g.kh == 1 && g.kw == 1 ? 1 : 0;
+  if (win == 2 && splits == 2)
+    X3C(2, 2, 2);
+  else if (win == 2 && splits == 1)
+    X3C(2, 2, 1);
+  else if (win == 1 && splits == 2)
+    X3C(1, 1, 2);
+  else
+    X3C(0, 0, 0);
+#undef X3C
+  return check_x3("x3_combine");
 }
 
 // ---- weights: HWIO fp32 [K = tap * C + c][N] -> split pieces in the kernel's fragment order
@@ -150,21 +311,27 @@ bool conv_x3_supported(int C, int OC, int H, int W, int OH, int OW, int kh, int 
 
 size_t x3_act_bytes(long long nimg, int H, int W, int C) { return (size_t)nimg * (H + 2) * (W + 2) * C * 6; }
 
+// N = 512 (conv5): 62 x 2 = 124 tiles of 176 x 256 at batch 64, half the chip -> 2 K slices;
+// wider layers fill it alone, narrower ones (N = 256: 246 tiles) too
+int x3_splits(int N, int K) { return (N > 256 && N <= 512 && (K / 288) % 2 == 0) ? 2 : 1; }
+
 int launch_conv_x3(const bf16_bits* in_split, const bf16_bits* Bt, float* out, bf16_bits* out_split, long long M,
-                   int N, int Npad, int K, int H, int W, int C, const EpiParams& epi, hipStream_t stream) {
+                   int N, int Npad, int K, int H, int W, int C, const EpiParams& epi, hipStream_t stream, int splits) {
   if (M == 0 || N == 0) return 0;
   const long long nimg = M / ((long long)H * W);
   const long long in_bytes = (long long)x3_act_bytes(nimg, H, W, C);
   const long long b_bytes = (long long)(Npad / 16) * (K / 32) * 3072;
   if (M % ((long long)H * W) != 0 || K != 9 * C || C % 32 != 0 || N % 256 != 0 || Npad != N ||
       in_bytes >= 0x80000000LL || b_bytes >= 0x80000000LL || M > 0x7fffffffLL || x3_span(M, H, W) > X3_NPR ||
-      (out_split == nullptr) == (out == nullptr)) {
+      (out_split == nullptr) == (out == nullptr) || splits < 1 || (K / 288) % splits != 0 ||
+      (splits > 1 && out_split != nullptr)) {
     set_error("conv_x3: unsupported shape M=%lld N=%d K=%d %dx%dx%d", M, N, K, H, W, C);
     return -2;
   }
   const int tilesM = (int)((M + X3_BM - 1) / X3_BM), tilesN = N / 256;
-  const X3Geom xg{H, W, C, out_split ? 1 : 0};
-  hipLaunchKernelGGL((conv3x3_x3_patch_kernel<X3_BM, X3_NPR>), dim3(tilesM * tilesN), dim3(512), 0, stream, in_split,
+  // splits > 1: `out` receives the raw partials [splits][M][N] (x3_combine_kernel finishes)
+  const X3Geom xg{H, W, C, splits > 1 ? 2 : out_split ? 1 : 0, splits};
+  hipLaunchKernelGGL((conv3x3_x3_patch_kernel<X3_BM, X3_NPR>), dim3(tilesM * tilesN * splits), dim3(512), 0, stream, in_split,
                      Bt, out, out_split, (int)M, N, K, epi, tilesM, xg, (unsigned)in_bytes, (unsigned)b_bytes);
   return check_x3("conv_x3");
 }

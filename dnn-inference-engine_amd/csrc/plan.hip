@@ -104,7 +104,7 @@ struct PlanLayer {
   bool pool = false;  // a 2x2/stride-2 max pool fused into this conv
   bool out_padded = false;  // output written zero-bordered (the next layer is MODE_PATCH16 / MODE_X3;
                             // fp32 plans: as x3 split planes)
-  int pad_region = 0;       // which of the two padded workspace regions it writes
+  size_t pad_off = 0;       // its zero-bordered output region: float offset inside the pad area
   int PH = 0, PW = 0;
   size_t w_off = 0, epi_off = 0;  // float offsets in the weight arena
   bool have_host = false;
@@ -206,7 +206,17 @@ static void layout(dnn_plan* p) {
         p->kernels.push_back({nm, (int)i, 1, flops, in_b + w_b + out_b});
         ++nconv;
       }
-      if (L.splits > 1 && fused_splitk(p)) {  // partials combined by the GEMM's last-arriving split
+      if (L.mode == MODE_X3 && L.splits > 1) {  // raw partials; combined by the next pool, or:
+        slab = std::max(slab, (size_t)L.splits * L.OH * L.OW * L.OC);
+        const bool pool_next = i + 1 < p->layers.size() && p->layers[i + 1].type == 1;
+        if (!pool_next) {
+          snprintf(nm, sizeof(nm), "conv%d.combine", nconv - 1);
+          p->kernels.push_back({nm, (int)i, 3, (L.splits - 1) * M * L.OC, 4.0 * (L.splits + 1) * M * L.OC});
+        }
+      }
+      if (L.mode == MODE_X3) {
+        // (split-K partials: below)
+      } else if (L.splits > 1 && fused_splitk(p)) {  // partials combined by the GEMM's last-arriving split
         const long long Mg = L.pool ? 4LL * p->batch * L.PH * L.PW : (long long)M;  // the GEMM's rows
         slab_fused = std::max(slab_fused, (size_t)(p->fp16 ? splitk16_fused_slab_floats(L.cfg, Mg, L.OC, L.splits)
                                                            : splitk_fused_slab_floats(L.cfg, Mg, L.OC, L.splits)));
@@ -237,17 +247,18 @@ static void layout(dnn_plan* p) {
   p->col_floats = align_up(col * (size_t)p->batch, 64);
   p->slab_floats = align_up(std::max(slab * (size_t)p->batch, slab_fused), 64);
   p->ticket_floats = align_up(tickets, 64);  // unsigned tickets of the fused split-K layers
-  // zero-bordered activations feeding MODE_PATCH16 (fp16) / MODE_X3 (3 bf16 pieces) layers: two
-  // regions, written alternately
-  size_t padh = 0;
-  int npad = 0;
+  // zero-bordered activations feeding MODE_PATCH16 (fp16, 2 B per element) / MODE_X3 (3 bf16
+  // pieces, 6 B) layers: one region per producer (zeroed once at finalize; each producer
+  // rewrites only its own interior, so its borders stay zero whatever the layers' shapes)
+  size_t pad_total = 0;
   for (auto& L : p->layers)
     if (L.out_padded) {
-      padh = std::max(padh, (size_t)p->batch * (L.out_h() + 2) * (L.out_w() + 2) * L.OC);
-      L.pad_region = npad++ & 1;
+      const size_t elems = (size_t)p->batch * (L.out_h() + 2) * (L.out_w() + 2) * L.OC;
+      L.pad_off = pad_total;
+      pad_total += align_up(p->fp16 ? (elems + 1) / 2 : elems * 3 / 2, 64);
     }
-  p->pad_floats = align_up(p->fp16 ? (padh + 1) / 2 : padh * 3 / 2, 64);
-  p->ws_floats = 2 * p->act_floats + p->col_floats + p->slab_floats + p->ticket_floats + 2 * p->pad_floats +
+  p->pad_floats = pad_total;
+  p->ws_floats = 2 * p->act_floats + p->col_floats + p->slab_floats + p->ticket_floats + p->pad_floats +
                  dnn_plan::kZeroFloats;
 }
 
@@ -286,11 +297,11 @@ void dnn_plan_destroy(dnn_plan* p) {
 
 static void set_cfg(dnn_plan* p, PlanLayer& L) {
   const long long M = (long long)p->batch * L.OH * L.OW;
-  if (!p->fp16 && L.mode == MODE_X3) {  // one config: 176x256 tiles, no split
+  if (!p->fp16 && L.mode == MODE_X3) {  // one config: 176x256 tiles; split-K by (N, K) only
     L.cfg = 0;
     L.Kpad = L.K;
     L.Npad = (int)align_up(L.OC, 256);
-    L.splits = 1;
+    L.splits = x3_splits(L.OC, L.K);
     return;
   }
   if (p->fp16 && L.mode == MODE_PATCH16) {  // one config: 192x256 tiles, no split
@@ -413,11 +424,14 @@ int dnn_plan_add_conv(dnn_plan* p, int kh, int kw, int od, int stride_h, int str
   // writes the split planes).  Batch plans choose it by the layer alone, so a batch-1 plan and a
   // batch-64 plan run the same arithmetic; latency plans (with the in-GEMM split-K combine) only
   // where its tiles fill half the chip (else split-K on the fp32 MFMA spreads the layer wider)
-  const long long x3_tiles = ((long long)p->batch * L.OH * L.OW + 175) / 176 * (od / 256);
+  const long long x3_tiles = ((long long)p->batch * L.OH * L.OW + 175) / 176 * (od / 256) * x3_splits(od, L.K);
   if (!p->fp16 && (!p->latency || !fused_splitk(p) || x3_tiles >= 128) && L.mode == MODE_IMPLICIT && !p->layers.empty() &&
       conv_x3_supported(L.C, od, L.H, L.W, L.OH, L.OW, kh, kw, stride_h, stride_w, L.pt, L.pl)) {
+    // producers that can write the split planes: a separate pool, another x3 conv, or a
+    // pool-fused implicit GEMM without split-K (its epilogue splits, EPI_OUT_X3)
     PlanLayer& prev = p->layers.back();
-    if ((prev.type == 1 && prev.C % 32 == 0) || (prev.type == 0 && prev.mode == MODE_X3 && !prev.pool)) {
+    if ((prev.type == 1 && prev.C % 32 == 0) || (prev.type == 0 && prev.mode == MODE_X3 && !prev.pool) ||
+        (prev.type == 0 && prev.mode == MODE_IMPLICIT && prev.pool && prev.splits == 1)) {
       L.mode = MODE_X3;
       prev.out_padded = true;
     }
@@ -619,7 +633,7 @@ int dnn_plan_finalize(dnn_plan* p, int device, void* weights, void* workspace) {
   DNN_HIP_TRY(hipMemset(p->ws + p->ws_floats - dnn_plan::kZeroFloats, 0, dnn_plan::kZeroFloats * sizeof(float)));
   if (p->pad_floats)  // zero borders of the padded activations (interiors are rewritten every run)
     DNN_HIP_TRY(hipMemset(p->ws + 2 * p->act_floats + p->col_floats + p->slab_floats + p->ticket_floats, 0,
-                          2 * p->pad_floats * sizeof(float)));
+                          p->pad_floats * sizeof(float)));
   if (p->ticket_floats)  // fused split-K tickets start at zero; every launch leaves them zero
     DNN_HIP_TRY(hipMemset(p->ws + 2 * p->act_floats + p->col_floats + p->slab_floats, 0,
                           p->ticket_floats * sizeof(float)));
@@ -674,7 +688,7 @@ static int run_fp16(dnn_plan* p, int n, const float* d_in, float* d_out, hipStre
                                             p->ticket_floats);
   for (int i = 0; i < nl; ++i) {
     PlanLayer& L = p->layers[i];
-    half_t* dst = L.out_padded ? padr + (size_t)L.pad_region * p->pad_floats * 2 : act[i & 1];
+    half_t* dst = L.out_padded ? padr + L.pad_off * 2 : act[i & 1];
     int k = L.kernel_idx;
     if (L.type == 0) {
       const float* e = p->weights + L.epi_off;
@@ -750,7 +764,7 @@ int dnn_plan_run(dnn_plan* p, int n, const float* d_in, float* d_out, void* stre
     PlanLayer& L = p->layers[i];
     float* dst = (i == nl - 1) ? d_out : act[i & 1];
     // output in x3 split planes (the next layer is MODE_X3)
-    unsigned short* dsplit = L.out_padded ? padr + (size_t)L.pad_region * p->pad_floats * 2 : nullptr;
+    unsigned short* dsplit = L.out_padded ? padr + L.pad_off * 2 : nullptr;
     int k = L.kernel_idx;
     int rc = 0;
     if (L.type == 0) {
@@ -777,11 +791,18 @@ int dnn_plan_run(dnn_plan* p, int n, const float* d_in, float* d_out, void* stre
                           L.pool ? 1 : 0};
           const long long M = L.pool ? 4LL * n * L.PH * L.PW : Mc;
           const int gm = L.pool ? GEMM_IMPLICIT_POOL : GEMM_IMPLICIT;
+          // feeding an x3 conv: the pooled epilogue stores the split planes (EPI_OUT_X3)
+          EpiParams ep = epi;
+          float* o = dst;
+          if (dsplit) {
+            ep.flags |= EPI_OUT_X3;
+            o = reinterpret_cast<float*>(dsplit);
+          }
           // unsplit layers: the persistent kernel (same bits) when it covers the config
-          rc = L.splits == 1 ? launch_gemm_persist(L.cfg, gm, cur, ic, wt, L.Kpad, dst, L.OC, M, L.OC, L.Kpad, epi, s)
+          rc = L.splits == 1 ? launch_gemm_persist(L.cfg, gm, cur, ic, wt, L.Kpad, o, L.OC, M, L.OC, L.Kpad, ep, s)
                              : -3;
           if (rc == -3)
-            rc = launch_gemm_implicit(L.cfg, gm, cur, ic, wt, L.Kpad, dst, L.OC, M, L.OC, L.Kpad, epi, s, L.splits,
+            rc = launch_gemm_implicit(L.cfg, gm, cur, ic, wt, L.Kpad, o, L.OC, M, L.OC, L.Kpad, ep, s, L.splits,
                                       slab, tickets);
           break;
         }
@@ -798,23 +819,43 @@ int dnn_plan_run(dnn_plan* p, int n, const float* d_in, float* d_out, void* stre
           break;
         }
         case MODE_X3:
-          rc = launch_conv_x3(reinterpret_cast<const unsigned short*>(cur),
-                              reinterpret_cast<const unsigned short*>(wt), dsplit ? nullptr : dst, dsplit, Mc, L.OC,
-                              L.Npad, L.K, L.H, L.W, L.C, epi, s);
+          if (L.splits > 1) {  // raw partials into the slab; the next pool or a combine kernel finishes
+            rc = launch_conv_x3(reinterpret_cast<const unsigned short*>(cur),
+                                reinterpret_cast<const unsigned short*>(wt), slab, nullptr, Mc, L.OC, L.Npad, L.K, L.H,
+                                L.W, L.C, epi, s, L.splits);
+            if (!rc && !(i + 1 < nl && p->layers[i + 1].type == 1)) {
+              PoolGeom id{n, L.OH, L.OW, L.OC, L.OH, L.OW, 1, 1, 1, 1, 0, 0, 0};
+              if ((rc = record(p, ++k, s))) return rc;
+              rc = launch_x3_combine(slab, L.splits, Mc * L.OC, epi, id, dsplit ? nullptr : dst, dsplit, s);
+            }
+          } else {
+            rc = launch_conv_x3(reinterpret_cast<const unsigned short*>(cur),
+                                reinterpret_cast<const unsigned short*>(wt), dsplit ? nullptr : dst, dsplit, Mc, L.OC,
+                                L.Npad, L.K, L.H, L.W, L.C, epi, s);
+          }
           break;
         default:
           set_error("dnn_plan_run: fp32 plan has an unsupported conv mode %d", L.mode);
           return -2;
       }
       if (rc) return rc;
-      if (L.splits > 1 && !tickets) {
+      if (L.splits > 1 && !tickets && L.mode != MODE_X3) {
         if ((rc = record(p, ++k, s))) return rc;
         if ((rc = launch_splitk_reduce(slab, L.splits, Mc, L.OC, dst, L.OC, epi, s))) return rc;
       }
     } else {
       PoolGeom g{n, L.H, L.W, L.C, L.OH, L.OW, L.kh, L.kw, L.sh, L.sw, L.pt, L.pl, 0};
       if ((rc = record(p, k, s))) return rc;
-      if ((rc = dsplit ? launch_maxpool_x3(cur, dsplit, g, s) : launch_maxpool(cur, dst, g, s))) return rc;
+      const PlanLayer* pv = i > 0 ? &p->layers[i - 1] : nullptr;
+      if (pv && pv->type == 0 && pv->mode == MODE_X3 && pv->splits > 1) {  // combine the x3 partials + pool
+        const float* e = p->weights + pv->epi_off;
+        const EpiParams pe{e, e + pv->Npad, e + 2 * pv->Npad, e + 3 * pv->Npad, pv->epi_flags};
+        rc = launch_x3_combine(slab, pv->splits, (long long)n * pv->OH * pv->OW * pv->OC, pe, g, dsplit ? nullptr : dst,
+                               dsplit, s);
+      } else {
+        rc = dsplit ? launch_maxpool_x3(cur, dsplit, g, s) : launch_maxpool(cur, dst, g, s);
+      }
+      if (rc) return rc;
     }
     cur = dsplit ? reinterpret_cast<const float*>(dsplit) : dst;
   }
@@ -901,7 +942,8 @@ int dnn_plan_describe(const dnn_plan* p, char* buf, int buf_len) {
       if (L.splits > 1) snprintf(sk, sizeof(sk), " splitK=%d", L.splits);
       snprintf(line, sizeof(line), "conv %dx%dx%d -> %dx%dx%d k%dx%d s%d mode=%s cfg=%d K=%d Kpad=%d%s%s%s%s%s\n", L.H,
                L.W, L.C, L.out_h(), L.out_w(), L.OC, L.kh, L.kw, L.sh, kModeName[L.mode], L.cfg, L.K, L.Kpad,
-               L.pool ? " +pool2x2s2" : "", sk, L.splits > 1 && fused_splitk(p) ? " combine" : "",
+               L.pool ? " +pool2x2s2" : "", sk,
+               L.splits > 1 ? (L.mode == MODE_X3 ? " x3-combine" : fused_splitk(p) ? " combine" : "") : "",
                p->fp16 ? " fp16" : "", p->latency ? " latency" : "");
     } else
       snprintf(line, sizeof(line), "pool %dx%dx%d -> %dx%dx%d k%dx%d s%d%s\n", L.H, L.W, L.C, L.OH, L.OW, L.OC, L.kh,

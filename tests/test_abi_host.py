@@ -179,23 +179,28 @@ def test_plan_shape_memory_and_flops_host_only(monkeypatch, fuse, splitk):
 
 
 def test_plan_x3_structure_host_only(monkeypatch):
-    """Default fp32 batch plan: conv6/conv7 on the x3 conv (exact 3-way bf16 splits, no split-K),
-    pool5 writing their split planes; weights of those layers in 3 bf16 pieces (6 B each)."""
+    """Default fp32 batch plan: conv4-conv7 on the x3 conv (exact 3-way bf16 splits), conv3's
+    pooled epilogue and the pools after conv4/conv5 writing their split planes; conv5 (N = 512)
+    in 2 K slices whose partials pool5 combines; weights of those layers in 3 bf16 pieces."""
     monkeypatch.delenv("DNN_HIP_X3", raising=False)
     ws = synth.yolo_weights()
     g, _ = yolo_graph.build_graph(dnn_hip.DnnGraphBuilder, ws, in_shape=(64, 416, 416, 3))
     entries = dnn_hip.lower_graph(g)
     wb, sb = dnn_hip.Plan.memory(64, (416, 416, 3), entries)
     nparams = sum(w["kernel"].size for w in ws)
-    x3params = 3 * 3 * 512 * 1024 + 3 * 3 * 1024 * 1024
+    x3params = 9 * (128 * 256 + 256 * 512 + 512 * 1024 + 1024 * 1024)
     assert wb >= 4 * nparams + 2 * x3params and wb < (4 * nparams + 2 * x3params) * 1.2
     act2 = 2 * 64 * 208 * 208 * 16 * 4
-    pad = 2 * 64 * 15 * 15 * 1024 * 6  # two zero-bordered split-plane regions (conv6's output is the larger)
-    slab = 85 * 128 * 512 * 3 * 4  # conv5's fused split-K partials only
-    assert act2 + pad + slab <= sb < act2 + pad + slab + 8192
+    # one zero-bordered split-plane region per producer: conv3 (26x26x128), pool4 (13x13x256),
+    # pool5 (13x13x512), conv6 (13x13x1024), 6 B per element
+    pad = sum(64 * 6 * (h + 2) ** 2 * c for h, c in ((26, 128), (13, 256), (13, 512), (13, 1024)))
+    slab = 2 * 64 * 13 * 13 * 512 * 4  # conv5's two raw K-slice partials
+    assert act2 + pad + slab <= sb < act2 + pad + slab + 16384
     lines = _describe_yolo(64, False)
-    assert [ln for ln in lines if "patch_x3" in ln] == [lines[-3], lines[-2]]  # conv6, conv7
-    assert sum("splitK=3" in ln for ln in lines) == 1  # conv5
+    conv = [ln for ln in lines if ln.startswith("conv")]
+    assert [i for i, ln in enumerate(conv) if "patch_x3" in ln] == [4, 5, 6, 7]
+    assert "splitK=2 x3-combine" in conv[5] and sum("splitK" in ln for ln in lines) == 1
+    assert sum(ln.startswith("pool") for ln in lines) == 2  # after conv4 (2x2 s2) and conv5 (s1)
     # latency plans keep the fp32 MFMA (split-K over the idle chip)
     assert not any("patch_x3" in ln for ln in _describe_yolo(1, True))
 
@@ -313,9 +318,9 @@ def test_latency_plan_layout():
     for i in (4, 5, 6, 7, 8):
         assert " splitK=" in conv[i] and " combine" in conv[i], conv[i]
     assert "+pool2x2s2" in conv[4]
-    # the batch plan at batch 1: only the (N, K) rule's 3 splits of conv5, conv6/conv7 on the x3 conv
-    assert [l for l in base if " splitK=" in l] == [l for l in base if " splitK=3 " in l] and \
-        sum(" splitK=3 " in l for l in base) == 1 and sum("patch_x3" in l for l in base) == 2
+    # the batch plan at batch 1: conv4-conv7 on the x3 conv, conv5 in the (N, K) rule's 2 K slices
+    assert [l for l in base if " splitK=" in l] == [l for l in base if " splitK=2 x3-combine" in l] and \
+        sum(" splitK=2 " in l for l in base) == 1 and sum("patch_x3" in l for l in base) == 4
     assert sum(" splitK=16 " in l for l in conv) == 2  # conv6/conv7 at batch 1: 48 tiles x 16
     # batch 64: latency mode leaves the (N, K)-only rule in charge of every layer that fills the chip
     assert [l.replace(" latency", "") for l in _describe_yolo(64, True)] == _describe_yolo(64, False)

@@ -457,7 +457,8 @@ def test_plan_timing_api(yolo_b1):
         plan.run_host(x)
     ms, cnt = plan.timing_end()
     ks = plan.kernels()
-    assert len(ms) == len(ks) == 10  # 10 plan kernels: conv5/6/7 combine their split-K partials in the GEMM
+    # 11 plan kernels: conv0-8 + pool4 (after conv4's x3 conv) + pool5 (combines conv5's K slices)
+    assert len(ms) == len(ks) == 11
     assert all(c == 3 for c in cnt)
     assert all(m > 0 for m in ms)
     # events around one kernel only (the bench's timed region): the others report no launches
@@ -467,7 +468,7 @@ def test_plan_timing_api(yolo_b1):
             plan.run_host(x)
         ms1, cnt1 = plan.timing_end()
         names = [k["name"] for k in ks]
-        assert [c for n, c in zip(names, cnt1) if n != only] == [0] * 9
+        assert [c for n, c in zip(names, cnt1) if n != only] == [0] * 10
         assert cnt1[names.index(only)] == 3 and ms1[names.index(only)] > 0
 
 
@@ -1099,3 +1100,77 @@ def test_x3_conv_vs_oracle(monkeypatch, case):
     # measured: the x3 layer error is 0.4-0.95x the fp32 path's (its accumulator sees two
     # roundings per 32-channel step, the fp32 MFMA chain one per 2 channels)
     assert errs["1"][0] <= 1.25 * errs["0"][0] and errs["1"][1] <= 1.25 * errs["0"][1], errs
+
+
+X3_CHAIN_CASES = [
+    # B, H, W, C0: conv3x3 C0->128 + pool 2x2 s2 (fp32 implicit GEMM writing the x3 split planes)
+    # -> conv3x3 128->512 (x3, 2 K slices) -> then "pool" (2x2 s1: pool5's combine) or "conv"
+    # (a standalone combine kernel) -> conv3x3 ->256 (x3)
+    (8, 26, 26, 64, "pool"),
+    (3, 26, 26, 32, "conv"),
+]
+
+
+@pytest.mark.parametrize("case", X3_CHAIN_CASES)
+def test_x3_split_combine_and_producer_vs_oracle(monkeypatch, case):
+    """The x3 conv's K slices (conv5's rule: N = 512 -> 2 slices of raw partials) combined in
+    split order by the next pool (sum, epilogue, pool in the reference's order) or by a
+    standalone combine kernel, and a pool-fused fp32 implicit GEMM storing its epilogue as
+    x3 split planes (EPI_OUT_X3).  Every layer mode as planned, the chain within the fp32
+    tolerance of the float64 oracle and within 1.25x of the fp32-MFMA plan's error
+    (DNN_HIP_X3=0), batch rows bit-equal to batch-1 runs."""
+    B, H, W, C0, mid = case
+    rng = np.random.default_rng(B * 7 + C0)
+    x = rng.standard_normal((B, H, W, C0)).astype(np.float32)
+
+    def layer(c, od):
+        k = (rng.standard_normal((3, 3, c, od)) * np.sqrt(2.0 / (9 * c))).astype(np.float32)
+        b = rng.standard_normal(od).astype(np.float32) * 0.1
+        n = (rng.standard_normal(od).astype(np.float32) * 0.1, rng.uniform(0.5, 1.5, od).astype(np.float32),
+             rng.uniform(0.5, 1.5, od).astype(np.float32))
+        return k, b, n
+
+    L0, L1 = layer(C0, 128), layer(128, 512)
+    L2 = layer(512, 256) if mid == "pool" else layer(512, 256)
+
+    def graph(shape):
+        g = dnn_hip.DnnGraphBuilder()
+        y = g.create_input(list(shape))
+        for idx, (k, b, n) in enumerate((L0, L1, L2)):
+            y = g.create_conv2d(y, k, [1, 1, 1, 1], "SAME")
+            y = g.create_bias_add(y, b)
+            y = g.create_batch_norm(y, *n, 1e-5)
+            y = g.create_leaky_relu(y)
+            if idx == 0:
+                y = g.create_max_pool2d(y, [1, 2, 2, 1], [1, 2, 2, 1], "SAME")
+            if idx == 1 and mid == "pool":
+                y = g.create_max_pool2d(y, [1, 2, 2, 1], [1, 1, 1, 1], "SAME")
+        g.set_out_node(y)
+        return g
+
+    ref = x
+    for idx, (k, b, n) in enumerate((L0, L1, L2)):
+        ref = R.leaky_relu(R.batch_norm(R.bias_add(R.conv2d(ref, k), b), *n, 1e-5))
+        if idx == 0:
+            ref = R.max_pool2d(ref, [1, 2, 2, 1], [1, 2, 2, 1], "SAME")
+        if idx == 1 and mid == "pool":
+            ref = R.max_pool2d(ref, [1, 2, 2, 1], [1, 1, 1, 1], "SAME")
+    errs = {}
+    for x3 in ("1", "0"):
+        monkeypatch.setenv("DNN_HIP_X3", x3)
+        eng = dnn_hip.DnnInferenceEngine(graph(x.shape), False)
+        desc = eng.plan().describe()
+        if x3 == "1":
+            conv = [ln for ln in desc.splitlines() if ln.startswith("conv")]
+            assert "mode=implicit" in conv[0] and "+pool2x2s2" in conv[0]
+            assert "mode=patch_x3" in conv[1] and "splitK=2 x3-combine" in conv[1] and "mode=patch_x3" in conv[2]
+            names = [k["name"] for k in eng.plan().kernels()]
+            assert ("conv1.combine" in names) == (mid == "conv")
+        y = eng.run(x)
+        errs[x3] = R.normwise_err(y, ref)
+        print("x3=%s chain normwise err %.3e" % (x3, errs[x3]))
+        if x3 == "1":
+            y0 = dnn_hip.DnnInferenceEngine(graph((1,) + x.shape[1:]), False).run(x[:1])
+            assert np.array_equal(y0, y[:1])
+    assert errs["1"] < 3 * LAYER_TOL and errs["0"] < 3 * LAYER_TOL, errs
+    assert errs["1"] <= 1.25 * errs["0"], errs
