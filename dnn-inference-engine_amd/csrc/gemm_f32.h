@@ -409,8 +409,9 @@ __device__ __forceinline__ void store_tile_pool(const typename Mfma<MF>::acc_t (
         const float val = pool_then_epilogue(v, pb, pm, ps, pg, epi.flags);
         if constexpr (std::is_same<OutT, float>::value) {
           if (epi.flags & EPI_OUT_X3) {  // pooled pixel -> interior row of the zero-bordered planes
-            const int b = win / (ic.PH * ic.PW), rr = win - b * (ic.PH * ic.PW), py = rr / ic.PW;
-            const size_t row = ((size_t)b * (ic.PH + 2) + py + 1) * (ic.PW + 2) + (rr - py * ic.PW) + 1;
+            const int q1 = div_magic(win, ic.mag_pw, ic.sh_pw), px = win - q1 * ic.PW;  // no division
+            const int b = div_magic(q1, ic.mag_ph, ic.sh_ph), py = q1 - b * ic.PH;
+            const size_t row = ((size_t)b * (ic.PH + 2) + py + 1) * (ic.PW + 2) + px + 1;
             unsigned short s0, s1, s2;
             split3(val, s0, s1, s2);
             bf16_bits* d = reinterpret_cast<bf16_bits*>(C) + row * (3 * (size_t)N) + (n >> 5) * 96 + (n & 31);

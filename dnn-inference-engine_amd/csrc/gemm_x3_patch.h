@@ -144,7 +144,7 @@ conv3x3_x3_patch_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __res
     int pr = prow[i];
     asm volatile("" : "+v"(pr));  // keep the taps' addresses from being hoisted
     const int row = pr + toff;
-    const unsigned char* q = P + row * RB + 16 * (fq ^ ((row >> 1) & 2));
+    const unsigned char* q = P + row * RB + 16 * (fq ^ ((row >> 1) & 2));  // (shift form: same time)
 #pragma unroll
     for (int p = 0; p < 3; ++p) a[p] = *reinterpret_cast<const bf16x8*>(q + 64 * p);
   };

@@ -331,8 +331,8 @@ int launch_conv_x3(const bf16_bits* in_split, const bf16_bits* Bt, float* out, b
   const int tilesM = (int)((M + X3_BM - 1) / X3_BM), tilesN = N / 256;
   // splits > 1: `out` receives the raw partials [splits][M][N] (x3_combine_kernel finishes)
   const X3Geom xg{H, W, C, splits > 1 ? 2 : out_split ? 1 : 0, splits};
-  hipLaunchKernelGGL((conv3x3_x3_patch_kernel<X3_BM, X3_NPR>), dim3(tilesM * tilesN * splits), dim3(512), 0, stream, in_split,
-                     Bt, out, out_split, (int)M, N, K, epi, tilesM, xg, (unsigned)in_bytes, (unsigned)b_bytes);
+  hipLaunchKernelGGL((conv3x3_x3_patch_kernel<X3_BM, X3_NPR>), dim3(tilesM * tilesN * splits), dim3(512), 0, stream,
+                     in_split, Bt, out, out_split, (int)M, N, K, epi, tilesM, xg, (unsigned)in_bytes, (unsigned)b_bytes);
   return check_x3("conv_x3");
 }
 
