@@ -88,7 +88,7 @@ int launch_maxpool_x3(const float* in, bf16_bits* out, const PoolGeom& g, hipStr
 // pool in the reference's order (window cells in row order, `m >= x ? m : x`, pad cells
 // skipped; kh = kw = 1, stride 1: no pool), into fp32 NHWC or the split planes of the next x3
 // layer (out_split).  8 channels per thread, epilogue parameters loaded once per thread.
-template <int KH, int KW, int S>  // KH = 0: any window / split count (runtime loops)
+template <int KH, int KW, int S>  // KH = 0: any window (runtime loops); S = 0: any split count
 __global__ void x3_combine_kernel(const float* __restrict__ part, int splits, long long slab, EpiParams epi,
                                   PoolGeom g, float* __restrict__ out, bf16_bits* __restrict__ out_split,
                                   long long total) {
@@ -134,19 +134,31 @@ __global__ void x3_combine_kernel(const float* __restrict__ part, int splits, lo
           iy = iy < 0 ? 0 : iy >= g.H ? g.H - 1 : iy;
           ix = ix < 0 ? 0 : ix >= g.W ? g.W - 1 : ix;
           const float* src = part + (((size_t)b * g.H + iy) * g.W + ix) * g.C + c;
-          float4 x[S][2];
-#pragma unroll
-          for (int sp = 0; sp < S; ++sp) {
-            x[sp][0] = *reinterpret_cast<const float4*>(src + sp * slab);
-            x[sp][1] = *reinterpret_cast<const float4*>(src + sp * slab + 4);
-          }
           float* w = v[dy * KW + dx];
-          w[0] = x[0][0].x, w[1] = x[0][0].y, w[2] = x[0][0].z, w[3] = x[0][0].w;
-          w[4] = x[0][1].x, w[5] = x[0][1].y, w[6] = x[0][1].z, w[7] = x[0][1].w;
+          if constexpr (S > 0) {
+            float4 x[S][2];
 #pragma unroll
-          for (int sp = 1; sp < S; ++sp) {  // split order ((p0 + p1) + p2 ...)
-            w[0] += x[sp][0].x, w[1] += x[sp][0].y, w[2] += x[sp][0].z, w[3] += x[sp][0].w;
-            w[4] += x[sp][1].x, w[5] += x[sp][1].y, w[6] += x[sp][1].z, w[7] += x[sp][1].w;
+            for (int sp = 0; sp < S; ++sp) {
+              x[sp][0] = *reinterpret_cast<const float4*>(src + sp * slab);
+              x[sp][1] = *reinterpret_cast<const float4*>(src + sp * slab + 4);
+            }
+            w[0] = x[0][0].x, w[1] = x[0][0].y, w[2] = x[0][0].z, w[3] = x[0][0].w;
+            w[4] = x[0][1].x, w[5] = x[0][1].y, w[6] = x[0][1].z, w[7] = x[0][1].w;
+#pragma unroll
+            for (int sp = 1; sp < S; ++sp) {  // split order ((p0 + p1) + p2 ...)
+              w[0] += x[sp][0].x, w[1] += x[sp][0].y, w[2] += x[sp][0].z, w[3] += x[sp][0].w;
+              w[4] += x[sp][1].x, w[5] += x[sp][1].y, w[6] += x[sp][1].z, w[7] += x[sp][1].w;
+            }
+          } else {  // many slices (latency plans): loads run ahead of the ordered sum
+            const float4 x0 = *reinterpret_cast<const float4*>(src), x1 = *reinterpret_cast<const float4*>(src + 4);
+            w[0] = x0.x, w[1] = x0.y, w[2] = x0.z, w[3] = x0.w, w[4] = x1.x, w[5] = x1.y, w[6] = x1.z, w[7] = x1.w;
+#pragma unroll 8
+            for (int sp = 1; sp < splits; ++sp) {
+              const float4 y0 = *reinterpret_cast<const float4*>(src + sp * slab);
+              const float4 y1 = *reinterpret_cast<const float4*>(src + sp * slab + 4);
+              w[0] += y0.x, w[1] += y0.y, w[2] += y0.z, w[3] += y0.w, w[4] += y1.x, w[5] += y1.y, w[6] += y1.z,
+                  w[7] += y1.w;
+            }
           }
         }
 #pragma unroll
@@ -237,6 +249,10 @@ int launch_x3_combine(const float* part, int splits, long long slab, const EpiPa
     X3C(2, 2, 1);
   else if (win == 1 && splits == 2)
     X3C(1, 1, 2);
+  else if (win == 1)
+    X3C(1, 1, 0);
+  else if (win == 2)
+    X3C(2, 2, 0);
   else
     X3C(0, 0, 0);
 #undef X3C
@@ -314,6 +330,7 @@ size_t x3_act_bytes(long long nimg, int H, int W, int C) { return (size_t)nimg *
 // N = 512 (conv5): 62 x 2 = 124 tiles of 176 x 256 at batch 64, half the chip -> 2 K slices;
 // wider layers fill it alone, narrower ones (N = 256: 246 tiles) too
 int x3_splits(int N, int K) { return (N > 256 && N <= 512 && (K / 288) % 2 == 0) ? 2 : 1; }
+
 
 int launch_conv_x3(const bf16_bits* in_split, const bf16_bits* Bt, float* out, bf16_bits* out_split, long long M,
                    int N, int Npad, int K, int H, int W, int C, const EpiParams& epi, hipStream_t stream, int splits) {

@@ -423,7 +423,9 @@ int dnn_plan_add_conv(dnn_plan* p, int kh, int kw, int od, int stride_h, int str
   // fp32 3x3 wide layers fed by a separate pool or another such conv: the x3 conv (its producer
   // writes the split planes).  Batch plans choose it by the layer alone, so a batch-1 plan and a
   // batch-64 plan run the same arithmetic; latency plans (with the in-GEMM split-K combine) only
-  // where its tiles fill half the chip (else split-K on the fp32 MFMA spreads the layer wider)
+  // where its tiles fill half the chip: at batch 1 a 176 x 256 tile's one-chunk K slice alone
+  // takes ~26 us (measured: conv6/conv7 as 16 / 32 x3 slices 0.053 / 0.056 ms with their
+  // combines, against 0.034 / 0.050 on the fp32 MFMA with split-K 16)
   const long long x3_tiles = ((long long)p->batch * L.OH * L.OW + 175) / 176 * (od / 256) * x3_splits(od, L.K);
   if (!p->fp16 && (!p->latency || !fused_splitk(p) || x3_tiles >= 128) && L.mode == MODE_IMPLICIT && !p->layers.empty() &&
       conv_x3_supported(L.C, od, L.H, L.W, L.OH, L.OW, kh, kw, stride_h, stride_w, L.pt, L.pl)) {
