@@ -1118,7 +1118,7 @@ def test_x3_split_combine_and_producer_vs_oracle(monkeypatch, case):
     standalone combine kernel, and a pool-fused fp32 implicit GEMM storing its epilogue as
     x3 split planes (EPI_OUT_X3).  Every layer mode as planned, the chain within the fp32
     tolerance of the float64 oracle and within 1.25x of the fp32-MFMA plan's error
-    (DNN_HIP_X3=0), batch rows bit-equal to batch-1 runs."""
+    (DNN_HIP_X3=0), batch rows bit-equal to batch-1 runs; negative-gamma channels throughout."""
     B, H, W, C0, mid = case
     rng = np.random.default_rng(B * 7 + C0)
     x = rng.standard_normal((B, H, W, C0)).astype(np.float32)
@@ -1126,12 +1126,14 @@ def test_x3_split_combine_and_producer_vs_oracle(monkeypatch, case):
     def layer(c, od):
         k = (rng.standard_normal((3, 3, c, od)) * np.sqrt(2.0 / (9 * c))).astype(np.float32)
         b = rng.standard_normal(od).astype(np.float32) * 0.1
-        n = (rng.standard_normal(od).astype(np.float32) * 0.1, rng.uniform(0.5, 1.5, od).astype(np.float32),
-             rng.uniform(0.5, 1.5, od).astype(np.float32))
+        # every 5th channel with a negative gamma: a decreasing epilogue, so the pools before the
+        # epilogue (conv0's EPI_OUT_X3 store, pool5's combine) must take the window's minimum
+        gam = rng.uniform(0.5, 1.5, od).astype(np.float32)
+        gam[::5] *= -1
+        n = (rng.standard_normal(od).astype(np.float32) * 0.1, rng.uniform(0.5, 1.5, od).astype(np.float32), gam)
         return k, b, n
 
-    L0, L1 = layer(C0, 128), layer(128, 512)
-    L2 = layer(512, 256) if mid == "pool" else layer(512, 256)
+    L0, L1, L2 = layer(C0, 128), layer(128, 512), layer(512, 256)
 
     def graph(shape):
         g = dnn_hip.DnnGraphBuilder()
