@@ -232,7 +232,8 @@ int launch_pack_weights_x3(const float* w, unsigned short* out, int K, int N, in
 int x3_splits(int N, int K);  // split-K of an x3 batch-plan layer: a function of (N, K) only
 int launch_conv_x3(const unsigned short* in_split, const unsigned short* Bt, float* out, unsigned short* out_split,
                    long long M, int N, int Npad, int K, int H, int W, int C, const EpiParams& epi, hipStream_t stream,
-                   int splits = 1);
+                   int splits = 1, int pool = 0);
+bool conv_x3_pool_supported(int H, int W);  // an x3 conv of this size can fuse a 2x2/s2 pool
 int launch_x3_combine(const float* part, int splits, long long slab, const EpiParams& epi, const PoolGeom& g,
                       float* out, unsigned short* out_split, hipStream_t s);
 int patch16_pack_order();  // launch_pack_weights order of the patch kernel's MFMA shape (3 or 4)

@@ -38,13 +38,18 @@ struct X3Geom {
                    // [B][H+2][W+2] buffer (next x3 layer); 2: raw fp32 partial of split-K slice
                    // s at out + s*M*N (no epilogue; x3_combine_kernel finishes)
   int splits;      // K split into this many contiguous chunk ranges (grid = tiles x splits)
+  int PH, PW;      // POOL kernels: the 2x2/s2 pooled output (rows are pool-window-major)
 };
 
 __device__ __forceinline__ f32x4 mfma16_bf16(bf16x8 a, bf16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
-template <int BM, int NPR>
+// POOL: a fused 2x2/s2 max pool -- GEMM rows pool-window-major (row 4 w + 2 dy + dx = cell (dy,
+// dx) of pooled pixel w; cells past an odd edge repeat cell (0, 0)), so a lane's 4 accumulator
+// registers (rows 4 q .. 4 q + 3 of its 16 x 16 block) are one window: pooled before the
+// epilogue (pool_then_epilogue, as the fp32 GEMMs' fused pools)
+template <int BM, int NPR, bool POOL = false>
 __global__ void __launch_bounds__(512, 1)
 conv3x3_x3_patch_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __restrict__ Bt, float* __restrict__ out,
                         bf16_bits* __restrict__ out_split, int M, int N, int K, EpiParams epi, int tilesM, X3Geom g,
@@ -66,7 +71,20 @@ conv3x3_x3_patch_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __res
     const int b = m / HWo, r = m - b * HWo, oy = r / g.W, ox = r - oy * g.W;
     return (b * (g.H + 2) + oy + 1) * Wp + ox + 1;
   };
-  const int P0 = padded(m0) - (Wp + 1);  // first patch row (>= 0: p(0) = Wp + 1)
+  // GEMM row -> padded row of its conv output pixel (raster, or pool-window-major)
+  auto pixrow = [&](int m) {
+    if constexpr (!POOL) {
+      return padded(m);
+    } else {
+      const int w = m >> 2, q = m & 3, PHW = g.PH * g.PW;
+      const int b = w / PHW, r = w - b * PHW, py = r / g.PW, px = r - py * g.PW;
+      int oy = 2 * py + (q >> 1), ox = 2 * px + (q & 1);
+      if (oy >= g.H || ox >= g.W) oy = 2 * py, ox = 2 * px;
+      return (b * (g.H + 2) + oy + 1) * Wp + ox + 1;
+    }
+  };
+  // first patch row (>= 0: p(0) = Wp + 1); row m0 is the tile's smallest in both orders
+  const int P0 = pixrow(m0) - (Wp + 1);
 
   // A fragment of row-block i: lane's output row 16 i + fr -> patch row of tap (1, 1); its k
   // slot fq (8 channels) of piece p sits at row*192 + 64 p + 16 (fq ^ ((row >> 1) & 2)).
@@ -82,7 +100,7 @@ conv3x3_x3_patch_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __res
   for (int i = 0; i < TM; ++i) {
     int m = m0 + 16 * i + fr;
     m = m < M ? m : M - 1;
-    prow[i] = padded(m) - P0;
+    prow[i] = pixrow(m) - P0;
   }
 
   // patch staging: thread (tid % 384) owns slot ss = t % 12 of rows t / 12 + 32 u (waves 6, 7
@@ -217,6 +235,41 @@ conv3x3_x3_patch_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __res
   // 0.895 ms, same call; the extra code costs the main loop registers.)
   int* orow = reinterpret_cast<int*>(smem);
   __syncthreads();  // every wave is done with the patches
+  if constexpr (POOL) {  // one entry per window: pooled pixel (or its zero-bordered row)
+    if (threadIdx.x < BM / 4) {
+      const int w = (m0 >> 2) + threadIdx.x, PHW = g.PH * g.PW;
+      const int b = w / PHW, r = w - b * PHW, py = r / g.PW, px = r - py * g.PW;
+      orow[threadIdx.x] = 4 * w >= M ? -1 : g.out_mode == 1 ? (b * (g.PH + 2) + py + 1) * (g.PW + 2) + px + 1 : w;
+    }
+    __syncthreads();
+    // (staging the pooled block through LDS for 16-B stores measured equal: conv4 0.133 ms)
+#pragma unroll
+    for (int jb = 0; jb < 2; ++jb) {
+      const int n = n0 + 16 * jb + fr;
+      const float pb = (epi.flags & EPI_BIAS) ? epi.bias[n] : 0.f;
+      const float pm = (epi.flags & (EPI_BN | EPI_BN_AB)) ? epi.mean[n] : 0.f;
+      const float ps = (epi.flags & (EPI_BN | EPI_BN_AB)) ? epi.sq[n] : 1.f;
+      const float pg = (epi.flags & EPI_BN) ? epi.gamma[n] : 1.f;
+      const int cofs = (n >> 5) * 96 + (n & 31);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int o = orow[4 * i + fq];
+        if (o < 0) continue;
+        const float v = pool_then_epilogue(acc[i][jb], pb, pm, ps, pg, epi.flags);
+        if (g.out_mode == 1) {
+          unsigned short s0, s1, s2;
+          split3(v, s0, s1, s2);
+          bf16_bits* d = out_split + (size_t)o * (3 * N) + cofs;
+          d[0] = s0;
+          d[32] = s1;
+          d[64] = s2;
+        } else {
+          out[(size_t)o * N + n] = v;
+        }
+      }
+    }
+    return;
+  }
   if (threadIdx.x < BM) {
     const int m = m0 + threadIdx.x;
     orow[threadIdx.x] = m >= M ? -1 : (g.out_mode == 1 ? padded(m) : m);

@@ -300,10 +300,18 @@ static bool x3_enabled() {
   return !(e && e[0] == '0');
 }
 
-// rows of the padded input one BM-row tile spans (tap offsets included)
-static long long x3_span(long long M, int H, int W) {
-  const int Wp = W + 2;
+constexpr int X3_NPR_POOL = 352;  // pool-window-major tiles span more rows (26x26: 350)
+
+// rows of the padded input one BM-row tile spans (tap offsets included); pool: window-major
+static long long x3_span(long long M, int H, int W, bool pool = false) {
+  const int Wp = W + 2, PH = (H + 1) / 2, PW = (W + 1) / 2;
   auto padded = [&](long long m) {
+    if (pool) {
+      const long long w = m >> 2, q = m & 3, b = w / (PH * PW), r = w - b * PH * PW, py = r / PW, px = r - py * PW;
+      long long oy = 2 * py + (q >> 1), ox = 2 * px + (q & 1);
+      if (oy >= H || ox >= W) oy = 2 * py, ox = 2 * px;
+      return (b * (H + 2) + oy + 1) * Wp + ox + 1;
+    }
     const long long b = m / (H * W), r = m - b * H * W, oy = r / W, ox = r - oy * W;
     return (b * (H + 2) + oy + 1) * Wp + ox + 1;
   };
@@ -325,6 +333,12 @@ bool conv_x3_supported(int C, int OC, int H, int W, int OH, int OW, int kh, int 
   return x3_span(2LL * H * W + X3_BM, H, W) <= X3_NPR;
 }
 
+// ... with a fused 2x2/s2 pool (pool-window-major rows)
+bool conv_x3_pool_supported(int H, int W) {
+  const long long rows = 4LL * ((H + 1) / 2) * ((W + 1) / 2);
+  return x3_span(2 * rows + X3_BM, H, W, true) <= X3_NPR_POOL;
+}
+
 size_t x3_act_bytes(long long nimg, int H, int W, int C) { return (size_t)nimg * (H + 2) * (W + 2) * C * 6; }
 
 // N = 512 (conv5): 62 x 2 = 124 tiles of 176 x 256 at batch 64, half the chip -> 2 K slices;
@@ -333,13 +347,18 @@ int x3_splits(int N, int K) { return (N > 256 && N <= 512 && (K / 288) % 2 == 0)
 
 
 int launch_conv_x3(const bf16_bits* in_split, const bf16_bits* Bt, float* out, bf16_bits* out_split, long long M,
-                   int N, int Npad, int K, int H, int W, int C, const EpiParams& epi, hipStream_t stream, int splits) {
+                   int N, int Npad, int K, int H, int W, int C, const EpiParams& epi, hipStream_t stream, int splits,
+                   int pool) {
   if (M == 0 || N == 0) return 0;
-  const long long nimg = M / ((long long)H * W);
+  // pool: M counts GEMM rows, 4 per pooled pixel
+  const int PH = pool ? (H + 1) / 2 : 0, PW = pool ? (W + 1) / 2 : 0;
+  const long long per_img = pool ? 4LL * PH * PW : (long long)H * W;
+  const long long nimg = M / per_img;
   const long long in_bytes = (long long)x3_act_bytes(nimg, H, W, C);
   const long long b_bytes = (long long)(Npad / 16) * (K / 32) * 3072;
-  if (M % ((long long)H * W) != 0 || K != 9 * C || C % 32 != 0 || N % 256 != 0 || Npad != N ||
-      in_bytes >= 0x80000000LL || b_bytes >= 0x80000000LL || M > 0x7fffffffLL || x3_span(M, H, W) > X3_NPR ||
+  if (M % per_img != 0 || K != 9 * C || C % 32 != 0 || N % 256 != 0 || Npad != N || (pool && splits != 1) ||
+      in_bytes >= 0x80000000LL || b_bytes >= 0x80000000LL || M > 0x7fffffffLL ||
+      x3_span(M, H, W, pool != 0) > (pool ? X3_NPR_POOL : X3_NPR) ||
       (out_split == nullptr) == (out == nullptr) || splits < 1 || (K / 288) % splits != 0 ||
       (splits > 1 && out_split != nullptr)) {
     set_error("conv_x3: unsupported shape M=%lld N=%d K=%d %dx%dx%d", M, N, K, H, W, C);
@@ -347,9 +366,15 @@ int launch_conv_x3(const bf16_bits* in_split, const bf16_bits* Bt, float* out, b
   }
   const int tilesM = (int)((M + X3_BM - 1) / X3_BM), tilesN = N / 256;
   // splits > 1: `out` receives the raw partials [splits][M][N] (x3_combine_kernel finishes)
-  const X3Geom xg{H, W, C, splits > 1 ? 2 : out_split ? 1 : 0, splits};
-  hipLaunchKernelGGL((conv3x3_x3_patch_kernel<X3_BM, X3_NPR>), dim3(tilesM * tilesN * splits), dim3(512), 0, stream,
-                     in_split, Bt, out, out_split, (int)M, N, K, epi, tilesM, xg, (unsigned)in_bytes, (unsigned)b_bytes);
+  const X3Geom xg{H, W, C, splits > 1 ? 2 : out_split ? 1 : 0, splits, PH, PW};
+  if (pool)
+    hipLaunchKernelGGL((conv3x3_x3_patch_kernel<X3_BM, X3_NPR_POOL, true>), dim3(tilesM * tilesN), dim3(512), 0, stream,
+                       in_split, Bt, out, out_split, (int)M, N, K, epi, tilesM, xg, (unsigned)in_bytes,
+                       (unsigned)b_bytes);
+  else
+    hipLaunchKernelGGL((conv3x3_x3_patch_kernel<X3_BM, X3_NPR>), dim3(tilesM * tilesN * splits), dim3(512), 0, stream,
+                       in_split, Bt, out, out_split, (int)M, N, K, epi, tilesM, xg, (unsigned)in_bytes,
+                       (unsigned)b_bytes);
   return check_x3("conv_x3");
 }
 

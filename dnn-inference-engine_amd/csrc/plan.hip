@@ -432,7 +432,7 @@ int dnn_plan_add_conv(dnn_plan* p, int kh, int kw, int od, int stride_h, int str
     // producers that can write the split planes: a separate pool, another x3 conv, or a
     // pool-fused implicit GEMM without split-K (its epilogue splits, EPI_OUT_X3)
     PlanLayer& prev = p->layers.back();
-    if ((prev.type == 1 && prev.C % 32 == 0) || (prev.type == 0 && prev.mode == MODE_X3 && !prev.pool) ||
+    if ((prev.type == 1 && prev.C % 32 == 0) || (prev.type == 0 && prev.mode == MODE_X3) ||
         (prev.type == 0 && prev.mode == MODE_IMPLICIT && prev.pool && prev.splits == 1)) {
       L.mode = MODE_X3;
       prev.out_padded = true;
@@ -520,6 +520,9 @@ int dnn_plan_add_max_pool(dnn_plan* p, int kh, int kw, int stride_h, int stride_
                                                                       prev.sw)) {
         prev.mode = MODE_DIRECT;
         ok = true;
+      } else if (prev.mode == MODE_X3 && !p->fp16 && conv_x3_pool_supported(prev.H, prev.W) &&
+                 !getenv_flag_off("DNN_HIP_X3_POOL")) {
+        ok = true;  // pool-window-major rows, pooled before the epilogue in the x3 kernel
       }
       if (ok) {
         prev.pool = true;
@@ -832,8 +835,9 @@ int dnn_plan_run(dnn_plan* p, int n, const float* d_in, float* d_out, void* stre
             }
           } else {
             rc = launch_conv_x3(reinterpret_cast<const unsigned short*>(cur),
-                                reinterpret_cast<const unsigned short*>(wt), dsplit ? nullptr : dst, dsplit, Mc, L.OC,
-                                L.Npad, L.K, L.H, L.W, L.C, epi, s);
+                                reinterpret_cast<const unsigned short*>(wt), dsplit ? nullptr : dst, dsplit,
+                                L.pool ? 4LL * n * L.PH * L.PW : Mc, L.OC, L.Npad, L.K, L.H, L.W, L.C, epi, s, 1,
+                                L.pool ? 1 : 0);
           }
           break;
         default:

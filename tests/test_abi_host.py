@@ -179,8 +179,8 @@ def test_plan_shape_memory_and_flops_host_only(monkeypatch, fuse, splitk):
 
 
 def test_plan_x3_structure_host_only(monkeypatch):
-    """Default fp32 batch plan: conv4-conv7 on the x3 conv (exact 3-way bf16 splits), conv3's
-    pooled epilogue and the pools after conv4/conv5 writing their split planes; conv5 (N = 512)
+    """Default fp32 batch plan: conv4-conv7 on the x3 conv (exact 3-way bf16 splits), conv4 with
+    its 2x2 pool fused, conv3's pooled epilogue and pool5 writing split planes; conv5 (N = 512)
     in 2 K slices whose partials pool5 combines; weights of those layers in 3 bf16 pieces."""
     monkeypatch.delenv("DNN_HIP_X3", raising=False)
     ws = synth.yolo_weights()
@@ -191,8 +191,8 @@ def test_plan_x3_structure_host_only(monkeypatch):
     x3params = 9 * (128 * 256 + 256 * 512 + 512 * 1024 + 1024 * 1024)
     assert wb >= 4 * nparams + 2 * x3params and wb < (4 * nparams + 2 * x3params) * 1.2
     act2 = 2 * 64 * 208 * 208 * 16 * 4
-    # one zero-bordered split-plane region per producer: conv3 (26x26x128), pool4 (13x13x256),
-    # pool5 (13x13x512), conv6 (13x13x1024), 6 B per element
+    # one zero-bordered split-plane region per producer: conv3 (26x26x128), conv4 (pooled
+    # 13x13x256), pool5 (13x13x512), conv6 (13x13x1024), 6 B per element
     pad = sum(64 * 6 * (h + 2) ** 2 * c for h, c in ((26, 128), (13, 256), (13, 512), (13, 1024)))
     slab = 2 * 64 * 13 * 13 * 512 * 4  # conv5's two raw K-slice partials
     assert act2 + pad + slab <= sb < act2 + pad + slab + 16384
@@ -200,7 +200,8 @@ def test_plan_x3_structure_host_only(monkeypatch):
     conv = [ln for ln in lines if ln.startswith("conv")]
     assert [i for i, ln in enumerate(conv) if "patch_x3" in ln] == [4, 5, 6, 7]
     assert "splitK=2 x3-combine" in conv[5] and sum("splitK" in ln for ln in lines) == 1
-    assert sum(ln.startswith("pool") for ln in lines) == 2  # after conv4 (2x2 s2) and conv5 (s1)
+    assert "+pool2x2s2" in conv[4]  # conv4's pool fused into the x3 conv (pool-window-major rows)
+    assert sum(ln.startswith("pool") for ln in lines) == 1  # pool5 (s1, combines conv5's slices)
     # latency plans keep the fp32 MFMA (split-K over the idle chip)
     assert not any("patch_x3" in ln for ln in _describe_yolo(1, True))
 

@@ -457,8 +457,8 @@ def test_plan_timing_api(yolo_b1):
         plan.run_host(x)
     ms, cnt = plan.timing_end()
     ks = plan.kernels()
-    # 11 plan kernels: conv0-8 + pool4 (after conv4's x3 conv) + pool5 (combines conv5's K slices)
-    assert len(ms) == len(ks) == 11
+    # 10 plan kernels: conv0-8 + pool5 (combines conv5's K slices; conv4's pool is fused)
+    assert len(ms) == len(ks) == 10
     assert all(c == 3 for c in cnt)
     assert all(m > 0 for m in ms)
     # events around one kernel only (the bench's timed region): the others report no launches
@@ -468,7 +468,7 @@ def test_plan_timing_api(yolo_b1):
             plan.run_host(x)
         ms1, cnt1 = plan.timing_end()
         names = [k["name"] for k in ks]
-        assert [c for n, c in zip(names, cnt1) if n != only] == [0] * 10
+        assert [c for n, c in zip(names, cnt1) if n != only] == [0] * 9
         assert cnt1[names.index(only)] == 3 and ms1[names.index(only)] > 0
 
 
@@ -999,8 +999,9 @@ PATCH16_CASES = [
 ]
 
 
+@pytest.mark.parametrize("mf", ["16", "32"])
 @pytest.mark.parametrize("case", PATCH16_CASES)
-def test_fp16_patch_conv_vs_oracle(monkeypatch, case):
+def test_fp16_patch_conv_vs_oracle(monkeypatch, case, mf):
     """conv3x3_f16_patch_kernel (input staged once per 64-channel chunk for all 9 taps, weights
     straight to registers): whole chain within the fp16 layer tolerance of the fp32 oracle,
     both convs on mode patch16, and batch rows independent of the batch (row 0 alone == row 0
@@ -1028,6 +1029,7 @@ def test_fp16_patch_conv_vs_oracle(monkeypatch, case):
         return g
 
     monkeypatch.setenv("DNN_HIP_PATCH16", "1")
+    monkeypatch.setenv("DNN_HIP_P16MF", mf)  # 16x16x32 (176-row tiles, default) / 32x32x16 (192-row)
     eng = dnn_hip.DnnInferenceEngine(graph(x.shape), False, precision="fp16")
     assert eng.plan().describe().count("mode=patch16") == 2
     y = eng.run(x)
@@ -1171,6 +1173,69 @@ def test_x3_split_combine_and_producer_vs_oracle(monkeypatch, case):
         y = eng.run(x)
         errs[x3] = R.normwise_err(y, ref)
         print("x3=%s chain normwise err %.3e" % (x3, errs[x3]))
+        if x3 == "1":
+            y0 = dnn_hip.DnnInferenceEngine(graph((1,) + x.shape[1:]), False).run(x[:1])
+            assert np.array_equal(y0, y[:1])
+    assert errs["1"] < 3 * LAYER_TOL and errs["0"] < 3 * LAYER_TOL, errs
+    assert errs["1"] <= 1.25 * errs["0"], errs
+
+
+X3_POOL_CASES = [
+    # B, H, W, C: pool (2x2 s1) -> conv3x3 C->256 + pool 2x2 s2 fused into the x3 conv (rows
+    # pool-window-major) -> conv3x3 256->512 (x3, 2 K slices) -> pool 2x2 s1 (combine)
+    (8, 26, 26, 128),   # conv4-like
+    (3, 13, 13, 64),    # odd: ragged windows (cells past the edge repeat cell (0, 0))
+]
+
+
+@pytest.mark.parametrize("case", X3_POOL_CASES)
+def test_x3_pool_fused_vs_oracle(monkeypatch, case):
+    """x3 conv with its 2x2/s2 pool fused (pooled before the epilogue, written as the next x3
+    layer's split planes): modes as planned, chain within the fp32 tolerance of the float64
+    oracle and within 1.25x of the fp32-MFMA plan's error, negative-gamma channels, batch rows
+    bit-equal to batch-1 runs."""
+    B, H, W, C = case
+    rng = np.random.default_rng(B * 13 + C)
+    x = rng.standard_normal((B, H, W, C)).astype(np.float32)
+
+    def layer(c, od):
+        k = (rng.standard_normal((3, 3, c, od)) * np.sqrt(2.0 / (9 * c))).astype(np.float32)
+        b = rng.standard_normal(od).astype(np.float32) * 0.1
+        gam = rng.uniform(0.5, 1.5, od).astype(np.float32)
+        gam[::5] *= -1
+        return k, b, (rng.standard_normal(od).astype(np.float32) * 0.1, rng.uniform(0.5, 1.5, od).astype(np.float32),
+                      gam)
+
+    L1, L2 = layer(C, 256), layer(256, 512)
+
+    def graph(shape):
+        g = dnn_hip.DnnGraphBuilder()
+        y = g.create_input(list(shape))
+        y = g.create_max_pool2d(y, [1, 2, 2, 1], [1, 1, 1, 1], "SAME")
+        for idx, (k, b, n) in enumerate((L1, L2)):
+            y = g.create_conv2d(y, k, [1, 1, 1, 1], "SAME")
+            y = g.create_bias_add(y, b)
+            y = g.create_batch_norm(y, *n, 1e-5)
+            y = g.create_leaky_relu(y)
+            y = g.create_max_pool2d(y, [1, 2, 2, 1], [1, 2, 2, 1] if idx == 0 else [1, 1, 1, 1], "SAME")
+        g.set_out_node(y)
+        return g
+
+    ref = R.max_pool2d(x, [1, 2, 2, 1], [1, 1, 1, 1], "SAME")
+    for idx, (k, b, n) in enumerate((L1, L2)):
+        ref = R.leaky_relu(R.batch_norm(R.bias_add(R.conv2d(ref, k), b), *n, 1e-5))
+        ref = R.max_pool2d(ref, [1, 2, 2, 1], [1, 2, 2, 1] if idx == 0 else [1, 1, 1, 1], "SAME")
+    errs = {}
+    for x3 in ("1", "0"):
+        monkeypatch.setenv("DNN_HIP_X3", x3)
+        eng = dnn_hip.DnnInferenceEngine(graph(x.shape), False)
+        if x3 == "1":
+            conv = [ln for ln in eng.plan().describe().splitlines() if ln.startswith("conv")]
+            assert "mode=patch_x3" in conv[0] and "+pool2x2s2" in conv[0], conv
+            assert "mode=patch_x3" in conv[1] and "splitK=2 x3-combine" in conv[1], conv
+        y = eng.run(x)
+        errs[x3] = R.normwise_err(y, ref)
+        print("x3=%s pool-fused chain normwise err %.3e" % (x3, errs[x3]))
         if x3 == "1":
             y0 = dnn_hip.DnnInferenceEngine(graph((1,) + x.shape[1:]), False).run(x[:1])
             assert np.array_equal(y0, y[:1])
