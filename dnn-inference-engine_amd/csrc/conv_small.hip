@@ -201,7 +201,7 @@ template <int CIN>
 __global__ void __launch_bounds__(256)
 conv0_packed_pool_kernel(const float* __restrict__ in, const float* __restrict__ w, float* __restrict__ out,
                          DirectGeom g, int tilesX, int tilesY, int ntiles, const float* __restrict__ zero,
-                         EpiParams epi) {
+                         EpiParams epi, uint4 mags) {  // mags: magic numbers of tilesX, tilesY (div_magic)
   constexpr int K = 9 * CIN, KS = (K + 3) / 4, RW = SC_P * CIN, RS = C0_RS;
   static_assert(RW <= RS && RW <= 64, "patch row");
   __shared__ __attribute__((aligned(16))) float patch[3][(4 * C0_ROWS_PER_WAVE) * RS];  // triple buffer
@@ -234,8 +234,8 @@ conv0_packed_pool_kernel(const float* __restrict__ in, const float* __restrict__
   struct Tile {
     int b, ty, tx;
   };
-  auto coords = [&](int t) {
-    const int tt = t / tilesX, b = tt / tilesY;
+  auto coords = [&](int t) {  // two multiply-high divisions (scalar), not two integer divisions
+    const int tt = div_magic(t, mags.x, (int)mags.y), b = div_magic(tt, mags.z, (int)mags.w);
     return Tile{b, tt - b * tilesY, t - tt * tilesX};
   };
   // lane l of a patch row DMA copies float l of the row's 18 * CIN (the row is contiguous in
@@ -370,8 +370,12 @@ int launch_conv0_mfma(const float* in, const float* w, float* out, const DirectG
   // persistent: 8 workgroups per CU loop over the tiles
   const long long slots = 8LL * device_cu_count();
   const unsigned grid = (unsigned)(blocks < slots ? blocks : slots);
+  unsigned mx, my;
+  int sx, sy;
+  magic_u32(tilesX, &mx, &sx);
+  magic_u32(tilesY, &my, &sy);
   hipLaunchKernelGGL((conv0_packed_pool_kernel<3>), dim3(grid), dim3(256), 0, s, in, w, out, g, tilesX, tilesY,
-                     (int)blocks, zero, epi);
+                     (int)blocks, zero, epi, make_uint4(mx, (unsigned)sx, my, (unsigned)sy));
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
     set_error("launch conv0_packed: %s", hipGetErrorString(e));

@@ -119,6 +119,7 @@ struct ImplicitConv {
 };
 bool implicit_conv_supported(int C, int kh, int kw);
 void implicit_conv_magic(ImplicitConv* ic);
+void magic_u32(int d, unsigned* mag, int* sh);  // n / d == (umulhi(n, mag) + n) >> sh, 0 <= n < 2^31
 enum GemmMode : int { GEMM_DENSE = 0, GEMM_IMPLICIT = 1, GEMM_IMPLICIT_POOL = 2 };
 
 // ---------------------------------------------------------------- launchers

@@ -305,7 +305,7 @@ bool implicit_conv_supported(int C, int kh, int kw) {
 
 // n / d == (umulhi(n, mag) + n) >> sh for 0 <= n < 2^31: the round-up method of Granlund and
 // Montgomery with sh = ceil(log2 d), mag = floor(2^32 (2^sh - d) / d) + 1 (d = 1: mag 1, sh 0)
-static void magic_u32(int d, unsigned* mag, int* sh) {
+void magic_u32(int d, unsigned* mag, int* sh) {
   if (d <= 0) {
     *mag = 0;
     *sh = 0;
