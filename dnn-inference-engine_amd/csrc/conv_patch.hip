@@ -34,7 +34,7 @@ template <int C>
 __global__ void __launch_bounds__(256)
 conv3x3_patch_pool_kernel(const float* __restrict__ in, const float* __restrict__ Bt, float* __restrict__ out,
                           DirectGeom g, int N, int tilesX, int tilesY, int nblkN, const float* __restrict__ zero,
-                          EpiParams epi) {
+                          EpiParams epi, bf16_bits* __restrict__ out_split) {
   typedef Mfma<16> MM;
   constexpr int KP = patch_kpad(C);
   constexpr int PATCH = PT_PATCH * PT_PATCH * C;  // floats
@@ -123,7 +123,18 @@ conv3x3_patch_pool_kernel(const float* __restrict__ in, const float* __restrict_
     for (int i = 0; i < 4; ++i) {
       const int wy = (y0 >> 1) + 2 * wid + (i >> 1), wx = (x0 >> 1) + 4 * (i & 1) + fp;
       const float v = pool_then_epilogue(acc[i][j], pb, pm, ps, pg, epi.flags);
-      if (wy < g.PH && wx < g.PW && n < N) out[(((size_t)b * g.PH + wy) * g.PW + wx) * N + n] = v;
+      if (!(wy < g.PH && wx < g.PW && n < N)) continue;
+      if (out_split) {  // x3 split planes of the zero-bordered next-layer input
+        unsigned short s0, s1, s2;
+        split3(v, s0, s1, s2);
+        bf16_bits* d = out_split + (((size_t)b * (g.PH + 2) + wy + 1) * (g.PW + 2) + wx + 1) * (3 * (size_t)N) +
+                       (n >> 5) * 96 + (n & 31);
+        d[0] = s0;
+        d[32] = s1;
+        d[64] = s2;
+      } else {
+        out[(((size_t)b * g.PH + wy) * g.PW + wx) * N + n] = v;
+      }
     }
   }
 }
@@ -145,10 +156,14 @@ constexpr int PP_PIX = PT_PATCH * PT_PATCH;             // 324 patch pixels
 constexpr int PP_CH = (PP_PIX * PP_C + 255) / 256;      // 1-KiB DMA chunks per patch (21)
 constexpr int PP_WG_PER_CU = 3;                         // 2 x 21 KiB of LDS per workgroup
 
+// X3OUT: store the pooled outputs as x3 split planes (3 bf16 pieces, 2-B buffer stores) into a
+// zero-bordered [B][PH+2][PW+2][3][32] buffer at `out` (the next layer is an x3 conv)
+template <bool X3OUT>
 __global__ void __launch_bounds__(256, PP_WG_PER_CU)  // 3 waves per SIMD: <= 168 registers
 conv3x3_patch_pool_c16_persistent(const float* __restrict__ in, const float* __restrict__ Bt, int ldb,
                                   float* __restrict__ out, DirectGeom g, int tilesX, int tilesY, int ntiles,
                                   const float* __restrict__ zero, EpiParams epi) {
+  constexpr int NST = X3OUT ? 24 : 8;  // stores per tile and lane (always issued)
   typedef Mfma<16> MM;
   constexpr int C = PP_C;
   __shared__ __attribute__((aligned(1024))) float smem[2 * PP_CH * 256];
@@ -201,16 +216,17 @@ conv3x3_patch_pool_c16_persistent(const float* __restrict__ in, const float* __r
     }
   };
 
-  const auto orsrc = out_rsrc(out, (unsigned)((size_t)g.B * g.PH * g.PW * 32 * sizeof(float)));
+  const auto orsrc = out_rsrc(out, X3OUT ? (unsigned)((size_t)g.B * (g.PH + 2) * (g.PW + 2) * 32 * 6)
+                                       : (unsigned)((size_t)g.B * g.PH * g.PW * 32 * sizeof(float)));
   int t = blockIdx.x, buf = 0;
   if (t < ntiles) issue_patch(t, 0);
   for (; t < ntiles; t += gridDim.x) {
-    // this wave's DMAs of `buf` landed: all but the previous tile's 8 stores (issued after
-    // them, never branched around: store4) have completed
+    // this wave's DMAs of `buf` landed: all but the previous tile's NST stores (issued after
+    // them, never branched around: buffer stores) have completed
     if (buf == 0 && t == (int)blockIdx.x)
       wait_vmcnt<0>();
     else
-      wait_vmcnt<8>();
+      wait_vmcnt<NST>();
     raw_barrier();    // everyone's landed; everyone finished reading buf ^ 1
     if (t + (int)gridDim.x < ntiles) issue_patch(t + gridDim.x, buf ^ 1);
     const float* P = smem + buf * PP_CH * 256;
@@ -242,7 +258,18 @@ conv3x3_patch_pool_c16_persistent(const float* __restrict__ in, const float* __r
       for (int i = 0; i < 4; ++i) {
         const int wy = ty * (PT_EDGE / 2) + 2 * wid + (i >> 1), wx = tx * (PT_EDGE / 2) + 4 * (i & 1) + fp;
         const float v = pool_then_epilogue(acc[i][j], pb[j], pm[j], ps[j], pg[j], epi.flags);
-        store4(orsrc, (wy < g.PH && wx < g.PW) ? (unsigned)(((((size_t)b * g.PH + wy) * g.PW + wx) * 32 + n) * 4) : OOB_OFF, v);
+        const bool in_frame = wy < g.PH && wx < g.PW;
+        if constexpr (X3OUT) {
+          unsigned short s0, s1, s2;
+          split3(v, s0, s1, s2);
+          const unsigned o = in_frame ? (unsigned)(((((size_t)b * (g.PH + 2) + wy + 1) * (g.PW + 2) + wx + 1) * 96 + n) * 2)
+                                      : OOB_OFF;
+          __builtin_amdgcn_raw_buffer_store_b16(s0, orsrc, o, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b16(s1, orsrc, o + (in_frame ? 64u : 0u), 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b16(s2, orsrc, o + (in_frame ? 128u : 0u), 0, 0);
+        } else {
+          store4(orsrc, in_frame ? (unsigned)(((((size_t)b * g.PH + wy) * g.PW + wx) * 32 + n) * 4) : OOB_OFF, v);
+        }
       }
     }
     buf ^= 1;
@@ -261,7 +288,8 @@ bool patch_conv_pool_supported(int C, int OC, int H, int W, int OH, int OW, int 
 int patch_conv_kpad(int C) { return patch_kpad(C); }
 
 int launch_conv3x3_patch_pool(const float* in, const float* Bt, int ldb, float* out, const DirectGeom& g, int C,
-                              int N, const float* zero, const EpiParams& epi, hipStream_t stream) {
+                              int N, const float* zero, const EpiParams& epi, hipStream_t stream,
+                              unsigned short* out_split) {
   if (g.B == 0) return 0;
   if (!(C == 16 || C == 32) || N % PT_NB != 0 || ldb != patch_kpad(C) || g.OH % 2 || g.OW % 2 ||
       g.PH != g.OH / 2 || g.PW != g.OW / 2 || g.OH != g.H || g.OW != g.W || g.pt != 1 || g.pl != 1) {
@@ -275,19 +303,23 @@ int launch_conv3x3_patch_pool(const float* in, const float* Bt, int ldb, float* 
     set_error("patch conv: grid too large");
     return -2;
   }
-  if (C == 16 && N == 32 && (size_t)g.B * g.PH * g.PW * 32 * sizeof(float) < OOB_OFF &&
-      !getenv_flag_off("DNN_HIP_PATCH_PERSIST")) {
+  const size_t out_bytes = out_split ? (size_t)g.B * (g.PH + 2) * (g.PW + 2) * N * 6 : (size_t)g.B * g.PH * g.PW * N * 4;
+  if (C == 16 && N == 32 && out_bytes < OOB_OFF && !getenv_flag_off("DNN_HIP_PATCH_PERSIST")) {
     // persistent: as many workgroups as fit resident (3 per CU by LDS), each looping over tiles
     const long long slots = (long long)device_cu_count() * PP_WG_PER_CU;
     const unsigned grid = (unsigned)(blocks < slots ? blocks : slots);
-    hipLaunchKernelGGL(conv3x3_patch_pool_c16_persistent, dim3(grid), dim3(256), 0, stream, in, Bt, ldb, out, g,
-                       tilesX, tilesY, (int)blocks, zero, epi);
+    if (out_split)
+      hipLaunchKernelGGL(conv3x3_patch_pool_c16_persistent<true>, dim3(grid), dim3(256), 0, stream, in, Bt, ldb,
+                         reinterpret_cast<float*>(out_split), g, tilesX, tilesY, (int)blocks, zero, epi);
+    else
+      hipLaunchKernelGGL(conv3x3_patch_pool_c16_persistent<false>, dim3(grid), dim3(256), 0, stream, in, Bt, ldb, out,
+                         g, tilesX, tilesY, (int)blocks, zero, epi);
   } else if (C == 16)
     hipLaunchKernelGGL((conv3x3_patch_pool_kernel<16>), dim3((unsigned)blocks), dim3(256), 0, stream, in, Bt, out, g,
-                       N, tilesX, tilesY, nblkN, zero, epi);
+                       N, tilesX, tilesY, nblkN, zero, epi, reinterpret_cast<bf16_bits*>(out_split));
   else
     hipLaunchKernelGGL((conv3x3_patch_pool_kernel<32>), dim3((unsigned)blocks), dim3(256), 0, stream, in, Bt, out, g,
-                       N, tilesX, tilesY, nblkN, zero, epi);
+                       N, tilesX, tilesY, nblkN, zero, epi, reinterpret_cast<bf16_bits*>(out_split));
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
     set_error("launch conv3x3_patch_pool: %s", hipGetErrorString(e));

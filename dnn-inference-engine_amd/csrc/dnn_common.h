@@ -182,8 +182,11 @@ int launch_conv3x3_pool2_direct(const float* in, const float* w, float* out, con
 bool patch_conv_pool_supported(int C, int OC, int H, int W, int OH, int OW, int kh, int kw, int sh, int sw, int pt,
                                int pl);
 int patch_conv_kpad(int C);
+// out_split != nullptr: the pooled outputs as x3 split planes of a zero-bordered
+// [B][PH+2][PW+2] buffer (the next layer is an x3 conv); `out` unused
 int launch_conv3x3_patch_pool(const float* in, const float* Bt, int ldb, float* out, const DirectGeom& g, int C,
-                              int N, const float* zero, const EpiParams& epi, hipStream_t stream);
+                              int N, const float* zero, const EpiParams& epi, hipStream_t stream,
+                              unsigned short* out_split = nullptr);
 
 // ---------------------------------------------------------------- fp16 path (kernels_f16.hip)
 // fp16 activations / weights, v_mfma_f32_32x32x16_f16 with fp32 accumulate and epilogue.
@@ -234,7 +237,9 @@ int x3_splits(int N, int K);  // split-K of an x3 batch-plan layer: a function o
 int launch_conv_x3(const unsigned short* in_split, const unsigned short* Bt, float* out, unsigned short* out_split,
                    long long M, int N, int Npad, int K, int H, int W, int C, const EpiParams& epi, hipStream_t stream,
                    int splits = 1, int pool = 0);
-bool conv_x3_pool_supported(int H, int W);  // an x3 conv of this size can fuse a 2x2/s2 pool
+bool conv_x3_pool_supported(int OC, int C, int H, int W);  // an x3 conv of this size can fuse a 2x2/s2 pool
+// x3 workgroups of a layer (batch-1 latency plans take x3 only where they fill half the chip)
+long long x3_tiles(long long batch, int OH, int OW, int OC, int C, int K);
 int launch_x3_combine(const float* part, int splits, long long slab, const EpiParams& epi, const PoolGeom& g,
                       float* out, unsigned short* out_split, hipStream_t s);
 int patch16_pack_order();  // launch_pack_weights order of the patch kernel's MFMA shape (3 or 4)

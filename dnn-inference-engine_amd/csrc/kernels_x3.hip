@@ -282,7 +282,7 @@ __global__ void pack_weights_x3_kernel(const float* __restrict__ w, bf16_bits* _
 }
 
 int launch_pack_weights_x3(const float* w, bf16_bits* out, int K, int N, int Npad, int C, hipStream_t s) {
-  if (K != 9 * C || C % 32 != 0 || Npad % 256 != 0 || Npad < N) {
+  if (K != 9 * C || C % 32 != 0 || Npad % 64 != 0 || Npad < N) {
     set_error("pack_weights_x3: unsupported K=%d N=%d Npad=%d C=%d", K, N, Npad, C);
     return -2;
   }
@@ -324,26 +324,51 @@ static long long x3_span(long long M, int H, int W, bool pool = false) {
   return mx;
 }
 
-bool conv_x3_supported(int C, int OC, int H, int W, int OH, int OW, int kh, int kw, int sh, int sw, int pt, int pl) {
-  if (!(kh == 3 && kw == 3 && sh == 1 && sw == 1 && pt == 1 && pl == 1 && OH == H && OW == W && C % 32 == 0 &&
-        OC % 256 == 0 && x3_enabled()))
-    return false;
-  // a tile must fit the patch for any batch: spans grow with M only until a tile crosses whole
-  // images, so two images' worth of rows decides it
-  return x3_span(2LL * H * W + X3_BM, H, W) <= X3_NPR;
+// narrow layers: the 2-D tile kernel (conv3x3_x3_tile_kernel), 4 x 52 output pixels per tile
+// (YOLOv2-tiny's 104- and 52-wide frames in whole tiles, 1.56x patch rows per output row)
+constexpr int X3T_TH = 4, X3T_TW = 52, X3T_TM = 7;  // 2 x 7 row blocks of 16 >= 208 rows
+
+// which kernel runs an x3 layer: 0 the row-run kernel (N % 256 == 0), 1 tile kernel N = 64 from
+// one 32-channel chunk (4 waves, two workgroups per CU), 2 tile kernel N % 128 == 0 (8 waves,
+// double-buffered chunks); -1 none (the layer stays on the fp32 MFMA)
+static int x3_kind(int N, int C) {
+  if (N % 256 == 0) return 0;
+  if (N == 64 && C == 32) return 1;
+  if (N % 128 == 0) return 2;
+  return -1;
 }
 
-// ... with a fused 2x2/s2 pool (pool-window-major rows)
-bool conv_x3_pool_supported(int H, int W) {
+bool conv_x3_supported(int C, int OC, int H, int W, int OH, int OW, int kh, int kw, int sh, int sw, int pt, int pl) {
+  if (!(kh == 3 && kw == 3 && sh == 1 && sw == 1 && pt == 1 && pl == 1 && OH == H && OW == W && C % 32 == 0 &&
+        x3_enabled()))
+    return false;
+  const int kind = x3_kind(OC, C);
+  if (kind < 0 || (kind > 0 && getenv_flag_off("DNN_HIP_X3_TILE"))) return false;
+  // a tile must fit the patch for any batch: spans grow with M only until a tile crosses whole
+  // images, so two images' worth of rows decides it (tile kernel: fixed patch)
+  return kind > 0 || x3_span(2LL * H * W + X3_BM, H, W) <= X3_NPR;
+}
+
+// ... with a fused 2x2/s2 pool (pool-window-major rows; tile kernel: even frames, so windows
+// never straddle tiles or the frame edge)
+bool conv_x3_pool_supported(int OC, int C, int H, int W) {
+  if (x3_kind(OC, C) > 0) return H % 2 == 0 && W % 2 == 0;
   const long long rows = 4LL * ((H + 1) / 2) * ((W + 1) / 2);
   return x3_span(2 * rows + X3_BM, H, W, true) <= X3_NPR_POOL;
+}
+
+long long x3_tiles(long long batch, int OH, int OW, int OC, int C, int K) {
+  const int kind = x3_kind(OC, C);
+  if (kind > 0)
+    return batch * ((OH + X3T_TH - 1) / X3T_TH) * ((OW + X3T_TW - 1) / X3T_TW) * (OC / (kind == 1 ? 64 : 128));
+  return (batch * OH * OW + X3_BM - 1) / X3_BM * (OC / 256) * x3_splits(OC, K);
 }
 
 size_t x3_act_bytes(long long nimg, int H, int W, int C) { return (size_t)nimg * (H + 2) * (W + 2) * C * 6; }
 
 // N = 512 (conv5): 62 x 2 = 124 tiles of 176 x 256 at batch 64, half the chip -> 2 K slices;
 // wider layers fill it alone, narrower ones (N = 256: 246 tiles) too
-int x3_splits(int N, int K) { return (N > 256 && N <= 512 && (K / 288) % 2 == 0) ? 2 : 1; }
+int x3_splits(int N, int K) { return (N % 256 == 0 && N > 256 && N <= 512 && (K / 288) % 2 == 0) ? 2 : 1; }
 
 
 int launch_conv_x3(const bf16_bits* in_split, const bf16_bits* Bt, float* out, bf16_bits* out_split, long long M,
@@ -356,6 +381,36 @@ int launch_conv_x3(const bf16_bits* in_split, const bf16_bits* Bt, float* out, b
   const long long nimg = M / per_img;
   const long long in_bytes = (long long)x3_act_bytes(nimg, H, W, C);
   const long long b_bytes = (long long)(Npad / 16) * (K / 32) * 3072;
+  const int kind = x3_kind(N, C);
+  if (kind > 0) {
+    if (M % per_img != 0 || K != 9 * C || Npad != N || splits != 1 || (pool && (H % 2 || W % 2)) ||
+        in_bytes >= 0x80000000LL || b_bytes >= 0x80000000LL || (out_split == nullptr) == (out == nullptr) ||
+        x3_act_bytes(nimg, pool ? PH : H, pool ? PW : W, N) >= 0x80000000ULL) {
+      set_error("conv_x3 (tile): unsupported shape M=%lld N=%d K=%d %dx%dx%d", M, N, K, H, W, C);
+      return -2;
+    }
+    const int tilesX = (W + X3T_TW - 1) / X3T_TW, tilesY = (H + X3T_TH - 1) / X3T_TH, tilesN = N / (kind == 1 ? 64 : 128);
+    const long long blocks = nimg * tilesX * tilesY * tilesN;
+    if (blocks > 0x7fffffffLL) {
+      set_error("conv_x3 (tile): grid too large");
+      return -2;
+    }
+    const X3Geom xg{H, W, C, out_split ? 1 : 0, 1, PH, PW};
+#define X3T(WN, NBUF, POOL)                                                                                        \
+  hipLaunchKernelGGL((conv3x3_x3_tile_kernel<X3T_TH, X3T_TW, 2, WN, X3T_TM, NBUF, POOL>), dim3((unsigned)blocks), \
+                     dim3(128 * WN), 0, stream, in_split, Bt, out, out_split, N, K, epi, tilesX, tilesY, tilesN, xg,  \
+                     (unsigned)in_bytes, (unsigned)b_bytes)
+    if (kind == 1 && pool)
+      X3T(2, 1, true);
+    else if (kind == 1)
+      X3T(2, 1, false);
+    else if (pool)
+      X3T(4, 2, true);
+    else
+      X3T(4, 2, false);
+#undef X3T
+    return check_x3("conv_x3 (tile)");
+  }
   if (M % per_img != 0 || K != 9 * C || C % 32 != 0 || N % 256 != 0 || Npad != N || (pool && splits != 1) ||
       in_bytes >= 0x80000000LL || b_bytes >= 0x80000000LL || M > 0x7fffffffLL ||
       x3_span(M, H, W, pool != 0) > (pool ? X3_NPR_POOL : X3_NPR) ||

@@ -297,10 +297,10 @@ void dnn_plan_destroy(dnn_plan* p) {
 
 static void set_cfg(dnn_plan* p, PlanLayer& L) {
   const long long M = (long long)p->batch * L.OH * L.OW;
-  if (!p->fp16 && L.mode == MODE_X3) {  // one config: 176x256 tiles; split-K by (N, K) only
+  if (!p->fp16 && L.mode == MODE_X3) {  // one config per width (kernels_x3.hip); split-K by (N, K) only
     L.cfg = 0;
     L.Kpad = L.K;
-    L.Npad = (int)align_up(L.OC, 256);
+    L.Npad = L.OC;  // (a multiple of 256, or of 64 for the tile kernel)
     L.splits = x3_splits(L.OC, L.K);
     return;
   }
@@ -426,14 +426,16 @@ int dnn_plan_add_conv(dnn_plan* p, int kh, int kw, int od, int stride_h, int str
   // where its tiles fill half the chip: at batch 1 a 176 x 256 tile's one-chunk K slice alone
   // takes ~26 us (measured: conv6/conv7 as 16 / 32 x3 slices 0.053 / 0.056 ms with their
   // combines, against 0.034 / 0.050 on the fp32 MFMA with split-K 16)
-  const long long x3_tiles = ((long long)p->batch * L.OH * L.OW + 175) / 176 * (od / 256) * x3_splits(od, L.K);
-  if (!p->fp16 && (!p->latency || !fused_splitk(p) || x3_tiles >= 128) && L.mode == MODE_IMPLICIT && !p->layers.empty() &&
-      conv_x3_supported(L.C, od, L.H, L.W, L.OH, L.OW, kh, kw, stride_h, stride_w, L.pt, L.pl)) {
-    // producers that can write the split planes: a separate pool, another x3 conv, or a
-    // pool-fused implicit GEMM without split-K (its epilogue splits, EPI_OUT_X3)
+  if (!p->fp16 && L.mode == MODE_IMPLICIT && !p->layers.empty() &&
+      conv_x3_supported(L.C, od, L.H, L.W, L.OH, L.OW, kh, kw, stride_h, stride_w, L.pt, L.pl) &&
+      (!p->latency || !fused_splitk(p) || x3_tiles(p->batch, L.OH, L.OW, od, L.C, L.K) >= 128)) {
+    // producers that can write the split planes: a separate pool, another x3 conv, a pool-fused
+    // implicit GEMM without split-K (its epilogue splits, EPI_OUT_X3) or the pool-fused patch
+    // conv (conv1)
     PlanLayer& prev = p->layers.back();
     if ((prev.type == 1 && prev.C % 32 == 0) || (prev.type == 0 && prev.mode == MODE_X3) ||
-        (prev.type == 0 && prev.mode == MODE_IMPLICIT && prev.pool && prev.splits == 1)) {
+        (prev.type == 0 && prev.mode == MODE_IMPLICIT && prev.pool && prev.splits == 1) ||
+        (prev.type == 0 && prev.mode == MODE_PATCH && prev.pool)) {
       L.mode = MODE_X3;
       prev.out_padded = true;
     }
@@ -520,7 +522,7 @@ int dnn_plan_add_max_pool(dnn_plan* p, int kh, int kw, int stride_h, int stride_
                                                                       prev.sw)) {
         prev.mode = MODE_DIRECT;
         ok = true;
-      } else if (prev.mode == MODE_X3 && !p->fp16 && conv_x3_pool_supported(prev.H, prev.W) &&
+      } else if (prev.mode == MODE_X3 && !p->fp16 && conv_x3_pool_supported(prev.OC, prev.C, prev.H, prev.W) &&
                  !getenv_flag_off("DNN_HIP_X3_POOL")) {
         ok = true;  // pool-window-major rows, pooled before the epilogue in the x3 kernel
       }
@@ -820,7 +822,7 @@ int dnn_plan_run(dnn_plan* p, int n, const float* d_in, float* d_out, void* stre
         }
         case MODE_PATCH: {
           DirectGeom g{n, L.H, L.W, L.OH, L.OW, L.PH, L.PW, L.pt, L.pl};
-          rc = launch_conv3x3_patch_pool(cur, wt, L.Kpad, dst, g, L.C, L.OC, zero, epi, s);
+          rc = launch_conv3x3_patch_pool(cur, wt, L.Kpad, dst, g, L.C, L.OC, zero, epi, s, dsplit);
           break;
         }
         case MODE_X3:

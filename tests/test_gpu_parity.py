@@ -1241,3 +1241,81 @@ def test_x3_pool_fused_vs_oracle(monkeypatch, case):
             assert np.array_equal(y0, y[:1])
     assert errs["1"] < 3 * LAYER_TOL and errs["0"] < 3 * LAYER_TOL, errs
     assert errs["1"] <= 1.25 * errs["0"], errs
+
+
+X3_TILE_CASES = [
+    # B, H, W, form.  "pool": conv3x3 16->32 + pool 2x2 s2 (pool-fused patch conv, conv1-like,
+    # writing split planes) -> 32->64 + pool (tile kernel, 4 waves) -> 64->128 + pool (tile kernel,
+    # 8 waves; fused when the frame is even) -> 128->256 (row-run x3 kernel).  "raster": pool 2x2 s1
+    # -> 32->64 -> 64->128, no pools (raster tile rows; ragged tiles in both directions)
+    (3, 104, 104, "pool"),  # conv2/conv3-like frames: 52 / 26 wide, whole 4 x 52 tiles
+    (2, 60, 60, "pool"),    # 30 wide: one partial tile per row band; 15x15 after: separate pool
+    (2, 27, 61, "raster"),
+]
+
+
+@pytest.mark.parametrize("case", X3_TILE_CASES)
+def test_x3_tile_kernel_vs_oracle(monkeypatch, case):
+    """conv3x3_x3_tile_kernel (N = 64 / 128 on 2-D 4 x 52 output tiles) and the patch conv's
+    split-plane epilogue: modes as planned, the chain within the fp32 tolerance of the float64
+    oracle and within 1.25x of the fp32-MFMA plan's error (DNN_HIP_X3=0), negative-gamma
+    channels, batch rows bit-equal to batch-1 runs, repeat runs identical."""
+    B, H, W, form = case
+    rng = np.random.default_rng(B * 31 + H + W)
+
+    def layer(c, od):
+        k = (rng.standard_normal((3, 3, c, od)) * np.sqrt(2.0 / (9 * c))).astype(np.float32)
+        b = rng.standard_normal(od).astype(np.float32) * 0.1
+        gam = rng.uniform(0.5, 1.5, od).astype(np.float32)
+        gam[::5] *= -1
+        return k, b, (rng.standard_normal(od).astype(np.float32) * 0.1, rng.uniform(0.5, 1.5, od).astype(np.float32),
+                      gam)
+
+    if form == "pool":
+        x = rng.standard_normal((B, H, W, 16)).astype(np.float32)
+        layers = [(layer(16, 32), True), (layer(32, 64), True), (layer(64, 128), True), (layer(128, 256), False)]
+    else:
+        x = rng.standard_normal((B, H, W, 32)).astype(np.float32)
+        layers = [(layer(32, 64), False), (layer(64, 128), False)]
+
+    def graph(shape):
+        g = dnn_hip.DnnGraphBuilder()
+        y = g.create_input(list(shape))
+        if form == "raster":
+            y = g.create_max_pool2d(y, [1, 2, 2, 1], [1, 1, 1, 1], "SAME")
+        for (k, b, n), pool in layers:
+            y = g.create_conv2d(y, k, [1, 1, 1, 1], "SAME")
+            y = g.create_bias_add(y, b)
+            y = g.create_batch_norm(y, *n, 1e-5)
+            y = g.create_leaky_relu(y)
+            if pool:
+                y = g.create_max_pool2d(y, [1, 2, 2, 1], [1, 2, 2, 1], "SAME")
+        g.set_out_node(y)
+        return g
+
+    ref = R.max_pool2d(x, [1, 2, 2, 1], [1, 1, 1, 1], "SAME") if form == "raster" else x
+    for (k, b, n), pool in layers:
+        ref = R.leaky_relu(R.batch_norm(R.bias_add(R.conv2d(ref, k), b), *n, 1e-5))
+        if pool:
+            ref = R.max_pool2d(ref, [1, 2, 2, 1], [1, 2, 2, 1], "SAME")
+    errs = {}
+    for x3 in ("1", "0"):
+        monkeypatch.setenv("DNN_HIP_X3", x3)
+        eng = dnn_hip.DnnInferenceEngine(graph(x.shape), False)
+        if x3 == "1":
+            conv = [ln for ln in eng.plan().describe().splitlines() if ln.startswith("conv")]
+            if form == "pool":
+                assert "mode=patch" in conv[0] and "+pool2x2s2" in conv[0], conv
+                assert all("mode=patch_x3" in c for c in conv[1:]), conv
+                assert "+pool2x2s2" in conv[1] and ("+pool2x2s2" in conv[2]) == (H % 8 == 0), conv
+            else:
+                assert all("mode=patch_x3" in c for c in conv), conv
+        y = eng.run(x)
+        errs[x3] = R.normwise_err(y, ref)
+        print("x3=%s tile chain normwise err %.3e" % (x3, errs[x3]))
+        if x3 == "1":
+            y0 = dnn_hip.DnnInferenceEngine(graph((1,) + x.shape[1:]), False).run(x[:1])
+            assert np.array_equal(y0, y[:1])
+            assert np.array_equal(eng.run(x), y)
+    assert errs["1"] < 3 * LAYER_TOL and errs["0"] < 3 * LAYER_TOL, errs
+    assert errs["1"] <= 1.25 * errs["0"], errs
