@@ -324,9 +324,9 @@ static long long x3_span(long long M, int H, int W, bool pool = false) {
   return mx;
 }
 
-// narrow layers: the 2-D tile kernel (conv3x3_x3_tile_kernel), 4 x 52 output pixels per tile
-// (YOLOv2-tiny's 104- and 52-wide frames in whole tiles, 1.56x patch rows per output row)
-constexpr int X3T_TH = 4, X3T_TW = 52, X3T_TM = 7;  // 2 x 7 row blocks of 16 >= 208 rows
+// narrow layers: the 2-D tile kernel (conv3x3_x3_tile_kernel), 8 x 26 (N = 64) or 4 x 26
+// (N % 128 == 0) output pixels per tile: YOLOv2-tiny's 104- and 52-wide frames in whole tiles
+constexpr int X3T_TM = 7;  // row blocks of 16 per wave
 
 // which kernel runs an x3 layer: 0 the row-run kernel (N % 256 == 0), 1 tile kernel N = 64 from
 // one 32-channel chunk (4 waves, two workgroups per CU), 2 tile kernel N % 128 == 0 (8 waves,
@@ -360,7 +360,7 @@ bool conv_x3_pool_supported(int OC, int C, int H, int W) {
 long long x3_tiles(long long batch, int OH, int OW, int OC, int C, int K) {
   const int kind = x3_kind(OC, C);
   if (kind > 0)
-    return batch * ((OH + X3T_TH - 1) / X3T_TH) * ((OW + X3T_TW - 1) / X3T_TW) * (OC / (kind == 1 ? 64 : 128));
+    return batch * ((OH + (kind == 1 ? 7 : 3)) / (kind == 1 ? 8 : 4)) * ((OW + 25) / 26) * (OC / (kind == 1 ? 64 : 128));
   return (batch * OH * OW + X3_BM - 1) / X3_BM * (OC / 256) * x3_splits(OC, K);
 }
 
@@ -389,25 +389,30 @@ int launch_conv_x3(const bf16_bits* in_split, const bf16_bits* Bt, float* out, b
       set_error("conv_x3 (tile): unsupported shape M=%lld N=%d K=%d %dx%dx%d", M, N, K, H, W, C);
       return -2;
     }
-    const int tilesX = (W + X3T_TW - 1) / X3T_TW, tilesY = (H + X3T_TH - 1) / X3T_TH, tilesN = N / (kind == 1 ? 64 : 128);
+    // kind 2: 4 x 26 tiles, 4 waves (1 x 4), 2 workgroups per CU (64.5 KB LDS each): at batch 64
+    // conv3 is 1,664 tiles, 6.5 per CU, where 4 x 52 tiles of 8 waves were 3.25 rounds of one per
+    // CU (measured 0.157 -> 0.131 ms).  kind 1: 8 x 26 tiles (1.35x patch rows per output row;
+    // 4 x 52: 1.56x, conv2 0.142 -> 0.140 ms)
+    const int TH = kind == 1 ? 8 : 4, TW = 26;
+    const int tilesX = (W + TW - 1) / TW, tilesY = (H + TH - 1) / TH, tilesN = N / (kind == 1 ? 64 : 128);
     const long long blocks = nimg * tilesX * tilesY * tilesN;
     if (blocks > 0x7fffffffLL) {
       set_error("conv_x3 (tile): grid too large");
       return -2;
     }
     const X3Geom xg{H, W, C, out_split ? 1 : 0, 1, PH, PW};
-#define X3T(WN, NBUF, POOL)                                                                                        \
-  hipLaunchKernelGGL((conv3x3_x3_tile_kernel<X3T_TH, X3T_TW, 2, WN, X3T_TM, NBUF, POOL>), dim3((unsigned)blocks), \
-                     dim3(128 * WN), 0, stream, in_split, Bt, out, out_split, N, K, epi, tilesX, tilesY, tilesN, xg,  \
-                     (unsigned)in_bytes, (unsigned)b_bytes)
-    if (kind == 1 && pool)
-      X3T(2, 1, true);
-    else if (kind == 1)
-      X3T(2, 1, false);
+#define X3T(TH_, TW_, WM, WN, NBUF, POOL)                                                                        \
+  hipLaunchKernelGGL((conv3x3_x3_tile_kernel<TH_, TW_, WM, WN, X3T_TM, NBUF, POOL>), dim3((unsigned)blocks),      \
+                     dim3(64 * WM * WN), 0, stream, in_split, Bt, out, out_split, N, K, epi, tilesX, tilesY, tilesN, \
+                     xg, (unsigned)in_bytes, (unsigned)b_bytes)
+    if (kind == 2 && pool)
+      X3T(4, 26, 1, 4, 2, true);
+    else if (kind == 2)
+      X3T(4, 26, 1, 4, 2, false);
     else if (pool)
-      X3T(4, 2, true);
+      X3T(8, 26, 2, 2, 1, true);
     else
-      X3T(4, 2, false);
+      X3T(8, 26, 2, 2, 1, false);
 #undef X3T
     return check_x3("conv_x3 (tile)");
   }

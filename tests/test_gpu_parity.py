@@ -1248,7 +1248,7 @@ X3_TILE_CASES = [
     # writing split planes) -> 32->64 + pool (tile kernel, 4 waves) -> 64->128 + pool (tile kernel,
     # 8 waves; fused when the frame is even) -> 128->256 (row-run x3 kernel).  "raster": pool 2x2 s1
     # -> 32->64 -> 64->128, no pools (raster tile rows; ragged tiles in both directions)
-    (3, 104, 104, "pool"),  # conv2/conv3-like frames: 52 / 26 wide, whole 4 x 52 tiles
+    (3, 104, 104, "pool"),  # conv2/conv3-like frames: 52 / 26 wide, whole 8 x 26 / 4 x 26 tiles
     (2, 60, 60, "pool"),    # 30 wide: one partial tile per row band; 15x15 after: separate pool
     (2, 27, 61, "raster"),
 ]
@@ -1256,7 +1256,7 @@ X3_TILE_CASES = [
 
 @pytest.mark.parametrize("case", X3_TILE_CASES)
 def test_x3_tile_kernel_vs_oracle(monkeypatch, case):
-    """conv3x3_x3_tile_kernel (N = 64 / 128 on 2-D 4 x 52 output tiles) and the patch conv's
+    """conv3x3_x3_tile_kernel (N = 64 / 128 on 2-D 8 x 26 / 4 x 26 output tiles) and the patch conv's
     split-plane epilogue: modes as planned, the chain within the fp32 tolerance of the float64
     oracle and within 1.25x of the fp32-MFMA plan's error (DNN_HIP_X3=0), negative-gamma
     channels, batch rows bit-equal to batch-1 runs, repeat runs identical."""
