@@ -538,4 +538,218 @@ conv3x3_x3_tile_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __rest
   }
 }
 
+// 16-channel layers (YOLOv2-tiny conv1, 208x208x16 -> 32): the input is the producer's plain
+// fp32 NHWC (no split planes), split into the three bf16 pieces while the patch is staged
+// (frame padding = the descriptor's zeros).  K = 144 runs as 5 steps of 32: step s feeds k
+// 0-15 from tap 2s and k 16-31 from tap 2s + 1 (lane group fq >> 1 picks the tap; tap 9 has zero
+// weights), so a lane's A fragment is 8 channels of one tap, 16 B at patch pixel (row + tap
+// offset) * 96 + 32 piece + 16 (fq & 1) (conflict-free for 16 consecutive or window-major rows
+// at the 96-B pitch).  The 30 KB of weights of the 32 columns (all of K) are copied into LDS
+// once per workgroup and read per step (6 fragments per 7 row blocks), instead of every wave
+// streaming them from L2 (73 B per MFMA at 2 waves per tile).  One chunk: no double buffer;
+// two workgroups per CU overlap each other's staging.  Same product order per step as the
+// kernels above; 32 columns (WN = 1), WM waves of TM 16-row blocks.
+template <int TH, int TW, int WM, int TM, bool POOL>
+__global__ void __launch_bounds__(64 * WM, 2)  // (waves per SIMD) two: <= 256 registers
+conv3x3_x3_c16_kernel(const float* __restrict__ in, const bf16_bits* __restrict__ Bt, float* __restrict__ out,
+                      bf16_bits* __restrict__ out_split, int N, EpiParams epi, int tilesX, int tilesY, X3Geom g,
+                      unsigned in_bytes) {
+  constexpr int NT = 64 * WM, PB = 96, PW2 = TW + 2, PR = (TH + 2) * PW2, T = TH * TW, NS = 5;
+  constexpr int ITEMS = PR * 4, PPT = (ITEMS + NT - 1) / NT;  // item = (patch pixel, channel quad)
+  constexpr int BB = 2 * NS * 3 * 1024, BPT = (BB / 16 + NT - 1) / NT;  // weight bytes, 16-B loads/thread
+  static_assert(TH % 2 == 0 && TW % 2 == 0 && WM * TM * 16 >= T && (WM * TM - 3) * 16 < T, "shape");
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[BB + PR * PB];
+  unsigned char* const patch = smem + BB;
+
+  const int lane = threadIdx.x & 63;
+  const int wm = wave_uniform(threadIdx.x >> 6);
+  int t = xcd_tile(blockIdx.x, gridDim.x);
+  const int tx = t % tilesX;
+  t /= tilesX;
+  const int ty = t % tilesY;
+  const int b = t / tilesY;
+  const int y0 = ty * TH, x0 = tx * TW;
+
+  // weights: the packed [n/16][step][piece][lane][8] block of columns 0-31 is contiguous
+  {
+    u32x4 w[BPT];
+#pragma unroll
+    for (int u = 0; u < BPT; ++u) {
+      int e = threadIdx.x + u * NT;
+      e = e < BB / 16 ? e : BB / 16 - 1;
+      w[u] = *reinterpret_cast<const u32x4*>(reinterpret_cast<const unsigned char*>(Bt) + 16 * e);
+    }
+#pragma unroll
+    for (int u = 0; u < BPT; ++u) {
+      int e = threadIdx.x + u * NT;
+      e = e < BB / 16 ? e : BB / 16 - 1;
+      *reinterpret_cast<u32x4*>(smem + 16 * e) = w[u];
+    }
+  }
+  // patch: 16-B fp32 channel quad -> three 8-B bf16 quads (pieces at 32 p + 8 q of the pixel)
+  {
+    const auto rsA = __builtin_amdgcn_make_buffer_rsrc((void*)in, 0, (int)in_bytes, 0x00020000);
+    constexpr int SB = 4;  // items in flight per thread
+#pragma unroll
+    for (int u0 = 0; u0 < PPT; u0 += SB) {
+      f32x4 v[SB];
+      int dst[SB];
+#pragma unroll
+      for (int d = 0; d < SB; ++d) {
+        int e = threadIdx.x + (u0 + d) * NT;
+        e = e < ITEMS ? e : ITEMS - 1;
+        const int pr = e >> 2, q = e & 3, py = pr / PW2, px = pr - py * PW2;
+        const int iy = y0 - 1 + py, ix = x0 - 1 + px;
+        const bool ok = (unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W;
+        const unsigned vo = ok ? (unsigned)((((b * g.H + iy) * g.W + ix) * 16 + 4 * q) * 4) : OOB_OFF;
+        v[d] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsA, vo, 0, 0));
+        dst[d] = pr * PB + 8 * q;
+      }
+#pragma unroll
+      for (int d = 0; d < SB; ++d) {
+        unsigned short sp[3][4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) split3(v[d][c], sp[0][c], sp[1][c], sp[2][c]);
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+          uint2 w;
+          w.x = (unsigned)sp[p][0] | ((unsigned)sp[p][1] << 16);
+          w.y = (unsigned)sp[p][2] | ((unsigned)sp[p][3] << 16);
+          *reinterpret_cast<uint2*>(patch + dst[d] + 32 * p) = w;
+        }
+      }
+    }
+  }
+
+  const int fr = lane & 15, fq = lane >> 4, th = fq >> 1;  // th: this lane's tap within a step pair
+  int prow[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    int r = (wm * TM + i) * 16 + fr;
+    r = r < T ? r : T - 1;
+    int ly, lx;
+    if constexpr (POOL) {
+      const int w = r >> 2, q = r & 3;
+      ly = 2 * (w / (TW / 2)) + (q >> 1);
+      lx = 2 * (w % (TW / 2)) + (q & 1);
+    } else {
+      ly = r / TW;
+      lx = r % TW;
+    }
+    prow[i] = ((ly + 1) * PW2 + lx + 1) * PB + 16 * (fq & 1);
+  }
+
+  f32x4 acc[TM][2];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  __syncthreads();
+
+  auto toff = [&](int s) {  // this lane's tap offset (bytes) in step s
+    const int ta = 2 * s, tb = 2 * s + 1 < 9 ? 2 * s + 1 : 8;  // (tap 9: zero weights)
+    const int oa = ((ta / 3 - 1) * PW2 + (ta % 3 - 1)) * PB, ob = ((tb / 3 - 1) * PW2 + (tb % 3 - 1)) * PB;
+    return th ? ob : oa;
+  };
+  auto frag = [&](int i, int off, bf16x8 (&a)[3]) {
+    int pr = prow[i];
+    asm volatile("" : "+v"(pr));
+    const unsigned char* q = patch + pr + off;
+#pragma unroll
+    for (int p = 0; p < 3; ++p) a[p] = *reinterpret_cast<const bf16x8*>(q + 32 * p);
+  };
+  auto bfrag = [&](int s, bf16x8 (&bb)[3][2]) {
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        bb[p][j] = *reinterpret_cast<const bf16x8*>(smem + (j * NS * 3 + s * 3 + p) * 1024 + lane * 16);
+  };
+  bf16x8 af[2][3], bq[2][3][2];
+  frag(0, toff(0), af[0]);
+  bfrag(0, bq[0]);
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    const int off = toff(s), off_next = toff(s + 1 < NS ? s + 1 : s);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int cur = (s * TM + i) & 1, nxt = cur ^ 1;
+      if (i + 1 < TM)
+        frag(i + 1, off, af[nxt]);
+      else if (s + 1 < NS)
+        frag(0, off_next, af[nxt]);
+      if (i == 0 && s + 1 < NS) bfrag(s + 1, bq[(s + 1) & 1]);  // next step's weights
+      const bf16x8(&bb)[3][2] = bq[s & 1];
+#pragma unroll
+      for (int jb = 0; jb < 2; ++jb) {
+        f32x4 c = mfma16_bf16(af[cur][2], bb[0][jb], f32x4{0.f, 0.f, 0.f, 0.f});
+        c = mfma16_bf16(af[cur][1], bb[1][jb], c);
+        c = mfma16_bf16(af[cur][0], bb[2][jb], c);
+        c = mfma16_bf16(af[cur][1], bb[0][jb], c);
+        c = mfma16_bf16(af[cur][0], bb[1][jb], c);
+        const f32x4 m = mfma16_bf16(af[cur][0], bb[0][jb], acc[i][jb]);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[i][jb][r] = m[r] + c[r];
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+
+  // epilogue (as conv3x3_x3_tile_kernel)
+  int* orow = reinterpret_cast<int*>(smem);
+  __syncthreads();
+  constexpr int NO = POOL ? T / 4 : T;
+  const int Wp = g.W + 2;
+  for (int r = threadIdx.x; r < NO; r += NT) {
+    int o;
+    if constexpr (POOL) {
+      const int py = (y0 >> 1) + r / (TW / 2), px = (x0 >> 1) + r % (TW / 2);
+      o = (py >= g.PH || px >= g.PW) ? -1
+          : g.out_mode == 1         ? (b * (g.PH + 2) + py + 1) * (g.PW + 2) + px + 1
+                                    : (b * g.PH + py) * g.PW + px;
+    } else {
+      const int oy = y0 + r / TW, ox = x0 + r % TW;
+      o = (oy >= g.H || ox >= g.W) ? -1 : g.out_mode == 1 ? (b * (g.H + 2) + oy + 1) * Wp + ox + 1 : (b * g.H + oy) * g.W + ox;
+    }
+    orow[r] = o;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int jb = 0; jb < 2; ++jb) {
+    const int n = 16 * jb + fr;
+    const float pb = (epi.flags & EPI_BIAS) ? epi.bias[n] : 0.f;
+    const float pm = (epi.flags & (EPI_BN | EPI_BN_AB)) ? epi.mean[n] : 0.f;
+    const float ps = (epi.flags & (EPI_BN | EPI_BN_AB)) ? epi.sq[n] : 1.f;
+    const float pg = (epi.flags & EPI_BN) ? epi.gamma[n] : 1.f;
+    auto put = [&](int o, float v) {
+      if (g.out_mode == 1) {
+        unsigned short s0, s1, s2;
+        split3(v, s0, s1, s2);
+        bf16_bits* d = out_split + (size_t)o * 96 + n;
+        d[0] = s0;
+        d[32] = s1;
+        d[64] = s2;
+      } else {
+        out[(size_t)o * N + n] = v;
+      }
+    };
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int rb = 16 * (wm * TM + i);
+      if constexpr (POOL) {
+        const int w = rb / 4 + fq;
+        const int o = w < NO ? orow[w] : -1;
+        if (o >= 0) put(o, pool_then_epilogue(acc[i][jb], pb, pm, ps, pg, epi.flags));
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = rb + 4 * fq + r;
+          const int o = row < NO ? orow[row] : -1;
+          if (o >= 0) put(o, apply_epilogue(acc[i][jb][r], pb, pm, ps, pg, epi.flags));
+        }
+      }
+    }
+  }
+}
+
 }  // namespace dnnhip

@@ -281,7 +281,31 @@ __global__ void pack_weights_x3_kernel(const float* __restrict__ w, bf16_bits* _
   }
 }
 
+// C = 16 (conv3x3_x3_c16_kernel): [n/16][step 0..4][piece][lane][8], k = 8 (lane >> 4) + e of
+// step s = tap 2 s + (k >> 4), channel k & 15 (tap 9: zero)
+__global__ void pack_weights_x3c16_kernel(const float* __restrict__ w, bf16_bits* __restrict__ out, int N, int Npad) {
+  const long long total = (long long)(Npad / 16) * 5 * 3 * 512;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int e = (int)(i & 7), lane = (int)((i >> 3) & 63);
+    const long long q = i >> 9;
+    const int p = (int)(q % 3);
+    const long long r = q / 3;
+    const int s = (int)(r % 5), nb = (int)(r / 5);
+    const int n = nb * 16 + (lane & 15), k = 8 * (lane >> 4) + e, tap = 2 * s + (k >> 4), c = k & 15;
+    const float v = n < N && tap < 9 ? w[((size_t)tap * 16 + c) * N + n] : 0.f;
+    unsigned short s0, s1, s2;
+    split3(v, s0, s1, s2);
+    out[i] = p == 0 ? s0 : p == 1 ? s1 : s2;
+  }
+}
+
 int launch_pack_weights_x3(const float* w, bf16_bits* out, int K, int N, int Npad, int C, hipStream_t s) {
+  if (C == 16 && K == 144 && Npad % 32 == 0 && Npad >= N) {
+    const long long total = (long long)(Npad / 16) * 5 * 3 * 512;
+    hipLaunchKernelGGL(pack_weights_x3c16_kernel, dim3(grid_x3(total)), dim3(256), 0, s, w, out, N, Npad);
+    return check_x3("pack_weights_x3 (c16)");
+  }
   if (K != 9 * C || C % 32 != 0 || Npad % 64 != 0 || Npad < N) {
     set_error("pack_weights_x3: unsupported K=%d N=%d Npad=%d C=%d", K, N, Npad, C);
     return -2;
@@ -329,9 +353,10 @@ static long long x3_span(long long M, int H, int W, bool pool = false) {
 constexpr int X3T_TM = 7;  // row blocks of 16 per wave
 
 // which kernel runs an x3 layer: 0 the row-run kernel (N % 256 == 0), 1 tile kernel N = 64 from
-// one 32-channel chunk (4 waves, two workgroups per CU), 2 tile kernel N % 128 == 0 (8 waves,
-// double-buffered chunks); -1 none (the layer stays on the fp32 MFMA)
+// one 32-channel chunk, 2 tile kernel N % 128 == 0 (double-buffered chunks), 3 the 16-channel
+// kernel (fp32 input, split while staged); -1 none (the layer stays on the fp32 MFMA)
 static int x3_kind(int N, int C) {
+  if (C == 16) return N == 32 && !getenv_flag_off("DNN_HIP_X3_C16") ? 3 : -1;
   if (N % 256 == 0) return 0;
   if (N == 64 && C == 32) return 1;
   if (N % 128 == 0) return 2;
@@ -339,11 +364,11 @@ static int x3_kind(int N, int C) {
 }
 
 bool conv_x3_supported(int C, int OC, int H, int W, int OH, int OW, int kh, int kw, int sh, int sw, int pt, int pl) {
-  if (!(kh == 3 && kw == 3 && sh == 1 && sw == 1 && pt == 1 && pl == 1 && OH == H && OW == W && C % 32 == 0 &&
-        x3_enabled()))
+  if (!(kh == 3 && kw == 3 && sh == 1 && sw == 1 && pt == 1 && pl == 1 && OH == H && OW == W &&
+        (C % 32 == 0 || C == 16) && x3_enabled()))
     return false;
   const int kind = x3_kind(OC, C);
-  if (kind < 0 || (kind > 0 && getenv_flag_off("DNN_HIP_X3_TILE"))) return false;
+  if (kind < 0 || ((kind == 1 || kind == 2) && getenv_flag_off("DNN_HIP_X3_TILE"))) return false;
   // a tile must fit the patch for any batch: spans grow with M only until a tile crosses whole
   // images, so two images' worth of rows decides it (tile kernel: fixed patch)
   return kind > 0 || x3_span(2LL * H * W + X3_BM, H, W) <= X3_NPR;
@@ -359,6 +384,7 @@ bool conv_x3_pool_supported(int OC, int C, int H, int W) {
 
 long long x3_tiles(long long batch, int OH, int OW, int OC, int C, int K) {
   const int kind = x3_kind(OC, C);
+  if (kind == 3) return batch * ((OH + 15) / 16) * ((OW + 25) / 26);
   if (kind > 0)
     return batch * ((OH + (kind == 1 ? 7 : 3)) / (kind == 1 ? 8 : 4)) * ((OW + 25) / 26) * (OC / (kind == 1 ? 64 : 128));
   return (batch * OH * OW + X3_BM - 1) / X3_BM * (OC / 256) * x3_splits(OC, K);
@@ -382,6 +408,31 @@ int launch_conv_x3(const bf16_bits* in_split, const bf16_bits* Bt, float* out, b
   const long long in_bytes = (long long)x3_act_bytes(nimg, H, W, C);
   const long long b_bytes = (long long)(Npad / 16) * (K / 32) * 3072;
   const int kind = x3_kind(N, C);
+  if (kind == 3) {  // fp32 NHWC input (in_split is the producer's float buffer)
+    const long long in32 = nimg * H * W * 64LL, b16 = (long long)(Npad / 16) * 5 * 3072;
+    if (M % per_img != 0 || K != 144 || Npad != N || splits != 1 || (pool && (H % 2 || W % 2)) ||
+        in32 >= 0x80000000LL || b16 >= 0x80000000LL || (out_split == nullptr) == (out == nullptr) ||
+        x3_act_bytes(nimg, pool ? PH : H, pool ? PW : W, N) >= 0x80000000ULL) {
+      set_error("conv_x3 (c16): unsupported shape M=%lld N=%d K=%d %dx%dx%d", M, N, K, H, W, C);
+      return -2;
+    }
+    const int tilesX = (W + 25) / 26, tilesY = (H + 15) / 16;
+    const long long blocks = nimg * tilesX * tilesY;
+    if (blocks > 0x7fffffffLL || N != 32) {
+      set_error("conv_x3 (c16): N=%d (32 only) or grid too large", N);
+      return -2;
+    }
+    const X3Geom xg{H, W, C, out_split ? 1 : 0, 1, PH, PW};
+    const float* in32p = reinterpret_cast<const float*>(in_split);
+    (void)b16;
+    if (pool)
+      hipLaunchKernelGGL((conv3x3_x3_c16_kernel<16, 26, 4, 7, true>), dim3((unsigned)blocks), dim3(256), 0, stream, in32p,
+                         Bt, out, out_split, N, epi, tilesX, tilesY, xg, (unsigned)in32);
+    else
+      hipLaunchKernelGGL((conv3x3_x3_c16_kernel<16, 26, 4, 7, false>), dim3((unsigned)blocks), dim3(256), 0, stream,
+                         in32p, Bt, out, out_split, N, epi, tilesX, tilesY, xg, (unsigned)in32);
+    return check_x3("conv_x3 (c16)");
+  }
   if (kind > 0) {
     if (M % per_img != 0 || K != 9 * C || Npad != N || splits != 1 || (pool && (H % 2 || W % 2)) ||
         in_bytes >= 0x80000000LL || b_bytes >= 0x80000000LL || (out_split == nullptr) == (out == nullptr) ||

@@ -299,8 +299,8 @@ static void set_cfg(dnn_plan* p, PlanLayer& L) {
   const long long M = (long long)p->batch * L.OH * L.OW;
   if (!p->fp16 && L.mode == MODE_X3) {  // one config per width (kernels_x3.hip); split-K by (N, K) only
     L.cfg = 0;
-    L.Kpad = L.K;
-    L.Npad = L.OC;  // (a multiple of 256, or of 64 for the tile kernel)
+    L.Kpad = L.C == 16 ? 160 : L.K;  // (16 channels: 5 steps of two taps)
+    L.Npad = L.OC;  // (a multiple of 256, or of 32 / 64 / 128 for the tile kernels)
     L.splits = x3_splits(L.OC, L.K);
     return;
   }
@@ -433,7 +433,9 @@ int dnn_plan_add_conv(dnn_plan* p, int kh, int kw, int od, int stride_h, int str
     // implicit GEMM without split-K (its epilogue splits, EPI_OUT_X3) or the pool-fused patch
     // conv (conv1)
     PlanLayer& prev = p->layers.back();
-    if ((prev.type == 1 && prev.C % 32 == 0) || (prev.type == 0 && prev.mode == MODE_X3) ||
+    if (L.C == 16) {  // the 16-channel x3 kernel reads the producer's fp32 output (conv1)
+      L.mode = MODE_X3;
+    } else if ((prev.type == 1 && prev.C % 32 == 0) || (prev.type == 0 && prev.mode == MODE_X3) ||
         (prev.type == 0 && prev.mode == MODE_IMPLICIT && prev.pool && prev.splits == 1) ||
         (prev.type == 0 && prev.mode == MODE_PATCH && prev.pool)) {
       L.mode = MODE_X3;

@@ -179,18 +179,19 @@ def test_plan_shape_memory_and_flops_host_only(monkeypatch, fuse, splitk):
 
 
 def test_plan_x3_structure_host_only(monkeypatch):
-    """Default fp32 batch plan: conv2-conv7 on the x3 conv (exact 3-way bf16 splits; conv2 and
-    conv3 on the 2-D tile kernel, N = 64 / 128), conv2-conv4 with their 2x2 pools fused, conv1's
-    pooled patch-conv epilogue and pool5 writing split planes; conv5 (N = 512) in 2 K slices
-    whose partials pool5 combines; weights of those layers in 3 bf16 pieces."""
+    """Default fp32 batch plan: conv1-conv7 on the x3 conv (exact 3-way bf16 splits; conv1 on the
+    16-channel kernel reading conv0's fp32 output, conv2 and conv3 on the 2-D tile kernel, N = 64 /
+    128), conv1-conv4 with their 2x2 pools fused, pool5 writing split planes; conv5 (N = 512) in
+    2 K slices whose partials pool5 combines; weights of those layers in 3 bf16 pieces."""
     monkeypatch.delenv("DNN_HIP_X3", raising=False)
     monkeypatch.delenv("DNN_HIP_X3_TILE", raising=False)
+    monkeypatch.delenv("DNN_HIP_X3_C16", raising=False)
     ws = synth.yolo_weights()
     g, _ = yolo_graph.build_graph(dnn_hip.DnnGraphBuilder, ws, in_shape=(64, 416, 416, 3))
     entries = dnn_hip.lower_graph(g)
     wb, sb = dnn_hip.Plan.memory(64, (416, 416, 3), entries)
     nparams = sum(w["kernel"].size for w in ws)
-    x3params = 9 * (32 * 64 + 64 * 128 + 128 * 256 + 256 * 512 + 512 * 1024 + 1024 * 1024)
+    x3params = 9 * (16 * 32 + 32 * 64 + 64 * 128 + 128 * 256 + 256 * 512 + 512 * 1024 + 1024 * 1024)
     assert wb >= 4 * nparams + 2 * x3params and wb < (4 * nparams + 2 * x3params) * 1.2
     act2 = 2 * 64 * 208 * 208 * 16 * 4
     # one zero-bordered split-plane region per producer: conv1 (pooled 104x104x32), conv2
@@ -201,17 +202,21 @@ def test_plan_x3_structure_host_only(monkeypatch):
     assert act2 + pad + slab <= sb < act2 + pad + slab + 16384
     lines = _describe_yolo(64, False)
     conv = [ln for ln in lines if ln.startswith("conv")]
-    assert [i for i, ln in enumerate(conv) if "patch_x3" in ln] == [2, 3, 4, 5, 6, 7]
-    assert "mode=patch" in conv[1] and "+pool2x2s2" in conv[1]
+    assert [i for i, ln in enumerate(conv) if "patch_x3" in ln] == [1, 2, 3, 4, 5, 6, 7]
     assert "splitK=2 x3-combine" in conv[5] and sum("splitK" in ln for ln in lines) == 1
-    assert all("+pool2x2s2" in conv[i] for i in (2, 3, 4))  # pools fused into the x3 convs
+    assert all("+pool2x2s2" in conv[i] for i in (1, 2, 3, 4))  # pools fused into the x3 convs
     assert sum(ln.startswith("pool") for ln in lines) == 1  # pool5 (s1, combines conv5's slices)
     # latency plans keep the fp32 MFMA (split-K over the idle chip)
     assert not any("patch_x3" in ln for ln in _describe_yolo(1, True))
-    # DNN_HIP_X3_TILE=0: conv2/conv3 back on the fp32 MFMA, conv3's pooled epilogue splits
+    # DNN_HIP_X3_TILE=0: conv2/conv3 back on the fp32 MFMA, conv3's pooled epilogue splits;
+    # DNN_HIP_X3_C16=0: conv1 on the fp32 patch kernel (its pooled epilogue splits for conv2)
     monkeypatch.setenv("DNN_HIP_X3_TILE", "0")
     conv = [ln for ln in _describe_yolo(64, False) if ln.startswith("conv")]
-    assert [i for i, ln in enumerate(conv) if "patch_x3" in ln] == [4, 5, 6, 7]
+    assert [i for i, ln in enumerate(conv) if "patch_x3" in ln] == [1, 4, 5, 6, 7]
+    monkeypatch.setenv("DNN_HIP_X3_TILE", "1")
+    monkeypatch.setenv("DNN_HIP_X3_C16", "0")
+    conv = [ln for ln in _describe_yolo(64, False) if ln.startswith("conv")]
+    assert [i for i, ln in enumerate(conv) if "patch_x3" in ln] == [2, 3, 4, 5, 6, 7] and "mode=patch " in conv[1] + " "
 
 
 def test_plan_errors_are_reported():
@@ -327,9 +332,9 @@ def test_latency_plan_layout():
     for i in (4, 5, 6, 7, 8):
         assert " splitK=" in conv[i] and " combine" in conv[i], conv[i]
     assert "+pool2x2s2" in conv[4]
-    # the batch plan at batch 1: conv2-conv7 on the x3 conv, conv5 in the (N, K) rule's 2 K slices
+    # the batch plan at batch 1: conv1-conv7 on the x3 conv, conv5 in the (N, K) rule's 2 K slices
     assert [l for l in base if " splitK=" in l] == [l for l in base if " splitK=2 x3-combine" in l] and \
-        sum(" splitK=2 " in l for l in base) == 1 and sum("patch_x3" in l for l in base) == 6
+        sum(" splitK=2 " in l for l in base) == 1 and sum("patch_x3" in l for l in base) == 7
     assert sum(" splitK=16 " in l for l in conv) == 2  # conv6/conv7 at batch 1: 48 tiles x 16
     # batch 64: latency mode leaves the (N, K)-only rule in charge of every layer that fills the chip
     assert [l.replace(" latency", "") for l in _describe_yolo(64, True)] == _describe_yolo(64, False)

@@ -1251,12 +1251,15 @@ X3_TILE_CASES = [
     (3, 104, 104, "pool"),  # conv2/conv3-like frames: 52 / 26 wide, whole 8 x 26 / 4 x 26 tiles
     (2, 60, 60, "pool"),    # 30 wide: one partial tile per row band; 15x15 after: separate pool
     (2, 27, 61, "raster"),
+    (2, 104, 104, "c16"),      # conv1-like: 16-channel x3 conv (fp32 input split while staged) + pool
+    (2, 37, 45, "c16raster"),  # ... without a pool: raster rows, ragged tiles
 ]
 
 
 @pytest.mark.parametrize("case", X3_TILE_CASES)
 def test_x3_tile_kernel_vs_oracle(monkeypatch, case):
-    """conv3x3_x3_tile_kernel (N = 64 / 128 on 2-D 8 x 26 / 4 x 26 output tiles) and the patch conv's
+    """conv3x3_x3_tile_kernel (N = 64 / 128 on 2-D 8 x 26 / 4 x 26 output tiles),
+    conv3x3_x3_c16_kernel (16 input channels, two taps per 32-wide K step) and the patch conv's
     split-plane epilogue: modes as planned, the chain within the fp32 tolerance of the float64
     oracle and within 1.25x of the fp32-MFMA plan's error (DNN_HIP_X3=0), negative-gamma
     channels, batch rows bit-equal to batch-1 runs, repeat runs identical."""
@@ -1274,6 +1277,12 @@ def test_x3_tile_kernel_vs_oracle(monkeypatch, case):
     if form == "pool":
         x = rng.standard_normal((B, H, W, 16)).astype(np.float32)
         layers = [(layer(16, 32), True), (layer(32, 64), True), (layer(64, 128), True), (layer(128, 256), False)]
+    elif form == "c16":
+        x = rng.standard_normal((B, H, W, 16)).astype(np.float32)
+        layers = [(layer(16, 32), True), (layer(32, 64), True), (layer(64, 128), False)]
+    elif form == "c16raster":
+        x = rng.standard_normal((B, H, W, 16)).astype(np.float32)
+        layers = [(layer(16, 32), False), (layer(32, 64), False)]
     else:
         x = rng.standard_normal((B, H, W, 32)).astype(np.float32)
         layers = [(layer(32, 64), False), (layer(64, 128), False)]
@@ -1281,7 +1290,7 @@ def test_x3_tile_kernel_vs_oracle(monkeypatch, case):
     def graph(shape):
         g = dnn_hip.DnnGraphBuilder()
         y = g.create_input(list(shape))
-        if form == "raster":
+        if form != "pool":  # (a producer before the first conv: conv1 is never a plan's first layer)
             y = g.create_max_pool2d(y, [1, 2, 2, 1], [1, 1, 1, 1], "SAME")
         for (k, b, n), pool in layers:
             y = g.create_conv2d(y, k, [1, 1, 1, 1], "SAME")
@@ -1293,7 +1302,7 @@ def test_x3_tile_kernel_vs_oracle(monkeypatch, case):
         g.set_out_node(y)
         return g
 
-    ref = R.max_pool2d(x, [1, 2, 2, 1], [1, 1, 1, 1], "SAME") if form == "raster" else x
+    ref = R.max_pool2d(x, [1, 2, 2, 1], [1, 1, 1, 1], "SAME") if form != "pool" else x
     for (k, b, n), pool in layers:
         ref = R.leaky_relu(R.batch_norm(R.bias_add(R.conv2d(ref, k), b), *n, 1e-5))
         if pool:
@@ -1310,6 +1319,8 @@ def test_x3_tile_kernel_vs_oracle(monkeypatch, case):
                 assert "+pool2x2s2" in conv[1] and ("+pool2x2s2" in conv[2]) == (H % 8 == 0), conv
             else:
                 assert all("mode=patch_x3" in c for c in conv), conv
+                if form == "c16":
+                    assert "+pool2x2s2" in conv[0] and "+pool2x2s2" in conv[1], conv
         y = eng.run(x)
         errs[x3] = R.normwise_err(y, ref)
         print("x3=%s tile chain normwise err %.3e" % (x3, errs[x3]))

@@ -20,7 +20,7 @@ from collections import defaultdict
 # kernel order of one YOLOv2-tiny forward in the default (fused) plan: conv5-7's split-K
 # partials are combined inside their GEMMs (DNN_HIP_SPLITK_FUSED=0 / --reduce: a separate
 # convN.reduce kernel after each)
-ORDER = ["conv0.direct", "conv1.patch", "conv2.gemm", "conv3.gemm", "conv4.gemm", "conv5.gemm", "pool5",
+ORDER = ["conv0.direct", "conv1.gemm", "conv2.gemm", "conv3.gemm", "conv4.gemm", "conv5.gemm", "pool5",
          "conv6.gemm", "conv7.gemm", "conv8.gemm"]
 # (the same kernel list with DNN_HIP_X3=0: conv5-7 split-K combined in the GEMM)
 # ... the fp16 plan (dnn_plan_set_precision 1): conv1 patch kernel, f16->f32 output conversion

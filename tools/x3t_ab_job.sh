@@ -8,5 +8,5 @@ done
 F="--steps 30 --warmup 5 --no-cpu --no-latency --no-fp16 --no-unfused --no-e2e --kernels"
 for a in $ARMS ${ARMS%% *}; do
 env $a timeout -k 10 120 python bench.py $F > $O/b.log 2>&1 || { tail -5 $O/b.log; exit 1; }
-tail -1 $O/b.log | python -c "import json,sys;d=json.loads(sys.stdin.read());k=d['kernels'];print('$a', d['value'], {n:v['ms'] for n,v in k.items() if n in ('conv1.patch','conv2.gemm','conv3.gemm')})"
+tail -1 $O/b.log | python -c "import json,sys;d=json.loads(sys.stdin.read());k=d['kernels'];print('$a', d['value'], {n:v['ms'] for n,v in k.items() if n in ('conv1.patch','conv1.gemm','conv2.gemm','conv3.gemm')})"
 done
