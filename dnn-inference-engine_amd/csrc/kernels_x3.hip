@@ -478,14 +478,28 @@ int launch_conv_x3(const bf16_bits* in_split, const bf16_bits* Bt, float* out, b
   const int tilesM = (int)((M + X3_BM - 1) / X3_BM), tilesN = N / 256;
   // splits > 1: `out` receives the raw partials [splits][M][N] (x3_combine_kernel finishes)
   const X3Geom xg{H, W, C, splits > 1 ? 2 : out_split ? 1 : 0, splits, PH, PW};
-  if (pool)
-    hipLaunchKernelGGL((conv3x3_x3_patch_kernel<X3_BM, X3_NPR_POOL, true>), dim3(tilesM * tilesN), dim3(512), 0, stream,
-                       in_split, Bt, out, out_split, (int)M, N, K, epi, tilesM, xg, (unsigned)in_bytes,
-                       (unsigned)b_bytes);
-  else
-    hipLaunchKernelGGL((conv3x3_x3_patch_kernel<X3_BM, X3_NPR>), dim3(tilesM * tilesN * splits), dim3(512), 0, stream,
-                       in_split, Bt, out, out_split, (int)M, N, K, epi, tilesM, xg, (unsigned)in_bytes,
-                       (unsigned)b_bytes);
+  static const int var = [] {
+    const char* e = getenv("DNN_HIP_X3V");
+    const int v = e ? atoi(e) : 1;
+    return v >= 0 && v <= 2 ? v : 1;
+  }();
+#define X3P(NPR_, POOL_, V_)                                                                                  \
+  hipLaunchKernelGGL((conv3x3_x3_patch_kernel<X3_BM, NPR_, POOL_, V_>), dim3(tilesM * tilesN * (POOL_ ? 1 : splits)), \
+                     dim3(512), 0, stream, in_split, Bt, out, out_split, (int)M, N, K, epi, tilesM, xg,           \
+                     (unsigned)in_bytes, (unsigned)b_bytes)
+#define X3PV(NPR_, POOL_)                 \
+  switch (var) {                          \
+    case 0: X3P(NPR_, POOL_, 0); break;   \
+    case 2: X3P(NPR_, POOL_, 2); break;   \
+    default: X3P(NPR_, POOL_, 1); break;  \
+  }
+  if (pool) {
+    X3PV(X3_NPR_POOL, true);
+  } else {
+    X3PV(X3_NPR, false);
+  }
+#undef X3PV
+#undef X3P
   return check_x3("conv_x3");
 }
 

@@ -1,0 +1,18 @@
+"""Write the YOLOv2-tiny output (batch argv[2], default 16) of the default fp32 plan to argv[1]
+(.npy): the x3 variant A/B (tools/x3v_job.sh, tests/test_gpu_parity.py) checks every
+DNN_HIP_X3V arm bit for bit against arm 0."""
+import os
+import sys
+
+R = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(R, "dnn-inference-engine_amd"))
+import numpy as np  # noqa: E402
+
+import dnn_hip  # noqa: E402
+import synth  # noqa: E402
+import yolo_graph  # noqa: E402
+
+B = int(sys.argv[2]) if len(sys.argv) > 2 else 16
+g, _ = yolo_graph.build_graph(dnn_hip.DnnGraphBuilder, synth.yolo_weights(), in_shape=(B, 416, 416, 3))
+eng = dnn_hip.DnnInferenceEngine(g, False, device=0)
+np.save(sys.argv[1], eng.run(synth.frames(list(range(B)))))
