@@ -477,7 +477,11 @@ int launch_conv_x3(const bf16_bits* in_split, const bf16_bits* Bt, float* out, b
   }
   const int tilesM = (int)((M + X3_BM - 1) / X3_BM), tilesN = N / 256;
   // splits > 1: `out` receives the raw partials [splits][M][N] (x3_combine_kernel finishes)
-  const X3Geom xg{H, W, C, splits > 1 ? 2 : out_split ? 1 : 0, splits, PH, PW};
+  static const int prio = [] {
+    const char* e = getenv("DNN_HIP_X3PRIO");
+    return e && e[0] == '1' ? 1 : 0;
+  }();
+  const X3Geom xg{H, W, C, splits > 1 ? 2 : out_split ? 1 : 0, splits, PH, PW, prio};
   static const int var = [] {
     const char* e = getenv("DNN_HIP_X3V");
     const int v = e ? atoi(e) : 1;
