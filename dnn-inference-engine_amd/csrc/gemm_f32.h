@@ -53,10 +53,22 @@ __device__ __forceinline__ float div_rn(float x, float d) {
 typedef unsigned short bf16_bits;
 __device__ __forceinline__ unsigned short bf16_rn(float x) { return __builtin_bit_cast(unsigned short, (__bf16)x); }
 __device__ __forceinline__ float bf16_f(unsigned short h) { return __builtin_bit_cast(float, (unsigned)h << 16); }
-// x = bf16_f(s0) + bf16_f(s1) + bf16_f(s2) exactly (finite x, |x| >= 2^-100)
+// x = bf16_f(s0) + bf16_f(s1) + bf16_f(s2) exactly for every finite x with |x| >= 2^-100 (below
+// that the pieces' exponents leave the normal range and the tail is partly lost: <= 2^-124
+// absolute).  Total over finite fp32: a finite |x| above the largest bf16 (0x1.fep127, where
+// round-to-nearest would give inf and x - inf a NaN) takes the TRUNCATED top piece instead, and
+// the remainder (< 2^-7 |x|, 16 bits) is still split exactly by the two lower pieces, so every
+// finite operand the reference's cblas_sgemm takes (dnn_openblas.c:184-192) is represented
+// exactly.  +-inf and NaN keep their bf16 value in the top piece with zero lower pieces (no
+// NaN from inf - inf here); their products still meet the other operand's lower pieces, which
+// are 0 for any weight exact in bf16, so a non-finite operand yields NaN where fp32 would give
+// +-inf: outside the finite domain the x3 path claims.
 __device__ __forceinline__ void split3(float x, unsigned short& s0, unsigned short& s1, unsigned short& s2) {
-  s0 = bf16_rn(x);
-  const float r1 = x - bf16_f(s0);
+  const unsigned short r = bf16_rn(x);
+  const bool fin = __builtin_isfinite(x);
+  const bool ovf = fin && (r & 0x7fffu) == 0x7f80u;  // finite, rounded to +-inf
+  s0 = ovf ? (unsigned short)(__builtin_bit_cast(unsigned, x) >> 16) : r;
+  const float r1 = fin ? x - bf16_f(s0) : 0.f;
   s1 = bf16_rn(r1);
   s2 = bf16_rn(r1 - bf16_f(s1));
 }

@@ -3,6 +3,7 @@
 // max pool that feeds it) and its weight packing.
 #include "dnn_common.h"
 #include "gemm_x3_patch.h"
+#include "gemm_x3_w1.h"
 
 #include <cfloat>
 #include <cstdlib>
@@ -325,6 +326,7 @@ static bool x3_enabled() {
 }
 
 constexpr int X3_NPR_POOL = 352;  // pool-window-major tiles span more rows (26x26: 350)
+constexpr int X3_NPR_POOL_W1 = 384;  // the one-wave kernel's DMA wants a multiple of 64 rows
 
 // rows of the padded input one BM-row tile spans (tap offsets included); pool: window-major
 static long long x3_span(long long M, int H, int W, bool pool = false) {
@@ -485,8 +487,24 @@ int launch_conv_x3(const bf16_bits* in_split, const bf16_bits* Bt, float* out, b
   static const int var = [] {
     const char* e = getenv("DNN_HIP_X3V");
     const int v = e ? atoi(e) : 1;
-    return v >= 0 && v <= 2 ? v : 1;
+    return v >= 0 && v <= 4 ? v : 1;
   }();
+  if (var >= 3) {  // one wave per SIMD, accumulators over all of K (gemm_x3_w1.h); 4: swizzled rows
+#define X3W(NPR_, POOL_, SWZ_)                                                                           \
+  hipLaunchKernelGGL((conv3x3_x3_w1_kernel<X3_BM, NPR_, POOL_, SWZ_>), dim3(tilesM * tilesN * (POOL_ ? 1 : splits)), \
+                     dim3(256), 0, stream, in_split, Bt, out, out_split, (int)M, N, K, epi, tilesM, xg,          \
+                     (unsigned)in_bytes, (unsigned)b_bytes)
+    if (pool && var == 4)
+      X3W(X3_NPR_POOL_W1, true, true);
+    else if (pool)
+      X3W(X3_NPR_POOL_W1, true, false);
+    else if (var == 4)
+      X3W(X3_NPR, false, true);
+    else
+      X3W(X3_NPR, false, false);
+#undef X3W
+    return check_x3("conv_x3 (w1)");
+  }
 #define X3P(NPR_, POOL_, V_)                                                                                  \
   hipLaunchKernelGGL((conv3x3_x3_patch_kernel<X3_BM, NPR_, POOL_, V_>), dim3(tilesM * tilesN * (POOL_ ? 1 : splits)), \
                      dim3(512), 0, stream, in_split, Bt, out, out_split, (int)M, N, K, epi, tilesM, xg,           \

@@ -6,9 +6,10 @@ exchange between layers.  The only collectives are the ones the north star names
   * one broadcast of the packed weight buffer from rank 0 at start-up (63.5 MB fp32);
   * per batch, a gather to rank 0 of either the raw outputs ([n,13,13,125] fp32 per rank,
     gather_outputs) or — after the on-GPU postprocessing (yolo_post.py) — the packed
-    detections (DetectionGather: sizes all-gathered then max-over-ranks valid rows, with
-    three steps in flight so the host wait is on a step whose successors are queued; or a
-    fixed-capacity buffer sent without any host synchronisation).
+    detections (DetectionGather: sizes all-gathered, then max-over-ranks valid rows; the
+    "deferred" mode reads the sizes on the host one step after their all-gather, so no
+    host ever waits on the step it is finishing; or a fixed-capacity buffer sent without
+    any host synchronisation).
 One process per GPU, torch.distributed over RCCL ("nccl" backend) on the GPU box, gloo
 for the CPU tests; the compute step is injected, so the same runner drives the HIP plan
 (bench.py) and a CPU stand-in (tests/test_dist_cpu.py).
@@ -114,6 +115,14 @@ class DetectionGather(object):
               host read waits for that step on all ranks, so the caller keeps steps in
               flight (ShardedRunner: three) and the wait is on a step whose successors are
               already queued on the GPU;
+      "deferred"  as "sized", split in two: launch_meta() enqueues the meta all-gather and an
+              asynchronous copy of it into pinned host memory; launch_payload(), called one
+              step later, reads the sizes there (the copy has long completed unless some rank
+              is more than a step behind) and enqueues the payload gather.  Every rank's host
+              touches a step's sizes only after it has enqueued the next step's meta, so the
+              cross-rank rendezvous of "sized" (each host waiting for that step on all ranks)
+              moves one step further behind the GPU queue; the caller keeps one more output
+              slot than steps in flight (ShardedRunner.inflight);
       "fixed"  meta is gathered to `dst` and the payload is the whole packed buffer (its
               capacity is the most detections `cap` images can have, 845 each: 2.16 MB per
               rank at 64 images), so no rank ever reads a size on the host before sending and
@@ -121,8 +130,10 @@ class DetectionGather(object):
               forward (measured: 0.13 ms at one rank vs 0.02 ms sized).
     Receive buffers are allocated once per slot."""
 
+    MODES = ("sized", "deferred", "fixed")
+
     def __init__(self, cap, rows, device, slots=2, dst=0, mode="sized"):
-        if mode not in ("sized", "fixed"):
+        if mode not in self.MODES:
             raise ValueError(f"mode {mode!r}")
         self.cap, self.rows, self.dst, self.mode = int(cap), int(rows), dst, mode
         self.rank = dist.get_rank() if _collectives() else 0
@@ -130,50 +141,108 @@ class DetectionGather(object):
         self.meta = [torch.zeros(2 + self.cap, dtype=torch.int32, device=device) for _ in range(slots)]
         root = self.rank == dst
         coll = _collectives()
-        all_meta = coll and mode == "sized"
+        all_meta = coll and mode in ("sized", "deferred")
         self.mparts = [[torch.empty_like(m) for _ in range(self.world)] if coll and (root or all_meta) else None
                        for m in self.meta]
         self.pparts = [[torch.empty((self.rows, 40), dtype=torch.uint8, device=device) for _ in range(self.world)]
                        if coll and root else None for _ in range(slots)]
+        # deferred: the all-gathered meta of each slot lands here (pinned: the copy is async)
+        pin = torch.device(device).type == "cuda"
+        self.hmeta = [torch.zeros((self.world, 2 + self.cap), dtype=torch.int32, pin_memory=pin)
+                      if all_meta and mode == "deferred" else None for _ in range(slots)]
 
-    def launch(self, slot, packed, total, counts, n):
-        """Enqueue slot `slot`'s gathers on the current stream ("sized": after reading the
-        all-gathered sizes on the host); returns a handle for finish()."""
-        if packed.shape[0] != self.rows:
-            raise ValueError(f"packed has {packed.shape[0]} rows, the gather was sized for {self.rows}")
+    def _stage_meta(self, slot, total, counts, n):
         meta = self.meta[slot]
         meta[0:1].copy_(total[:1], non_blocking=True)
         meta[1].fill_(int(n))
         k = min(self.cap, counts.shape[0])
         meta[2:2 + k].copy_(counts[:k], non_blocking=True)
-        coll, root = _collectives(), self.rank == self.dst
-        sizes = None
-        if not coll:
-            mparts, pparts = [meta], [packed]
-        elif self.mode == "sized":
-            mparts = self.mparts[slot]
-            if _host_staged(meta):
-                hp = [torch.empty(p.shape, dtype=p.dtype) for p in mparts]
-                dist.all_gather(hp, meta.cpu())
-                for p, h in zip(mparts, hp):
-                    p.copy_(h)
-            else:
-                dist.all_gather(mparts, meta)
-            sizes = torch.stack(mparts).cpu().numpy()  # host read: this step, every rank
-            pmax = int(sizes[:, 0].max())
-            pparts = self.pparts[slot]
-            if pmax > 0:
-                _gather(packed[:pmax], [p[:pmax] for p in pparts] if root else None, self.dst)
+        return meta
+
+    def _all_gather_meta(self, slot, meta):
+        mparts = self.mparts[slot]
+        if _host_staged(meta):
+            hp = [torch.empty(p.shape, dtype=p.dtype) for p in mparts]
+            dist.all_gather(hp, meta.cpu())
+            for p, h in zip(mparts, hp):
+                p.copy_(h)
         else:
-            mparts, pparts = self.mparts[slot], self.pparts[slot]
-            _gather(meta, mparts if root else None, self.dst)
-            _gather(packed, pparts if root else None, self.dst)
+            dist.all_gather(mparts, meta)
+        return mparts
+
+    def _payload(self, slot, packed, sizes):
+        """Enqueue the payload gather of max-over-ranks valid rows (sizes: numpy [world, ...])."""
+        pmax = int(sizes[:, 0].max())
+        pparts = self.pparts[slot]
+        if pmax > 0:
+            _gather(packed[:pmax], [p[:pmax] for p in pparts] if self.rank == self.dst else None, self.dst)
+        return pparts
+
+    def _handle(self, mparts, pparts, sizes, packed):
         done, stream = None, None
         if packed.is_cuda:
             stream = torch.cuda.current_stream(packed.device)
             done = torch.cuda.Event()
             done.record(stream)
-        return (mparts, pparts, sizes) if root else None, done, stream
+        return (mparts, pparts, sizes) if self.rank == self.dst else None, done, stream
+
+    def launch_meta(self, slot, packed, total, counts, n):
+        """deferred, first half: enqueue slot `slot`'s meta all-gather and its asynchronous
+        copy to pinned host memory on the current stream; nothing waits on the host.  Returns
+        a handle for launch_payload()."""
+        if self.mode != "deferred":
+            raise ValueError("launch_meta is the deferred mode's first half")
+        if packed.shape[0] != self.rows:
+            raise ValueError(f"packed has {packed.shape[0]} rows, the gather was sized for {self.rows}")
+        meta = self._stage_meta(slot, total, counts, n)
+        if not _collectives():
+            return slot, packed, [meta], None
+        mparts = self._all_gather_meta(slot, meta)
+        hm = self.hmeta[slot]
+        ev = None
+        if meta.is_cuda:
+            hm.copy_(torch.stack(mparts), non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(meta.device))
+        else:
+            hm.copy_(torch.stack(mparts))
+        return slot, packed, mparts, ev
+
+    def launch_payload(self, handle):
+        """deferred, second half (a step later): read the sizes the first half copied to the
+        host (waiting only if that copy has not landed yet) and enqueue the payload gather on
+        the current stream.  Returns a handle for finish()."""
+        slot, packed, mparts, ev = handle
+        if not _collectives():
+            return self._handle(mparts, [packed], None, packed)
+        if ev is not None:
+            ev.synchronize()
+        sizes = self.hmeta[slot].numpy().copy()
+        pparts = self._payload(slot, packed, sizes)
+        return self._handle(mparts, pparts, sizes, packed)
+
+    def launch(self, slot, packed, total, counts, n):
+        """Enqueue slot `slot`'s gathers on the current stream ("sized": after reading the
+        all-gathered sizes on the host); returns a handle for finish()."""
+        if self.mode == "deferred":
+            return self.launch_payload(self.launch_meta(slot, packed, total, counts, n))
+        if packed.shape[0] != self.rows:
+            raise ValueError(f"packed has {packed.shape[0]} rows, the gather was sized for {self.rows}")
+        meta = self._stage_meta(slot, total, counts, n)
+        coll = _collectives()
+        sizes = None
+        if not coll:
+            mparts, pparts = [meta], [packed]
+        elif self.mode == "sized":
+            mparts = self._all_gather_meta(slot, meta)
+            sizes = torch.stack(mparts).cpu().numpy()  # host read: this step, every rank
+            pparts = self._payload(slot, packed, sizes)
+        else:
+            mparts, pparts = self.mparts[slot], self.pparts[slot]
+            root = self.rank == self.dst
+            _gather(meta, mparts if root else None, self.dst)
+            _gather(packed, pparts if root else None, self.dst)
+        return self._handle(mparts, pparts, sizes, packed)
 
     @staticmethod
     def finish(handle):
@@ -229,12 +298,20 @@ class ShardedRunner(object):
     """
 
     def __init__(self, compute, global_batch, in_shape, out_shape, device, dtype=torch.float32, timing=True,
-                 slots=3, gather_mode="sized"):
+                 slots=None, gather_mode="sized"):
         self.timing = bool(timing)  # per-step HIP timing events for stats()
+        if gather_mode not in DetectionGather.MODES:
+            raise ValueError(f"gather_mode {gather_mode!r}")
         self.gather_mode = gather_mode  # DetectionGather mode of the pipelined path
-        # steps in flight on the pipelined path (launch_detections / finish_detections):
-        # step k is collected after step k + slots - 1 has been launched
-        self.slots = int(slots)
+        # output / detection buffer slots of the pipelined path (launch_detections /
+        # finish_detections), and steps in flight: the caller finishes step k once step
+        # k + inflight - 1 has been launched.  "deferred" completes a step's gather one finish
+        # later, so it holds one slot more than it keeps steps in flight
+        deferred = gather_mode == "deferred"
+        self.slots = int(slots) if slots is not None else (4 if deferred else 3)
+        self.inflight = self.slots - 1 if deferred else self.slots
+        if self.inflight < 1:
+            raise ValueError(f"slots={self.slots} leaves no step in flight")
         self.rank = dist.get_rank() if dist.is_initialized() else 0
         self.world = dist.get_world_size() if dist.is_initialized() else 1
         self.global_batch = int(global_batch)
@@ -281,6 +358,7 @@ class ShardedRunner(object):
             self._post = torch.cuda.Stream(dev, priority=-1)
             self._freed = [None] * self.slots
             self._gather = None
+            self._deferred = None
             self.reset_stats()
         cur = torch.cuda.current_stream(dev)
         if self._freed[slot] is not None:
@@ -297,19 +375,32 @@ class ShardedRunner(object):
         return slot, packed, total, counts, ev
 
     def finish_detections(self, handle):
-        """Second half, called once the next slots - 1 steps have been launched (three steps
-        in flight by default, so rank 0 waits for a gather that finished a forward ago and
-        the host never starves the queue while an RCCL gather waits for CUs): enqueue the
-        detection gather (DetectionGather) on a side stream that waits only
-        for this step's pack — enqueued this late so that no stream whose hardware queue may
-        be shared with the run stream holds a wait ahead of the next forward — then on
-        rank 0 wait for it and return (dets_u8 [P, 40], counts [global_batch]) numpy; other
-        ranks return None at once (no host synchronisation)."""
+        """Second half, called once the next inflight - 1 steps have been launched (three by
+        default, so rank 0 waits for a gather that finished a forward ago and the host never
+        starves the queue while an RCCL gather waits for CUs): enqueue the detection gather
+        (DetectionGather) on a side stream that waits only for this step's pack — enqueued
+        this late so that no stream whose hardware queue may be shared with the run stream
+        holds a wait ahead of the next forward — then on rank 0 wait for it and return
+        (dets_u8 [P, 40], counts [global_batch]) numpy, None on other ranks.
+        Host synchronisation by mode: "fixed" — none on non-root ranks; "sized" — every
+        rank reads this step's all-gathered sizes (a wait for this step's pack on ALL ranks);
+        "deferred" — this call enqueues this step's size exchange and completes the PREVIOUS
+        step's gather (sizes read a step after their exchange), returning the previous
+        step's detections; flush_detections() completes the last one."""
         slot, packed, total, counts, ev = handle
         if self._gather is None:
             self._gather = DetectionGather(self.shard_cap, packed.shape[0], self.out.device,
                                            slots=self.slots, mode=self.gather_mode)
         t0 = time.perf_counter()
+        if self.gather_mode == "deferred":
+            with torch.cuda.stream(self._side):
+                self._side.wait_event(ev[2])
+                ev[3].record(self._side)
+                ha = self._gather.launch_meta(slot, packed, total, counts, self.count)
+            prev, self._deferred = self._deferred, (ha, ev, slot)
+            r = self._complete(prev) if prev is not None else None
+            self._host_blocked += time.perf_counter() - t0
+            return r
         with torch.cuda.stream(self._side):
             self._side.wait_event(ev[2])
             ev[3].record(self._side)
@@ -318,22 +409,63 @@ class ShardedRunner(object):
         self._freed[slot] = ev[4]
         r = DetectionGather.finish(gh)
         self._host_blocked += time.perf_counter() - t0
-        self._events.append(ev)
+        self._note(ev)
         return r
 
+    def _complete(self, deferred):
+        """deferred mode: the payload gather of a step whose size exchange was enqueued one
+        finish earlier, then (rank 0) its detections."""
+        ha, ev, slot = deferred
+        with torch.cuda.stream(self._side):
+            gh = self._gather.launch_payload(ha)
+            ev[4].record(self._side)
+        self._freed[slot] = ev[4]
+        r = DetectionGather.finish(gh)
+        self._note(ev)
+        return r
+
+    def flush_detections(self):
+        """deferred mode: complete the last step's gather (rank 0: its detections); None when
+        nothing is pending or in the other modes."""
+        if self.gather_mode != "deferred" or getattr(self, "_deferred", None) is None:
+            return None
+        t0 = time.perf_counter()
+        prev, self._deferred = self._deferred, None
+        r = self._complete(prev)
+        self._host_blocked += time.perf_counter() - t0
+        return r
+
+    def _note(self, ev):
+        """Account a finished step's events: running sums, not a growing list (a serving loop
+        runs unbounded steps); events are read once complete."""
+        self._evq.append(ev)
+        self._account(force=False)
+
+    def _account(self, force):
+        while self._evq and (force or self._evq[0][4].query()):
+            e = self._evq.pop(0)
+            self._nsteps += 1
+            if self.timing:
+                if force:
+                    e[4].synchronize()
+                self._sums[0] += e[0].elapsed_time(e[1])
+                self._sums[1] += e[1].elapsed_time(e[2])
+                self._sums[2] += e[3].elapsed_time(e[4])
+
     def reset_stats(self):
-        self._events, self._host_blocked = [], 0.0
+        self._evq, self._nsteps, self._sums, self._host_blocked = [], 0, [0.0, 0.0, 0.0], 0.0
+        self._deferred = getattr(self, "_deferred", None)
 
     def stats(self):
         """Per-step means (ms) over the steps finished since reset_stats(): forward (run
-        stream), post (postprocess + pack), gather (the collectives on the side stream),
-        host_blocked (host time inside finish_detections).  Call after synchronising."""
-        n = len(self._events)
+        stream), post (postprocess + pack), gather (side stream, from the step's size exchange
+        to its payload gather), host_blocked (host time inside finish_detections /
+        flush_detections).  Call after synchronising."""
+        self._account(force=True)
+        n = self._nsteps
         if n == 0 or not self.timing:
             return {"host_blocked_ms": round(self._host_blocked * 1e3 / max(n, 1), 4), "steps": n}
-        f = sum(e[0].elapsed_time(e[1]) for e in self._events) / n
-        p = sum(e[1].elapsed_time(e[2]) for e in self._events) / n
-        g = sum(e[3].elapsed_time(e[4]) for e in self._events) / n
+        f, p, g = (v / n for v in self._sums)
         return {"forward_ms": round(f, 4), "post_ms": round(p, 4), "gather_ms": round(g, 4),
                 "host_blocked_ms": round(self._host_blocked * 1e3 / n, 4), "steps": n}
 

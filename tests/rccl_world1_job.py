@@ -61,16 +61,18 @@ def main():
     local = yolo_post.detect_batch(ref_out.cpu().numpy(), raise_errors=False)  # no process group
     n_det = sum(len(im) for im in local if not isinstance(im, int))
     res = {}
-    for mode in ("sized", "fixed"):
+    for mode in ("sized", "fixed", "deferred"):
         runner = D.ShardedRunner(compute, B, (416, 416, 3), (13, 13, 125), dev, gather_mode=mode)
         dbufs = [yolo_post.DetectionBuffers(runner.shard_cap, dev) for _ in range(runner.slots)]
         got, pending = [], []
-        for k in range(5):  # five steps through three slots: every slot reused
+        for k in range(6):  # six steps through three or four slots: every slot reused
             pending.append(runner.launch_detections(frames, post, k % runner.slots))
-            if len(pending) == runner.slots:
+            if len(pending) == runner.inflight:
                 got.append(runner.finish_detections(pending.pop(0)))
         while pending:
             got.append(runner.finish_detections(pending.pop(0)))
+        got.append(runner.flush_detections())
+        got = [r for r in got if r is not None]  # deferred: the first finish returns nothing
         torch.cuda.synchronize()
         rows = [D.unpack_detections(*r) for r in got]
         res[mode] = {"ok": all(r == local for r in rows), "steps": len(got), "stats": runner.stats()}

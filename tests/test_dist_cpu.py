@@ -130,9 +130,9 @@ def _det_worker(rank, world, port, total, q, mode):
 
 
 @pytest.mark.parametrize("world,total,mode", [(2, 6, "sized"), (2, 5, "fixed"), (8, 19, "sized"), (8, 6, "sized"),
-                                              (8, 13, "fixed")])
+                                              (8, 13, "fixed"), (2, 7, "deferred"), (8, 19, "deferred")])
 def test_sharded_detection_gather_gloo(world, total, mode):
-    """Per-rank postprocessing + packed detection gather (dist.DetectionGather, both modes)
+    """Per-rank postprocessing + packed detection gather (dist.DetectionGather, all modes)
     gives rank 0 every image's detections in global order, with unequal per-rank detection
     counts, ragged shards and (8, 6) ranks that hold no image at all."""
     ctx = mp.get_context("spawn")

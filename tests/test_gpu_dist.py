@@ -31,6 +31,28 @@ def test_bench_two_ranks_one_gpu(gather):
         assert d["postprocess"]["detections_last_step"] > 0
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["deferred", "sized"])
+def test_bench_eight_ranks_one_gpu(mode):
+    """BASELINE config 4's process layout rehearsed on one GPU: `bench.py --gpus 8` relaunches
+    under torch.distributed.run with 8 ranks, each laying out its own device plan (batch 4:
+    the shard), receiving the weight arena by broadcast, postprocessing on the device and
+    gathering packed detections to rank 0 in the given gather mode; gloo host-staged
+    collectives stand in for RCCL (one card).  The JSON line carries all 8 ranks."""
+    env = dict(os.environ, DNN_BENCH_SHARED_GPU="1", DNN_BENCH_BACKEND="gloo", DNN_BENCH_GATHER_MODE=mode)
+    cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "8", "--batch", "4", "--steps", "4",
+           "--warmup", "2", "--no-cpu", "--no-latency", "--no-e2e", "--no-fp16", "--no-unfused"]
+    r = subprocess.run(cmd, env=env, cwd=REPO, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-3000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 8 and d["config"]["global_batch"] == 32 and d["config"]["parallelism"] == "dp8"
+    assert len(d["per_rank"]) == 8 and [p["rank"] for p in d["per_rank"]] == list(range(8))
+    assert all(p["wall_ms"] > 0 and p["forward_ms"] > 0 for p in d["per_rank"])
+    assert d["postprocess"]["detections_last_step"] > 0
+
+
 def _torchrun(script_args, timeout=300):
     import socket
     with socket.socket() as s:
@@ -44,17 +66,19 @@ def _torchrun(script_args, timeout=300):
 @pytest.mark.gpu
 def test_rccl_world1_broadcast_and_gathers():
     """A real RCCL process group (backend "nccl", world size 1, cuda:0): the weight-arena
-    broadcast, gather_outputs and the pipelined detection gather (both modes) all execute
-    on MI355X and agree with the same work done without a process group."""
+    broadcast, gather_outputs and the pipelined detection gather (all three modes, six steps
+    through every output slot; "deferred" completes each step one finish later and the last
+    by flush_detections) all execute on MI355X and agree with the same work done without a
+    process group."""
     r = _torchrun([os.path.join(REPO, "tests", "rccl_world1_job.py")])
     assert r.returncode == 0, r.stderr[-3000:]
     d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
     assert d["backend"] == "nccl" and d["arena_ok"] and d["detections"] > 0
     assert d["outputs_shape"] == [8, 13, 13, 125]
-    for mode in ("sized", "fixed"):
+    for mode in ("sized", "fixed", "deferred"):
         m = d["modes"][mode]
-        assert m["ok"] and m["steps"] == 5, (mode, m)
-        assert m["stats"]["steps"] == 5 and m["stats"]["forward_ms"] > 0
+        assert m["ok"] and m["steps"] == 6, (mode, m)
+        assert m["stats"]["steps"] == 6 and m["stats"]["forward_ms"] > 0
 
 
 @pytest.mark.gpu

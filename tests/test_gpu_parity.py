@@ -1349,3 +1349,52 @@ def test_x3_patch_variants_bit_equal(tmp_path):
     assert outs["0"].shape == (2, 13, 13, 125)
     assert np.isfinite(outs["1"]).all()
     assert np.array_equal(outs["0"], outs["1"]) and np.array_equal(outs["0"], outs["2"])
+
+
+@pytest.mark.parametrize("kind", ["huge", "tiny"])
+def test_x3_split_total_over_finite_fp32(monkeypatch, kind):
+    """split3 (gemm_f32.h) is total over finite fp32: an operand above the largest bf16
+    (0x1.fep127 < |x| <= FLT_MAX, where round-to-nearest gives inf and the remainder a NaN)
+    takes the truncated top piece and stays exact; operands below 2^-100 lose at most 2^-124
+    absolute.  A pool -> conv3x3 (x3 patch kernel, C = 64 -> 256) on inputs holding such values
+    among normal ones: finite everywhere, within the layer tolerance of the float64 oracle and
+    of the fp32-MFMA path's error (DNN_HIP_X3=0) on the same input."""
+    rng = np.random.default_rng(11 if kind == "huge" else 12)
+    B, H, W, C, N = 2, 13, 13, 64, 256
+    x = rng.standard_normal((B, H, W, C)).astype(np.float32)
+    fmax = np.finfo(np.float32).max
+    if kind == "huge":
+        # FLT_MAX, values between the largest bf16 and FLT_MAX, and their negatives, spread over
+        # pixels and channels; weights small enough that every sum stays finite
+        vals = np.array([fmax, 3.3999e38, 3.3962e38, -fmax, -3.398e38, 3.3895e38], np.float32)
+        idx = rng.choice(B * H * W * C, size=120, replace=False)
+        x.reshape(-1)[idx] = vals[np.arange(idx.size) % vals.size]
+        scale = 1e-8
+    else:
+        # a quarter of the elements below 2^-100 (down into fp32 denormals)
+        tiny = (rng.standard_normal(x.size // 4) * 10.0 ** rng.uniform(-44, -31, x.size // 4)).astype(np.float32)
+        x.reshape(-1)[rng.choice(x.size, size=tiny.size, replace=False)] = tiny
+        scale = 1.0
+    k = (rng.standard_normal((3, 3, C, N)) * np.sqrt(2.0 / (9 * C)) * scale).astype(np.float32)
+
+    def graph():
+        g = dnn_hip.DnnGraphBuilder()
+        y = g.create_input(list(x.shape))
+        y = g.create_max_pool2d(y, [1, 2, 2, 1], [1, 1, 1, 1], "SAME")
+        y = g.create_conv2d(y, k, [1, 1, 1, 1], "SAME")
+        g.set_out_node(y)
+        return g
+
+    ref = R.conv2d(R.max_pool2d(x, [1, 2, 2, 1], [1, 1, 1, 1], "SAME"), k)
+    assert np.isfinite(ref).all()
+    errs = {}
+    for x3 in ("1", "0"):
+        monkeypatch.setenv("DNN_HIP_X3", x3)
+        eng = dnn_hip.DnnInferenceEngine(graph(), False)
+        assert eng.plan().describe().count("mode=patch_x3") == (1 if x3 == "1" else 0)
+        y = eng.run(x)
+        assert np.isfinite(y).all(), (x3, int((~np.isfinite(y)).sum()))
+        errs[x3] = R.normwise_err(y, ref)
+        print("%s x3=%s normwise err %.3e" % (kind, x3, errs[x3]))
+    assert errs["1"] < LAYER_TOL and errs["0"] < LAYER_TOL, errs
+    assert errs["1"] <= max(1.25 * errs["0"], 2e-7), errs
