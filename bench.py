@@ -508,7 +508,7 @@ def main():
 
     runner = D.ShardedRunner(compute, B * world, (416, 416, 3), (13, 13, 125), dev,
                              timing=os.environ.get("DNN_BENCH_STEP_EVENTS", "1") == "1",
-                             gather_mode=os.environ.get("DNN_BENCH_GATHER_MODE", "sized"))
+                             gather_mode=os.environ.get("DNN_BENCH_GATHER_MODE", "deferred"))
     if args.gather == "detections":
         import yolo_post
         dbufs = [yolo_post.DetectionBuffers(runner.shard_cap, dev) for _ in range(runner.slots)]

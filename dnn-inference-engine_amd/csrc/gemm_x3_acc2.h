@@ -1,0 +1,278 @@
+// fp32 3x3 conv on the bf16 MFMA with exact three-way operand splits ("x3", gemm_x3_patch.h),
+// two accumulators per output and no per-step adds: the default kernel of the wide-N layers of
+// the fp32 path (YOLOv2-tiny conv4-conv7), device code only.
+//
+// The round-2 kernel (conv3x3_x3_patch_kernel, DNN_HIP_X3V=1) sums each 32-channel step's five
+// correction products from zero and adds them into the accumulator: 4 v_add per 6 MFMAs, with
+// two waves per SIMD sharing the vector issue of v_mfma_f32_16x16x32_bf16's 16-cycle slot.
+// Here every output keeps TWO accumulators over the whole K range: `accm` takes the main
+// product a0*b0 of every step, `accc` the five corrections a2b0 + a1b1 + a0b2 + a1b0 + a0b1;
+// the output is accm + accc, one add per output at the end.  The main accumulator still sees
+// one MFMA rounding per step and no longer the per-step add; the corrections (<= 2^-7 of the
+// main product each) are rounded at their own, 2^-8 smaller, magnitude
+// (tests/test_gpu_parity.py::test_x3_conv_vs_oracle holds the error to <= 1.25x the fp32
+// MFMA path's).  Summation order: per output, accm over the steps (chunk-major, tap-minor) of
+// a0 b0; accc over the same steps of (a2b0, a1b1, a0b2, a1b0, a0b1) in that order; then
+// accm + accc.  It depends on (N, K) only (batch rows are bit-identical to batch-1 runs).
+#pragma once
+#include "gemm_x3_patch.h"
+
+namespace dnnhip {
+
+template <int I, int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<I + 1, N>(f);
+  }
+}
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// Structure: BM x 256 tiles, 8 waves of BM x 32 (two per SIMD, 256 registers each: the two
+// accumulator sets take 176), the weights of the next tap loaded while this one runs (48), the
+// A fragments read at each row block's start (the partner wave's MFMAs cover the LDS latency),
+// the patch of one 32-channel chunk staged by LDS-DMA into a double buffer (no staging
+// registers), one barrier per chunk.  Why two waves per SIMD: a one-wave-per-SIMD form (4 waves
+// of 176 x 64 with 512 registers, round 3, git history) lost its MFMA pipe to the issue cost of
+// every vector-memory instruction (~60 cycles each: the weight loads alone 12 % of the kernel,
+// measured with diagnostic builds that dropped them), which only a partner wave can cover.
+// LP: LDS bytes per patch row.  192 (the data) costs 7 bank-conflict cycles per fragment read at
+// 13-wide frames, 224 about 4 (tools/lds_conflict_model.py: the two 8-lane halves of each
+// ds_read_b128 lane group then fall on even / odd bank quads for any 8 rows distinct mod 8;
+// the image-row wraps inside a 16-row fragment leave the rest) with plain row-offset addresses
+// (the round-2 kernel's XOR swizzle reaches the same count but costs ~5 VALU per fragment:
+// 0.850 vs 0.826 ms conv7 here, same call).  The padding bytes of each LDS row are whatever
+// follows the chunk in global memory, never read.
+template <int BM, int NPR, bool POOL, int LP = 224>
+__global__ void __launch_bounds__(512, 2)
+conv3x3_x3_acc2_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __restrict__ Bt, float* __restrict__ out,
+                       bf16_bits* __restrict__ out_split, int M, int N, int K, EpiParams epi, int tilesM, X3Geom g,
+                       unsigned in_bytes, unsigned b_bytes) {
+  constexpr int BN = 256, TM = BM / 16, RB = 192, NJ = 2, NW = 8;
+  constexpr int NQW = (NPR * LP + NW * 1024 - 1) / (NW * 1024);  // 1-KiB DMA pieces per wave per patch
+  constexpr int BUFB = NQW * NW * 1024;                            // one patch buffer (>= NPR LP)
+  static_assert(BM % 16 == 0 && LP % 16 == 0 && LP >= RB && NQW <= 18, "shape");
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * BUFB];
+
+  const int lane = threadIdx.x & 63;
+  const int wid = wave_uniform(threadIdx.x >> 6);
+  const int tile_s = xcd_tile(blockIdx.x, gridDim.x), ntiles = gridDim.x / g.splits;
+  const int split = tile_s / ntiles, tile = tile_s - split * ntiles;
+  const int tn = tile / tilesM, tm = tile - tn * tilesM;
+  const int m0 = tm * BM, n0 = tn * BN + wid * 32;  // this wave's 32 columns
+  const int Wp = g.W + 2, HWo = g.H * g.W;
+  auto padded = [&](int m) {
+    const int b = m / HWo, r = m - b * HWo, oy = r / g.W, ox = r - oy * g.W;
+    return (b * (g.H + 2) + oy + 1) * Wp + ox + 1;
+  };
+  auto pixrow = [&](int m) {
+    if constexpr (!POOL) {
+      return padded(m);
+    } else {
+      const int w = m >> 2, q = m & 3, PHW = g.PH * g.PW;
+      const int b = w / PHW, r = w - b * PHW, py = r / g.PW, px = r - py * g.PW;
+      int oy = 2 * py + (q >> 1), ox = 2 * px + (q & 1);
+      if (oy >= g.H || ox >= g.W) oy = 2 * py, ox = 2 * px;
+      return (b * (g.H + 2) + oy + 1) * Wp + ox + 1;
+    }
+  };
+  const int P0 = pixrow(m0) - (Wp + 1);  // first patch row
+
+  // A fragment of row-block i: byte offset (in a patch buffer) of the lane's tap (0, 0) row + 16 fq
+  const int fr = lane & 15, fq = lane >> 4;
+  int prow[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    int m = m0 + 16 * i + fr;
+    m = m < M ? m : M - 1;
+    prow[i] = (pixrow(m) - P0 - (Wp + 1)) * LP + 16 * fq;
+  }
+
+  // patch DMA: this wave's piece k lands at LDS byte 1024 (wid + 8 k) + 16 lane = patch row r
+  // (LP bytes each: the 192 data bytes of the chunk and, with LP > 192, the next LP - 192 bytes
+  // of global memory as never-read padding), unit u; one 16-B unit from (P0 + r) rowB + chunk
+  // 192 + 16 u.  Per-lane part computed at issue (a few VALU per tap)
+  const int nk = K / 32, nch = nk / 9 / g.splits, cb = split * nch;
+  const int rowB = 6 * g.C;
+  const auto rsA = __builtin_amdgcn_make_buffer_rsrc((void*)in, 0, (int)in_bytes, 0x00020000);
+  const unsigned dsoff = (unsigned)(P0 * rowB + cb * RB);
+  auto issue_patch = [&](int chunk, int k, int buf) {
+    const unsigned b = 1024u * (unsigned)(wid + NW * k) + 16u * (unsigned)lane;
+    const unsigned r = b / LP, u = (b - r * LP) >> 4;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(
+        rsA, (__attribute__((address_space(3))) void*)(smem + buf * BUFB + 1024 * (wid + NW * k)), 16,
+        (int)(__umul24(r, (unsigned)rowB) + 16 * u), (int)(dsoff + chunk * RB), 0, 0);
+  };
+
+  // weights [n/16][step][piece][lane][8]: the wave's two 16-column blocks, one tap ahead
+  const unsigned bvo = (unsigned)((n0 / 16) * nk * 3072 + lane * 16 + cb * 9 * 3072);
+  const int bjs = nk * 3072;
+  const auto rsB = __builtin_amdgcn_make_buffer_rsrc((void*)Bt, 0, (int)b_bytes, 0x00020000);
+  bf16x8 bq[2][3][NJ];
+  auto load_b1 = [&](int s, int p, int j, bf16x8& dst) {
+    dst = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rsB, bvo, s * 3072 + p * 1024 + j * bjs, 0));
+  };
+  auto load_b = [&](int s, bf16x8 (&dst)[3][NJ]) {
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) load_b1(s, p, j, dst[p][j]);
+  };
+
+  f32x4 accm[TM][NJ], accc[TM][NJ];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      accm[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      accc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+
+#pragma unroll
+  for (int k = 0; k < NQW; ++k) issue_patch(0, k, 0);
+  load_b(0, bq[0]);
+  vm_wait<0>();
+  __syncthreads();
+
+  // Per tap: TM row blocks of 12 MFMAs (per column block the five corrections back to back,
+  // then the main product), the first ones also issuing the next tap's weights and DMA pieces
+  // t (and t + 9 when NQW > 9) of chunk j + 1; the chunk's barrier after tap 8 waits for this
+  // wave's DMA pieces and everyone's reads.
+  const int nsteps = 9 * nch;
+  const unsigned char* P = smem;
+  int t = 0, j = 0;
+  for (int s = 0; s < nsteps; ++s) {
+    const int toff = (t / 3) * Wp + (t % 3);  // tap (dy, dx) relative to (0, 0)
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      // the tap's vector-memory instructions spread over its first row blocks (one each: a
+      // lone wave stalls ~60 cycles per issue, and waves in step after the chunk barrier would
+      // otherwise all stall at once): the next tap's 6 weight fragments, then the DMA pieces
+      static_assert(TM >= 3 * NJ + 2, "row blocks to spread the tap's loads over");
+      if (i < 3 * NJ) load_b1(s + 1, i / NJ, i % NJ, bq[1][i / NJ][i % NJ]);
+      if (i == 3 * NJ) issue_patch(j + 1, t < NQW ? t : NQW - 1, (j + 1) & 1);  // (uniform count per tap)
+      if constexpr (NQW > 9) {  // pieces past NQW rewrite piece NQW - 1
+        if (i == 3 * NJ + 1) issue_patch(j + 1, t + 9 < NQW ? t + 9 : NQW - 1, (j + 1) & 1);
+      }
+      bf16x8 a[3];
+      const unsigned char* q = P + prow[i] + toff * LP;
+#pragma unroll
+      for (int p = 0; p < 3; ++p) a[p] = *reinterpret_cast<const bf16x8*>(q + 64 * p);
+#pragma unroll
+      for (int jb = 0; jb < NJ; ++jb) {
+        f32x4 c = accc[i][jb];
+        c = mfma16_bf16(a[2], bq[0][0][jb], c);
+        c = mfma16_bf16(a[1], bq[0][1][jb], c);
+        c = mfma16_bf16(a[0], bq[0][2][jb], c);
+        c = mfma16_bf16(a[1], bq[0][0][jb], c);
+        c = mfma16_bf16(a[0], bq[0][1][jb], c);
+        accc[i][jb] = c;
+        accm[i][jb] = mfma16_bf16(a[0], bq[0][0][jb], accm[i][jb]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+#pragma unroll
+      for (int jb = 0; jb < NJ; ++jb) bq[0][p][jb] = bq[1][p][jb];
+    if (++t == 9) {
+      t = 0;
+      ++j;
+      vm_wait<0>();  // this wave's DMA pieces landed (issued mid-tap: ~5 row blocks ago)
+      wait_lgkm0();
+      raw_barrier();
+      P = smem + (j & 1) * BUFB;
+    }
+  }
+  vm_wait<0>();
+
+  // epilogue: the reference's fp32 epilogue on accm + accc, then fp32 [M][N], the split planes of
+  // the next x3 layer's zero-bordered input, or the raw partial of split-K slice `split`
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int jb = 0; jb < NJ; ++jb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) accm[i][jb][r] = accm[i][jb][r] + accc[i][jb][r];
+  int* orow = reinterpret_cast<int*>(smem);
+  __syncthreads();
+  if constexpr (POOL) {
+    if (threadIdx.x < BM / 4) {
+      const int w = (m0 >> 2) + threadIdx.x, PHW = g.PH * g.PW;
+      const int b = w / PHW, r = w - b * PHW, py = r / g.PW, px = r - py * g.PW;
+      orow[threadIdx.x] = 4 * w >= M ? -1 : g.out_mode == 1 ? (b * (g.PH + 2) + py + 1) * (g.PW + 2) + px + 1 : w;
+    }
+    __syncthreads();
+    static_for<0, NJ>([&](auto jbc) {
+      constexpr int jb = decltype(jbc)::value;
+      const int n = n0 + 16 * jb + fr;
+      const float pb = (epi.flags & EPI_BIAS) ? epi.bias[n] : 0.f;
+      const float pm = (epi.flags & (EPI_BN | EPI_BN_AB)) ? epi.mean[n] : 0.f;
+      const float ps = (epi.flags & (EPI_BN | EPI_BN_AB)) ? epi.sq[n] : 1.f;
+      const float pg = (epi.flags & EPI_BN) ? epi.gamma[n] : 1.f;
+      const int cofs = (n >> 5) * 96 + (n & 31);
+      static_for<0, TM>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        const int o = orow[4 * i + fq];
+        if (o < 0) return;
+        const float e = pool_then_epilogue(accm[i][jb], pb, pm, ps, pg, epi.flags);
+        if (g.out_mode == 1) {
+          unsigned short s0, s1, s2;
+          split3(e, s0, s1, s2);
+          bf16_bits* d = out_split + (size_t)o * (3 * N) + cofs;
+          d[0] = s0;
+          d[32] = s1;
+          d[64] = s2;
+        } else {
+          out[(size_t)o * N + n] = e;
+        }
+      });
+    });
+    return;
+  }
+  if (threadIdx.x < BM) {
+    const int m = m0 + threadIdx.x;
+    orow[threadIdx.x] = m >= M ? -1 : (g.out_mode == 1 ? padded(m) : m);
+  }
+  __syncthreads();
+  static_for<0, NJ>([&](auto jbc) {
+    constexpr int jb = decltype(jbc)::value;
+    const int n = n0 + 16 * jb + fr;
+    const float pb = (epi.flags & EPI_BIAS) ? epi.bias[n] : 0.f;
+    const float pm = (epi.flags & (EPI_BN | EPI_BN_AB)) ? epi.mean[n] : 0.f;
+    const float ps = (epi.flags & (EPI_BN | EPI_BN_AB)) ? epi.sq[n] : 1.f;
+    const float pg = (epi.flags & EPI_BN) ? epi.gamma[n] : 1.f;
+    const int cofs = (n >> 5) * 96 + (n & 31);
+    static_for<0, TM>([&](auto ic) {
+      constexpr int i = decltype(ic)::value;
+      static_for<0, 4>([&](auto rc) {
+        constexpr int r = decltype(rc)::value;
+        const int o = orow[16 * i + 4 * fq + r];
+        if (o < 0) return;
+        const float v = accm[i][jb][r];
+        if (g.out_mode == 2) {
+          out[((size_t)split * M + o) * N + n] = v;
+          return;
+        }
+        const float e = apply_epilogue(v, pb, pm, ps, pg, epi.flags);
+        if (g.out_mode == 1) {
+          unsigned short s0, s1, s2;
+          split3(e, s0, s1, s2);
+          bf16_bits* d = out_split + (size_t)o * (3 * N) + cofs;
+          d[0] = s0;
+          d[32] = s1;
+          d[64] = s2;
+        } else {
+          out[(size_t)o * N + n] = e;
+        }
+      });
+    });
+  });
+}
+
+}  // namespace dnnhip

@@ -50,15 +50,12 @@ __device__ __forceinline__ f32x4 mfma16_bf16(bf16x8 a, bf16x8 b, f32x4 c) {
 // dx) of pooled pixel w; cells past an odd edge repeat cell (0, 0)), so a lane's 4 accumulator
 // registers (rows 4 q .. 4 q + 3 of its 16 x 16 block) are one window: pooled before the
 // epilogue (pool_then_epilogue, as the fp32 GEMMs' fused pools)
-// VAR (DNN_HIP_X3V): 1 (default) = weight ring of 2 steps, patch rows packed three per register;
-// 0 = ring of 3, rows one per register (round-2 kernel); 2 = ring of 2, rows read from an LDS
-// table per fragment.  All three compute the same bits (tools/x3v_job.sh checks the net's output).
-// At 256 registers the row table is what the compiler spills, and every reload's vmcnt(0) also
-// drained the weight loads issued two taps ahead: 13 such waits per chunk with VAR 0, 4 with
-// VAR 1, 1 with VAR 2 (which pays an LDS read per fragment instead).  Measured at batch 64
-// (same call): conv7 0.840 / 0.791 / 0.811 ms, conv6 0.455 / 0.419 / 0.429, conv4 (pool-fused)
-// 0.129 / 0.114 / 0.116, conv5 0.139 / 0.129 / 0.131 for VAR 0 / 1 / 2.
-template <int BM, int NPR, bool POOL = false, int VAR = 1>
+// Weight ring of 2 steps, patch rows packed three per register (10-bit fields): at 256
+// registers a row table is what the compiler spills, and every reload's vmcnt(0) also drained
+// the weight loads in flight (round 2 measured a 3-step ring with one row per register and an
+// LDS row table: conv7 0.840 / 0.811 ms against 0.791 for this form).  Since round 3 the
+// default for these layers is conv3x3_x3_acc2_kernel (gemm_x3_acc2.h); DNN_HIP_X3V=1 keeps this.
+template <int BM, int NPR, bool POOL = false>
 __global__ void __launch_bounds__(512, 1)
 conv3x3_x3_patch_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __restrict__ Bt, float* __restrict__ out,
                         bf16_bits* __restrict__ out_split, int M, int N, int K, EpiParams epi, int tilesM, X3Geom g,
@@ -66,11 +63,8 @@ conv3x3_x3_patch_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __res
   constexpr int BN = 256, TM = BM / 16, RB = 192;  // 8 waves of BM x 32; patch row bytes
   constexpr int SR = 32, PPT = NPR / SR;           // staging: 384 threads = 32 rows x 12 slots
   static_assert(BM % 16 == 0 && NPR % SR == 0 && PPT >= 1 && PPT <= 16, "shape");
-  static_assert(VAR >= 0 && VAR <= 2, "variant");
-  constexpr int BD = VAR == 0 ? 3 : 2;
-  constexpr bool RTAB = VAR == 2;
+  constexpr int BD = 2;
   __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * NPR * RB];
-  __shared__ int rowtab[RTAB ? BM : 1];
 
   const int lane = threadIdx.x & 63;
   const int wid = wave_uniform(threadIdx.x >> 6);
@@ -108,10 +102,9 @@ conv3x3_x3_patch_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __res
   // from x to x+4, and XOR-ing it into slot bit 1 separates them for any first row (no
   // conflict for 16 consecutive rows; an image-row wrap inside a fragment costs a few 2-ways)
   const int fr = lane & 15, fq = lane >> 4;
-  // BD = 2: the patch rows (< NPR <= 1024) packed three per register (10-bit fields)
-  constexpr bool PACK = VAR == 1;
-  static_assert(!PACK || NPR <= 1024, "packed patch rows");
-  constexpr int NPW = PACK ? (TM + 2) / 3 : TM;
+  // the patch rows (< NPR <= 1024) packed three per register (10-bit fields)
+  static_assert(NPR <= 1024, "packed patch rows");
+  constexpr int NPW = (TM + 2) / 3;
   int prow[NPW];
 #pragma unroll
   for (int i = 0; i < NPW; ++i) prow[i] = 0;
@@ -119,17 +112,7 @@ conv3x3_x3_patch_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __res
   for (int i = 0; i < TM; ++i) {
     int m = m0 + 16 * i + fr;
     m = m < M ? m : M - 1;
-    if constexpr (PACK)
-      prow[i / 3] |= (pixrow(m) - P0) << (10 * (i % 3));
-    else if constexpr (!RTAB)
-      prow[i] = pixrow(m) - P0;
-  }
-  if constexpr (RTAB) {  // published before the prologue's barrier
-    if (threadIdx.x < BM) {
-      int m = m0 + threadIdx.x;
-      m = m < M ? m : M - 1;
-      rowtab[threadIdx.x] = pixrow(m) - P0;
-    }
+    prow[i / 3] |= (pixrow(m) - P0) << (10 * (i % 3));
   }
 
   // patch staging: thread (tid % 384) owns slot ss = t % 12 of rows t / 12 + 32 u (waves 6, 7
@@ -192,16 +175,9 @@ conv3x3_x3_patch_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __res
 
   // piece u of patch j+1: loaded at tap L(u) = 8u / PPT of chunk j, written at tap L(u) + 1
   auto frag = [&](const unsigned char* P, int i, int toff, bf16x8 (&a)[3]) {
-    int pr;
-    if constexpr (RTAB) {
-      int ta = (16 * i + fr) * 4;
-      asm volatile("" : "+v"(ta));  // one LDS read per fragment (no CSE across the taps)
-      pr = *reinterpret_cast<const int*>(reinterpret_cast<const unsigned char*>(rowtab) + ta);
-    } else {
-      pr = prow[PACK ? i / 3 : i];
-      asm volatile("" : "+v"(pr));  // keep the taps' addresses from being hoisted
-      if constexpr (PACK) pr = (pr >> (10 * (i % 3))) & 1023;
-    }
+    int pr = prow[i / 3];
+    asm volatile("" : "+v"(pr));  // keep the taps' addresses from being hoisted
+    pr = (pr >> (10 * (i % 3))) & 1023;
     const int row = pr + toff;
     const unsigned char* q = P + row * RB + 16 * (fq ^ ((row >> 1) & 2));  // (shift form: same time)
 #pragma unroll

@@ -3,7 +3,7 @@
 // max pool that feeds it) and its weight packing.
 #include "dnn_common.h"
 #include "gemm_x3_patch.h"
-#include "gemm_x3_w1.h"
+#include "gemm_x3_acc2.h"
 
 #include <cfloat>
 #include <cstdlib>
@@ -326,7 +326,6 @@ static bool x3_enabled() {
 }
 
 constexpr int X3_NPR_POOL = 352;  // pool-window-major tiles span more rows (26x26: 350)
-constexpr int X3_NPR_POOL_W1 = 384;  // the one-wave kernel's DMA wants a multiple of 64 rows
 
 // rows of the padded input one BM-row tile spans (tap offsets included); pool: window-major
 static long long x3_span(long long M, int H, int W, bool pool = false) {
@@ -479,49 +478,39 @@ int launch_conv_x3(const bf16_bits* in_split, const bf16_bits* Bt, float* out, b
   }
   const int tilesM = (int)((M + X3_BM - 1) / X3_BM), tilesN = N / 256;
   // splits > 1: `out` receives the raw partials [splits][M][N] (x3_combine_kernel finishes)
-  static const int prio = [] {
-    const char* e = getenv("DNN_HIP_X3PRIO");
-    return e && e[0] == '1' ? 1 : 0;
-  }();
-  const X3Geom xg{H, W, C, splits > 1 ? 2 : out_split ? 1 : 0, splits, PH, PW, prio};
+  const X3Geom xg{H, W, C, splits > 1 ? 2 : out_split ? 1 : 0, splits, PH, PW, 0};
+  // DNN_HIP_X3V: unset / 0 = the two-accumulator kernel (gemm_x3_acc2.h) with 224-B LDS rows,
+  // 2 = the same with 192-B rows, 1 = the round-2 kernel (conv3x3_x3_patch_kernel: per-step adds;
+  // a different summation order, so not the same bits)
   static const int var = [] {
     const char* e = getenv("DNN_HIP_X3V");
-    const int v = e ? atoi(e) : 1;
-    return v >= 0 && v <= 4 ? v : 1;
+    return e ? atoi(e) : 0;
   }();
-  if (var >= 3) {  // one wave per SIMD, accumulators over all of K (gemm_x3_w1.h); 4: swizzled rows
-#define X3W(NPR_, POOL_, SWZ_)                                                                           \
-  hipLaunchKernelGGL((conv3x3_x3_w1_kernel<X3_BM, NPR_, POOL_, SWZ_>), dim3(tilesM * tilesN * (POOL_ ? 1 : splits)), \
-                     dim3(256), 0, stream, in_split, Bt, out, out_split, (int)M, N, K, epi, tilesM, xg,          \
-                     (unsigned)in_bytes, (unsigned)b_bytes)
-    if (pool && var == 4)
-      X3W(X3_NPR_POOL_W1, true, true);
-    else if (pool)
-      X3W(X3_NPR_POOL_W1, true, false);
-    else if (var == 4)
-      X3W(X3_NPR, false, true);
+  const dim3 grid(tilesM * tilesN * (pool ? 1 : splits));
+#define X3A(NPR_, POOL_, LP_)                                                                                  \
+  hipLaunchKernelGGL((conv3x3_x3_acc2_kernel<X3_BM, NPR_, POOL_, LP_>), grid, dim3(512), 0, stream, in_split, Bt, \
+                     out, out_split, (int)M, N, K, epi, tilesM, xg, (unsigned)in_bytes, (unsigned)b_bytes)
+#define X3P(NPR_, POOL_)                                                                                       \
+  hipLaunchKernelGGL((conv3x3_x3_patch_kernel<X3_BM, NPR_, POOL_>), grid, dim3(512), 0, stream, in_split, Bt, out, \
+                     out_split, (int)M, N, K, epi, tilesM, xg, (unsigned)in_bytes, (unsigned)b_bytes)
+  if (var == 1) {
+    if (pool)
+      X3P(X3_NPR_POOL, true);
     else
-      X3W(X3_NPR, false, false);
-#undef X3W
-    return check_x3("conv_x3 (w1)");
-  }
-#define X3P(NPR_, POOL_, V_)                                                                                  \
-  hipLaunchKernelGGL((conv3x3_x3_patch_kernel<X3_BM, NPR_, POOL_, V_>), dim3(tilesM * tilesN * (POOL_ ? 1 : splits)), \
-                     dim3(512), 0, stream, in_split, Bt, out, out_split, (int)M, N, K, epi, tilesM, xg,           \
-                     (unsigned)in_bytes, (unsigned)b_bytes)
-#define X3PV(NPR_, POOL_)                 \
-  switch (var) {                          \
-    case 0: X3P(NPR_, POOL_, 0); break;   \
-    case 2: X3P(NPR_, POOL_, 2); break;   \
-    default: X3P(NPR_, POOL_, 1); break;  \
-  }
-  if (pool) {
-    X3PV(X3_NPR_POOL, true);
+      X3P(X3_NPR, false);
+  } else if (var == 2) {
+    if (pool)
+      X3A(X3_NPR_POOL, true, 192);
+    else
+      X3A(X3_NPR, false, 192);
   } else {
-    X3PV(X3_NPR, false);
+    if (pool)
+      X3A(X3_NPR_POOL, true, 224);
+    else
+      X3A(X3_NPR, false, 224);
   }
-#undef X3PV
 #undef X3P
+#undef X3A
   return check_x3("conv_x3");
 }
 

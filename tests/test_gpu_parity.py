@@ -1332,23 +1332,25 @@ def test_x3_tile_kernel_vs_oracle(monkeypatch, case):
     assert errs["1"] <= 1.25 * errs["0"], errs
 
 
-def test_x3_patch_variants_bit_equal(tmp_path):
-    """The x3 patch kernel's register variants (DNN_HIP_X3V 0 / 1 / 2: weight ring depth and where
-    the patch-row table lives, gemm_x3_patch.h) compute the same bits: the whole net at batch 2
-    (conv4-conv7 on the patch kernel), each arm in its own process (the switch is read once)."""
+def test_x3_patch_variants(tmp_path):
+    """The wide-layer x3 kernels (DNN_HIP_X3V, read once per process: each arm in its own process)
+    on the whole net at batch 2 (conv4-conv7): the two-accumulator kernel with 224-B and with
+    192-B LDS rows (gemm_x3_acc2.h; same products in the same order) give the same bits; the
+    round-2 kernel (per-step adds: another summation order) agrees within the net tolerance."""
     import subprocess
     import sys
 
     tool = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "x3v_out.py")
     outs = {}
-    for v in ("0", "1", "2"):
+    for v in ("0", "2", "1"):
         f = str(tmp_path / ("out%s.npy" % v))
         env = dict(os.environ, DNN_HIP_X3V=v)
         subprocess.run([sys.executable, tool, f, "2"], env=env, check=True, timeout=110)
         outs[v] = np.load(f)
     assert outs["0"].shape == (2, 13, 13, 125)
-    assert np.isfinite(outs["1"]).all()
-    assert np.array_equal(outs["0"], outs["1"]) and np.array_equal(outs["0"], outs["2"])
+    assert np.isfinite(outs["0"]).all()
+    assert np.array_equal(outs["0"], outs["2"])
+    assert R.normwise_err(outs["1"], outs["0"]) < NET_TOL
 
 
 @pytest.mark.parametrize("kind", ["huge", "tiny"])

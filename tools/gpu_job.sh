@@ -5,7 +5,8 @@
 # Tasks (output under gpurun_out/$OUT, default gpurun_out/job):
 #   tests [PYTEST_ARGS...]     pytest -m gpu (extra args passed through, e.g. -k x3)
 #   bench [BENCH_ARGS...]      one bench.py line (fp32 forward only unless args say otherwise)
-#   ab VAR V1 V2 [BENCH_ARGS]  bench.py --kernels with env VAR=V1, then VAR=V2, per-kernel ms side by side
+#   ab VAR V1 V2 [BENCH_ARGS]  bench.py --kernels with env VAR=V1, then VAR=V2, then V1 again
+#   sweep VAR V1 V2 ...        bench.py --kernels (forward only) for each value of env VAR, then V1 again
 #   trace [BENCH_ARGS...]      rocprofv3 --kernel-trace --stats of a short bench run
 #   pmc GROUP [BENCH_ARGS...]  one rocprofv3 --pmc pass: GROUP = fetch | write | sqa | sqb
 #   full                       round evidence: tests, default bench line, trace, fetch/write, SQ a/b
@@ -58,6 +59,13 @@ case $task in
     export "$var=$v2"; run_bench "ab_$v2" --kernels $FAST "$@" || exit 1
     export "$var=$v1"; run_bench "ab_${v1}_again" --kernels $FAST "$@" || exit 1
     ;;
+  sweep)
+    var=$1; shift
+    first=$1
+    for v in "$@" "$first"; do
+      export "$var=$v"; run_bench "sweep_$v" --kernels $FAST --steps 20 --warmup 3 || exit 1
+    done
+    ;;
   trace) prof trace --kernel-trace --stats -- --steps 10 --warmup 3 $FAST "$@" ;;
   pmc)
     group=$1; shift
@@ -68,7 +76,10 @@ case $task in
       sqb) C="SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU SQ_INSTS_LDS GRBM_GUI_ACTIVE" ;;
       *) echo "unknown pmc group $group"; exit 2 ;;
     esac
-    prof "pmc_$group" --pmc $C -- --steps 3 --warmup 1 $FAST "$@"
+    # --gather outputs: no postprocess kernels on the side stream, so no other kernel runs
+    # beside a profiled dispatch (GRBM_GUI_ACTIVE and the SQ counters sample the whole GPU:
+    # a concurrent postprocess inflated round 2's conv4 row 5x)
+    prof "pmc_$group" --pmc $C -- --steps 3 --warmup 1 $FAST --gather outputs "$@"
     ;;
   full)
     run_tests || exit 1

@@ -1,6 +1,5 @@
 """Write the YOLOv2-tiny output (batch argv[2], default 16) of the default fp32 plan to argv[1]
-(.npy): the x3 variant A/B (tools/x3v_job.sh, tests/test_gpu_parity.py) checks every
-DNN_HIP_X3V arm bit for bit against arm 0."""
+(.npy), for tests/test_gpu_parity.py::test_x3_patch_variants (one process per DNN_HIP_X3V arm)."""
 import os
 import sys
 
