@@ -46,6 +46,42 @@ __device__ __forceinline__ f32x4 mfma16_bf16(bf16x8 a, bf16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
+// One 32-channel step of one 16 x 16 block, column block jb of the weight set b[piece][jb].
+// A2 (gemm_x3_acc2.h): corrections a2b0, a1b1, a0b2, a1b0, a0b1 back to back onto accc, the main
+// product a0b0 onto acc; else the round-2 form: corrections from zero, acc = (acc + a0b0) + c.
+template <bool A2, int NB>
+__device__ __forceinline__ void x3_step(f32x4& acc, f32x4& accc, const bf16x8 (&a)[3], const bf16x8 (&b)[3][NB],
+                                        int jb) {
+  if constexpr (A2) {
+    f32x4 c = accc;
+    c = mfma16_bf16(a[2], b[0][jb], c);
+    c = mfma16_bf16(a[1], b[1][jb], c);
+    c = mfma16_bf16(a[0], b[2][jb], c);
+    c = mfma16_bf16(a[1], b[0][jb], c);
+    c = mfma16_bf16(a[0], b[1][jb], c);
+    accc = c;
+    acc = mfma16_bf16(a[0], b[0][jb], acc);
+  } else {
+    f32x4 c = mfma16_bf16(a[2], b[0][jb], f32x4{0.f, 0.f, 0.f, 0.f});
+    c = mfma16_bf16(a[1], b[1][jb], c);
+    c = mfma16_bf16(a[0], b[2][jb], c);
+    c = mfma16_bf16(a[1], b[0][jb], c);
+    c = mfma16_bf16(a[0], b[1][jb], c);
+    const f32x4 m = mfma16_bf16(a[0], b[0][jb], acc);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) acc[r] = m[r] + c[r];
+  }
+}
+template <int TM, int NB>
+__device__ __forceinline__ void x3_fold(f32x4 (&acc)[TM][NB], const f32x4 (&accc)[TM][NB]) {
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < NB; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[i][j][r] = acc[i][j][r] + accc[i][j][r];
+}
+
 // POOL: a fused 2x2/s2 max pool -- GEMM rows pool-window-major (row 4 w + 2 dy + dx = cell (dy,
 // dx) of pooled pixel w; cells past an odd edge repeat cell (0, 0)), so a lane's 4 accumulator
 // registers (rows 4 q .. 4 q + 3 of its 16 x 16 block) are one window: pooled before the
@@ -344,7 +380,9 @@ conv3x3_x3_patch_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __res
 // (the order depends on (N, K) only).  NBUF = 1: one 32-channel chunk (K = 288), the patch is
 // staged once; NBUF = 2: chunk j + 1 staged during chunk j's taps.  Rows past the tile
 // (WM TM 16 > TH TW) and pixels past the frame compute on clamped rows and are not stored.
-template <int TH, int TW, int WM, int WN, int TM, int NBUF, bool POOL>
+// A2: two accumulators per output over all of K and no per-step adds (gemm_x3_acc2.h's
+// arithmetic and product order); false: the correction chain from zero + one add per step.
+template <int TH, int TW, int WM, int WN, int TM, int NBUF, bool POOL, bool A2 = true>
 __global__ void __launch_bounds__(64 * WM * WN, 512 / (64 * WM * WN))
 conv3x3_x3_tile_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __restrict__ Bt, float* __restrict__ out,
                        bf16_bits* __restrict__ out_split, int N, int K, EpiParams epi, int tilesX, int tilesY,
@@ -429,11 +467,11 @@ conv3x3_x3_tile_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __rest
         dst[p][j] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rsB, bvo, s * 3072 + p * 1024 + j * bjs, 0));
   };
 
-  f32x4 acc[TM][2];
+  f32x4 acc[TM][2], accc[TM][2];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < 2; ++j) acc[i][j] = accc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
 #pragma unroll
   for (int u = 0; u < PPT; ++u) load_piece(0, u);
@@ -482,16 +520,7 @@ conv3x3_x3_tile_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __rest
           frag(P, 0, toff_next, af[nxt]);
         const bf16x8(&bb)[3][2] = bq[tp % 3];
 #pragma unroll
-        for (int jb = 0; jb < 2; ++jb) {  // the kernel above's product order and two roundings
-          f32x4 c = mfma16_bf16(af[cur][2], bb[0][jb], f32x4{0.f, 0.f, 0.f, 0.f});
-          c = mfma16_bf16(af[cur][1], bb[1][jb], c);
-          c = mfma16_bf16(af[cur][0], bb[2][jb], c);
-          c = mfma16_bf16(af[cur][1], bb[0][jb], c);
-          c = mfma16_bf16(af[cur][0], bb[1][jb], c);
-          const f32x4 m = mfma16_bf16(af[cur][0], bb[0][jb], acc[i][jb]);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) acc[i][jb][r] = m[r] + c[r];
-        }
+        for (int jb = 0; jb < 2; ++jb) x3_step<A2>(acc[i][jb], accc[i][jb], af[cur], bb, jb);
         __builtin_amdgcn_sched_barrier(0);
       }
       if constexpr (TM & 1) {
@@ -507,6 +536,7 @@ conv3x3_x3_tile_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __rest
     }
   }
 
+  if constexpr (A2) x3_fold(acc, accc);
   // epilogue: output rows (or pooled pixels) of the tile tabulated in LDS, -1 past the frame
   int* orow = reinterpret_cast<int*>(smem);
   __syncthreads();
@@ -575,7 +605,7 @@ conv3x3_x3_tile_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __rest
 // streaming them from L2 (73 B per MFMA at 2 waves per tile).  One chunk: no double buffer;
 // two workgroups per CU overlap each other's staging.  Same product order per step as the
 // kernels above; 32 columns (WN = 1), WM waves of TM 16-row blocks.
-template <int TH, int TW, int WM, int TM, bool POOL>
+template <int TH, int TW, int WM, int TM, bool POOL, bool A2 = true>  // A2: as the tile kernel
 __global__ void __launch_bounds__(64 * WM, 2)  // (waves per SIMD) two: <= 256 registers
 conv3x3_x3_c16_kernel(const float* __restrict__ in, const bf16_bits* __restrict__ Bt, float* __restrict__ out,
                       bf16_bits* __restrict__ out_split, int N, EpiParams epi, int tilesX, int tilesY, X3Geom g,
@@ -665,11 +695,11 @@ conv3x3_x3_c16_kernel(const float* __restrict__ in, const bf16_bits* __restrict_
     prow[i] = ((ly + 1) * PW2 + lx + 1) * PB + 16 * (fq & 1);
   }
 
-  f32x4 acc[TM][2];
+  f32x4 acc[TM][2], accc[TM][2];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < 2; ++j) acc[i][j] = accc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   __syncthreads();
 
   auto toff = [&](int s) {  // this lane's tap offset (bytes) in step s
@@ -707,20 +737,12 @@ conv3x3_x3_c16_kernel(const float* __restrict__ in, const bf16_bits* __restrict_
       if (i == 0 && s + 1 < NS) bfrag(s + 1, bq[(s + 1) & 1]);  // next step's weights
       const bf16x8(&bb)[3][2] = bq[s & 1];
 #pragma unroll
-      for (int jb = 0; jb < 2; ++jb) {
-        f32x4 c = mfma16_bf16(af[cur][2], bb[0][jb], f32x4{0.f, 0.f, 0.f, 0.f});
-        c = mfma16_bf16(af[cur][1], bb[1][jb], c);
-        c = mfma16_bf16(af[cur][0], bb[2][jb], c);
-        c = mfma16_bf16(af[cur][1], bb[0][jb], c);
-        c = mfma16_bf16(af[cur][0], bb[1][jb], c);
-        const f32x4 m = mfma16_bf16(af[cur][0], bb[0][jb], acc[i][jb]);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) acc[i][jb][r] = m[r] + c[r];
-      }
+      for (int jb = 0; jb < 2; ++jb) x3_step<A2>(acc[i][jb], accc[i][jb], af[cur], bb, jb);
       __builtin_amdgcn_sched_barrier(0);
     }
   }
 
+  if constexpr (A2) x3_fold(acc, accc);
   // epilogue (as conv3x3_x3_tile_kernel)
   int* orow = reinterpret_cast<int*>(smem);
   __syncthreads();

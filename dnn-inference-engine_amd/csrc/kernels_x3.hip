@@ -319,6 +319,16 @@ int launch_pack_weights_x3(const float* w, bf16_bits* out, int K, int N, int Npa
 // ---- the conv
 constexpr int X3_BM = 176, X3_NPR = 320;
 
+// the narrow x3 kernels (16-channel and tile kernels) with two accumulators per output and no
+// per-step adds (gemm_x3_patch.h x3_step); DNN_HIP_X3A2=0: the round-2 form
+static bool x3_narrow_a2() {
+  static const bool on = [] {
+    const char* e = getenv("DNN_HIP_X3A2");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 // DNN_HIP_X3=0 keeps these layers on the fp32 MFMA (implicit GEMM)
 static bool x3_enabled() {
   const char* e = getenv("DNN_HIP_X3");
@@ -426,12 +436,18 @@ int launch_conv_x3(const bf16_bits* in_split, const bf16_bits* Bt, float* out, b
     const X3Geom xg{H, W, C, out_split ? 1 : 0, 1, PH, PW};
     const float* in32p = reinterpret_cast<const float*>(in_split);
     (void)b16;
-    if (pool)
-      hipLaunchKernelGGL((conv3x3_x3_c16_kernel<16, 26, 4, 7, true>), dim3((unsigned)blocks), dim3(256), 0, stream, in32p,
-                         Bt, out, out_split, N, epi, tilesX, tilesY, xg, (unsigned)in32);
+#define X3C(POOL_, A2_)                                                                                      \
+  hipLaunchKernelGGL((conv3x3_x3_c16_kernel<16, 26, 4, 7, POOL_, A2_>), dim3((unsigned)blocks), dim3(256), 0, stream, \
+                     in32p, Bt, out, out_split, N, epi, tilesX, tilesY, xg, (unsigned)in32)
+    if (pool && x3_narrow_a2())
+      X3C(true, true);
+    else if (pool)
+      X3C(true, false);
+    else if (x3_narrow_a2())
+      X3C(false, true);
     else
-      hipLaunchKernelGGL((conv3x3_x3_c16_kernel<16, 26, 4, 7, false>), dim3((unsigned)blocks), dim3(256), 0, stream,
-                         in32p, Bt, out, out_split, N, epi, tilesX, tilesY, xg, (unsigned)in32);
+      X3C(false, false);
+#undef X3C
     return check_x3("conv_x3 (c16)");
   }
   if (kind > 0) {
@@ -453,19 +469,29 @@ int launch_conv_x3(const bf16_bits* in_split, const bf16_bits* Bt, float* out, b
       return -2;
     }
     const X3Geom xg{H, W, C, out_split ? 1 : 0, 1, PH, PW};
-#define X3T(TH_, TW_, WM, WN, NBUF, POOL)                                                                        \
-  hipLaunchKernelGGL((conv3x3_x3_tile_kernel<TH_, TW_, WM, WN, X3T_TM, NBUF, POOL>), dim3((unsigned)blocks),      \
+#define X3T_(TH_, TW_, WM, WN, NBUF, POOL, A2_)                                                                  \
+  hipLaunchKernelGGL((conv3x3_x3_tile_kernel<TH_, TW_, WM, WN, X3T_TM, NBUF, POOL, A2_>), dim3((unsigned)blocks),   \
                      dim3(64 * WM * WN), 0, stream, in_split, Bt, out, out_split, N, K, epi, tilesX, tilesY, tilesN, \
                      xg, (unsigned)in_bytes, (unsigned)b_bytes)
+#define X3T(TH_, TW_, WM, WN, NBUF, POOL) \
+  do {                                    \
+    if (x3_narrow_a2())                   \
+      X3T_(TH_, TW_, WM, WN, NBUF, POOL, true); \
+    else                                  \
+      X3T_(TH_, TW_, WM, WN, NBUF, POOL, false); \
+  } while (0)
+    // (kind 2 keeps the round-2 form: its 3-step weight ring and staging registers leave no
+    // room for the second accumulator set)
     if (kind == 2 && pool)
-      X3T(4, 26, 1, 4, 2, true);
+      X3T_(4, 26, 1, 4, 2, true, false);
     else if (kind == 2)
-      X3T(4, 26, 1, 4, 2, false);
+      X3T_(4, 26, 1, 4, 2, false, false);
     else if (pool)
       X3T(8, 26, 2, 2, 1, true);
     else
       X3T(8, 26, 2, 2, 1, false);
 #undef X3T
+#undef X3T_
     return check_x3("conv_x3 (tile)");
   }
   if (M % per_img != 0 || K != 9 * C || C % 32 != 0 || N % 256 != 0 || Npad != N || (pool && splits != 1) ||
