@@ -240,6 +240,13 @@ int launch_conv_x3(const unsigned short* in_split, const unsigned short* Bt, flo
 bool conv_x3_pool_supported(int OC, int C, int H, int W);  // an x3 conv of this size can fuse a 2x2/s2 pool
 // x3 workgroups of a layer (batch-1 latency plans take x3 only where they fill half the chip)
 long long x3_tiles(long long batch, int OH, int OW, int OC, int C, int K);
+// small-M x3 conv of the latency plans (gemm_x3_lat.h): raw partials [splits][M][N] of
+// x3_lat_splits(N, K) K slices into `part`, summed with the epilogue by launch_x3_combine
+bool conv_x3_lat_supported(long long batch, int C, int OC, int H, int W, int OH, int OW, int kh, int kw, int sh,
+                           int sw, int pt, int pl);
+int x3_lat_splits(int N, int K);
+int launch_conv_x3_lat(const unsigned short* in_split, const unsigned short* Bt, float* part, long long M, int N,
+                       int Npad, int K, int H, int W, int C, int splits, hipStream_t stream);
 int launch_x3_combine(const float* part, int splits, long long slab, const EpiParams& epi, const PoolGeom& g,
                       float* out, unsigned short* out_split, hipStream_t s);
 int patch16_pack_order();  // launch_pack_weights order of the patch kernel's MFMA shape (3 or 4)

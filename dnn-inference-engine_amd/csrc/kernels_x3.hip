@@ -4,6 +4,7 @@
 #include "dnn_common.h"
 #include "gemm_x3_patch.h"
 #include "gemm_x3_acc2.h"
+#include "gemm_x3_lat.h"
 
 #include <cfloat>
 #include <cstdlib>
@@ -88,143 +89,144 @@ int launch_maxpool_x3(const float* in, bf16_bits* out, const PoolGeom& g, hipStr
 // summed in split order ((p0 + p1) + p2 ...), the conv's fp32 epilogue, then an optional max
 // pool in the reference's order (window cells in row order, `m >= x ? m : x`, pad cells
 // skipped; kh = kw = 1, stride 1: no pool), into fp32 NHWC or the split planes of the next x3
-// layer (out_split).  8 channels per thread, epilogue parameters loaded once per thread.
-template <int KH, int KW, int S>  // KH = 0: any window (runtime loops); S = 0: any split count
+// layer (out_split).  CPT channels per thread (8, or 4 for the many-slice combines of the
+// latency plans: twice the threads, and every slice's load in flight at once), epilogue
+// parameters loaded once per thread.
+template <int KH, int KW, int S, int CPT = 8>  // KH = 0: any window (runtime loops); S = 0: any split count
 __global__ void x3_combine_kernel(const float* __restrict__ part, int splits, long long slab, EpiParams epi,
                                   PoolGeom g, float* __restrict__ out, bf16_bits* __restrict__ out_split,
                                   long long total) {
-  const int cq = g.C / 8;
+  static_assert(CPT == 4 || CPT == 8, "channels per thread");
+  constexpr int NV = CPT / 4;
+  const int cq = g.C / CPT;
   // blocks in consecutive pixel order per XCD (xcd_tile): a window's other rows are read by
   // blocks of the same XCD, from its L2, instead of by every XCD from HBM (stride-1 pools
   // read each partial 4 times)
   const long long i = (long long)xcd_tile(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
-  if (i < total) {
-    const int c = (int)(i % cq) * 8;
-    long long t = i / cq;
-    const int ox = (int)(t % g.OW);
-    t /= g.OW;
-    const int oy = (int)(t % g.OH);
-    const int b = (int)(t / g.OH);
-    // epilogue parameters of the 8 channels: two 16-B loads per array (c % 8 == 0; the plan's
-    // arrays hold Npad >= C floats), not 32 scalar loads
-    float pb[8], pm[8], ps[8], pg[8];
-    auto ld8 = [&](const float* a, float (&d)[8], float dflt, bool on) {
-      if (on) {
-        const float4 x0 = *reinterpret_cast<const float4*>(a + c), x1 = *reinterpret_cast<const float4*>(a + c + 4);
-        d[0] = x0.x, d[1] = x0.y, d[2] = x0.z, d[3] = x0.w, d[4] = x1.x, d[5] = x1.y, d[6] = x1.z, d[7] = x1.w;
-      } else {
+  if (i >= total) return;
+  const int c = (int)(i % cq) * CPT;
+  long long t = i / cq;
+  const int ox = (int)(t % g.OW);
+  t /= g.OW;
+  const int oy = (int)(t % g.OH);
+  const int b = (int)(t / g.OH);
+  auto ldv = [&](const float* a, float* d) {  // CPT floats, 16-B loads (c % CPT == 0)
 #pragma unroll
-        for (int e = 0; e < 8; ++e) d[e] = dflt;
-      }
-    };
-    ld8(epi.bias, pb, 0.f, (epi.flags & EPI_BIAS) != 0);
-    ld8(epi.mean, pm, 0.f, (epi.flags & (EPI_BN | EPI_BN_AB)) != 0);
-    ld8(epi.sq, ps, 1.f, (epi.flags & (EPI_BN | EPI_BN_AB)) != 0);
-    ld8(epi.gamma, pg, 1.f, (epi.flags & EPI_BN) != 0);
-    float hi[8], lo[8];
-    if constexpr (KH > 0) {
-      // fixed window and split count: every load issued up front.  Window cells past the frame
-      // are clamped into it: a clamped row / column is the window's first or last in-frame
-      // one, so the cell repeats a window member and the max is unchanged
-      float v[KH * KW][8];
+    for (int v = 0; v < NV; ++v) {
+      const float4 x = *reinterpret_cast<const float4*>(a + 4 * v);
+      d[4 * v] = x.x, d[4 * v + 1] = x.y, d[4 * v + 2] = x.z, d[4 * v + 3] = x.w;
+    }
+  };
+  // epilogue parameters of the CPT channels (the plan's arrays hold Npad >= C floats)
+  float pb[CPT], pm[CPT], ps[CPT], pg[CPT];
+  auto ldp = [&](const float* a, float (&d)[CPT], float dflt, bool on) {
+    if (on) {
+      ldv(a + c, d);
+    } else {
 #pragma unroll
-      for (int dy = 0; dy < KH; ++dy)
+      for (int e = 0; e < CPT; ++e) d[e] = dflt;
+    }
+  };
+  ldp(epi.bias, pb, 0.f, (epi.flags & EPI_BIAS) != 0);
+  ldp(epi.mean, pm, 0.f, (epi.flags & (EPI_BN | EPI_BN_AB)) != 0);
+  ldp(epi.sq, ps, 1.f, (epi.flags & (EPI_BN | EPI_BN_AB)) != 0);
+  ldp(epi.gamma, pg, 1.f, (epi.flags & EPI_BN) != 0);
+  float hi[CPT], lo[CPT];
+  if constexpr (KH > 0) {
+    // fixed window: every load issued up front.  Window cells past the frame are clamped into
+    // it: a clamped row / column is the window's first or last in-frame one, so the cell
+    // repeats a window member and the max is unchanged
+    float v[KH * KW][CPT];
 #pragma unroll
-        for (int dx = 0; dx < KW; ++dx) {
-          int iy = oy * g.sh - g.pt + dy, ix = ox * g.sw - g.pl + dx;
-          iy = iy < 0 ? 0 : iy >= g.H ? g.H - 1 : iy;
-          ix = ix < 0 ? 0 : ix >= g.W ? g.W - 1 : ix;
-          const float* src = part + (((size_t)b * g.H + iy) * g.W + ix) * g.C + c;
-          float* w = v[dy * KW + dx];
-          if constexpr (S > 0) {
-            float4 x[S][2];
+    for (int dy = 0; dy < KH; ++dy)
 #pragma unroll
-            for (int sp = 0; sp < S; ++sp) {
-              x[sp][0] = *reinterpret_cast<const float4*>(src + sp * slab);
-              x[sp][1] = *reinterpret_cast<const float4*>(src + sp * slab + 4);
-            }
-            w[0] = x[0][0].x, w[1] = x[0][0].y, w[2] = x[0][0].z, w[3] = x[0][0].w;
-            w[4] = x[0][1].x, w[5] = x[0][1].y, w[6] = x[0][1].z, w[7] = x[0][1].w;
+      for (int dx = 0; dx < KW; ++dx) {
+        int iy = oy * g.sh - g.pt + dy, ix = ox * g.sw - g.pl + dx;
+        iy = iy < 0 ? 0 : iy >= g.H ? g.H - 1 : iy;
+        ix = ix < 0 ? 0 : ix >= g.W ? g.W - 1 : ix;
+        const float* src = part + (((size_t)b * g.H + iy) * g.W + ix) * g.C + c;
+        float* w = v[dy * KW + dx];
+        if constexpr (S > 0) {
+          float x[S][CPT];
 #pragma unroll
-            for (int sp = 1; sp < S; ++sp) {  // split order ((p0 + p1) + p2 ...)
-              w[0] += x[sp][0].x, w[1] += x[sp][0].y, w[2] += x[sp][0].z, w[3] += x[sp][0].w;
-              w[4] += x[sp][1].x, w[5] += x[sp][1].y, w[6] += x[sp][1].z, w[7] += x[sp][1].w;
-            }
-          } else {  // many slices (latency plans): loads run ahead of the ordered sum
-            const float4 x0 = *reinterpret_cast<const float4*>(src), x1 = *reinterpret_cast<const float4*>(src + 4);
-            w[0] = x0.x, w[1] = x0.y, w[2] = x0.z, w[3] = x0.w, w[4] = x1.x, w[5] = x1.y, w[6] = x1.z, w[7] = x1.w;
-#pragma unroll 8
-            for (int sp = 1; sp < splits; ++sp) {
-              const float4 y0 = *reinterpret_cast<const float4*>(src + sp * slab);
-              const float4 y1 = *reinterpret_cast<const float4*>(src + sp * slab + 4);
-              w[0] += y0.x, w[1] += y0.y, w[2] += y0.z, w[3] += y0.w, w[4] += y1.x, w[5] += y1.y, w[6] += y1.z,
-                  w[7] += y1.w;
-            }
+          for (int sp = 0; sp < S; ++sp) ldv(src + sp * slab, x[sp]);
+#pragma unroll
+          for (int e = 0; e < CPT; ++e) {
+            w[e] = x[0][e];
+#pragma unroll
+            for (int sp = 1; sp < S; ++sp) w[e] += x[sp][e];  // split order ((p0 + p1) + p2 ...)
+          }
+        } else {  // many slices (latency plans): loads run ahead of the ordered sum
+          ldv(src, w);
+#pragma unroll 16
+          for (int sp = 1; sp < splits; ++sp) {
+            float y[CPT];
+            ldv(src + sp * slab, y);
+#pragma unroll
+            for (int e = 0; e < CPT; ++e) w[e] += y[e];
           }
         }
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        hi[e] = lo[e] = v[0][e];
-#pragma unroll
-        for (int q = 1; q < KH * KW; ++q) {
-          hi[e] = __builtin_fmaxf(hi[e], v[q][e]);
-          lo[e] = __builtin_fminf(lo[e], v[q][e]);
-        }
       }
-    } else {
+#pragma unroll
+    for (int e = 0; e < CPT; ++e) {
+      hi[e] = lo[e] = v[0][e];
+#pragma unroll
+      for (int q = 1; q < KH * KW; ++q) {
+        hi[e] = __builtin_fmaxf(hi[e], v[q][e]);
+        lo[e] = __builtin_fminf(lo[e], v[q][e]);
+      }
+    }
+  } else {
     bool first = true;
     for (int dy = 0; dy < g.kh; ++dy)
       for (int dx = 0; dx < g.kw; ++dx) {
         const int iy = oy * g.sh - g.pt + dy, ix = ox * g.sw - g.pl + dx;
         if ((unsigned)iy >= (unsigned)g.H || (unsigned)ix >= (unsigned)g.W) continue;  // -FLT_MAX pad cell
         const float* src = part + (((size_t)b * g.H + iy) * g.W + ix) * g.C + c;
-        float v[8];
-        {
-          const float4 x0 = *reinterpret_cast<const float4*>(src), x1 = *reinterpret_cast<const float4*>(src + 4);
-          v[0] = x0.x, v[1] = x0.y, v[2] = x0.z, v[3] = x0.w, v[4] = x1.x, v[5] = x1.y, v[6] = x1.z, v[7] = x1.w;
-        }
+        float v[CPT];
+        ldv(src, v);
         for (int sp = 1; sp < splits; ++sp) {
-          const float* q = src + sp * slab;
-          const float4 x0 = *reinterpret_cast<const float4*>(q), x1 = *reinterpret_cast<const float4*>(q + 4);
-          v[0] += x0.x, v[1] += x0.y, v[2] += x0.z, v[3] += x0.w, v[4] += x1.x, v[5] += x1.y, v[6] += x1.z,
-              v[7] += x1.w;
+          float y[CPT];
+          ldv(src + sp * slab, y);
+#pragma unroll
+          for (int e = 0; e < CPT; ++e) v[e] += y[e];
         }
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
+        for (int e = 0; e < CPT; ++e) {
           hi[e] = first ? v[e] : __builtin_fmaxf(hi[e], v[e]);
           lo[e] = first ? v[e] : __builtin_fminf(lo[e], v[e]);
         }
         first = false;
       }
-    }
-    // pool before the epilogue, as the GEMMs' fused pools (pool_then_epilogue):
-    // the epilogue is a chain of IEEE-monotone steps, so max f(v_i) = f(max v_i) (min for a
-    // decreasing channel) -- one exact-division epilogue per output instead of one per cell
-    float m[8];
+  }
+  // pool before the epilogue, as the GEMMs' fused pools (pool_then_epilogue):
+  // the epilogue is a chain of IEEE-monotone steps, so max f(v_i) = f(max v_i) (min for a
+  // decreasing channel) -- one exact-division epilogue per output instead of one per cell
+  float m[CPT];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const bool dec = ((epi.flags & EPI_BN) && pg[e] < 0.f) || ((epi.flags & EPI_BN_AB) && pm[e] < 0.f);
-      m[e] = apply_epilogue(dec ? lo[e] : hi[e], pb[e], pm[e], ps[e], pg[e], epi.flags);
-    }
-    if (out_split) {
-      typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
-      u16x8 s0, s1, s2;
+  for (int e = 0; e < CPT; ++e) {
+    const bool dec = ((epi.flags & EPI_BN) && pg[e] < 0.f) || ((epi.flags & EPI_BN_AB) && pm[e] < 0.f);
+    m[e] = apply_epilogue(dec ? lo[e] : hi[e], pb[e], pm[e], ps[e], pg[e], epi.flags);
+  }
+  if (out_split) {
+    typedef unsigned short u16v __attribute__((ext_vector_type(CPT)));
+    u16v s0, s1, s2;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        unsigned short a, b2, c2;
-        split3(m[e], a, b2, c2);
-        s0[e] = a, s1[e] = b2, s2[e] = c2;
-      }
-      const size_t row = ((size_t)b * (g.OH + 2) + oy + 1) * (g.OW + 2) + ox + 1;
-      bf16_bits* d = out_split + row * (3 * (size_t)g.C) + (c >> 5) * 96 + (c & 31);
-      *reinterpret_cast<u16x8*>(d) = s0;
-      *reinterpret_cast<u16x8*>(d + 32) = s1;
-      *reinterpret_cast<u16x8*>(d + 64) = s2;
-    } else {
-      float* d = out + (((size_t)b * g.OH + oy) * g.OW + ox) * g.C + c;
-      *reinterpret_cast<float4*>(d) = make_float4(m[0], m[1], m[2], m[3]);
-      *reinterpret_cast<float4*>(d + 4) = make_float4(m[4], m[5], m[6], m[7]);
+    for (int e = 0; e < CPT; ++e) {
+      unsigned short a, b2, c2;
+      split3(m[e], a, b2, c2);
+      s0[e] = a, s1[e] = b2, s2[e] = c2;
     }
+    const size_t row = ((size_t)b * (g.OH + 2) + oy + 1) * (g.OW + 2) + ox + 1;
+    bf16_bits* d = out_split + row * (3 * (size_t)g.C) + (c >> 5) * 96 + (c & 31);
+    *reinterpret_cast<u16v*>(d) = s0;
+    *reinterpret_cast<u16v*>(d + 32) = s1;
+    *reinterpret_cast<u16v*>(d + 64) = s2;
+  } else {
+    float* d = out + (((size_t)b * g.OH + oy) * g.OW + ox) * g.C + c;
+#pragma unroll
+    for (int v = 0; v < NV; ++v)
+      *reinterpret_cast<float4*>(d + 4 * v) = make_float4(m[4 * v], m[4 * v + 1], m[4 * v + 2], m[4 * v + 3]);
   }
 }
 
@@ -235,27 +237,34 @@ int launch_x3_combine(const float* part, int splits, long long slab, const EpiPa
     set_error("x3_combine: unsupported C=%d splits=%d", g.C, splits);
     return -2;
   }
-  const long long total = (long long)g.B * g.OH * g.OW * (g.C / 8);
+  const int win = g.kh == 2 && g.kw == 2 ? 2 : g.kh == 1 && g.kw == 1 ? 1 : 0;
+  // many slices (> 2: latency plans): 4 channels per thread (DNN_HIP_X3C_CPT=8: 8)
+  const char* ce = getenv("DNN_HIP_X3C_CPT");
+  const int cpt = splits > 2 && win > 0 && !(ce && atoi(ce) == 8) ? 4 : 8;
+  const long long total = (long long)g.B * g.OH * g.OW * (g.C / cpt);
   if ((total + 255) / 256 > 0x7fffffffLL) {
     set_error("x3_combine: %lld outputs", total);
     return -2;
   }
   const dim3 grid((unsigned)((total + 255) / 256));
-#define X3C(KH, KW, S) \
-  hipLaunchKernelGGL((x3_combine_kernel<KH, KW, S>), grid, dim3(256), 0, s, part, splits, slab, epi, g, out, out_split, total)
-  const int win = g.kh == 2 && g.kw == 2 ? 2 : g.kh == 1 && g.kw == 1 ? 1 : 0;
+#define X3C(KH, KW, S, CPT) \
+  hipLaunchKernelGGL((x3_combine_kernel<KH, KW, S, CPT>), grid, dim3(256), 0, s, part, splits, slab, epi, g, out, out_split, total)
   if (win == 2 && splits == 2)
-    X3C(2, 2, 2);
+    X3C(2, 2, 2, 8);
   else if (win == 2 && splits == 1)
-    X3C(2, 2, 1);
+    X3C(2, 2, 1, 8);
   else if (win == 1 && splits == 2)
-    X3C(1, 1, 2);
+    X3C(1, 1, 2, 8);
+  else if (win == 1 && cpt == 4)
+    X3C(1, 1, 0, 4);
   else if (win == 1)
-    X3C(1, 1, 0);
+    X3C(1, 1, 0, 8);
+  else if (win == 2 && cpt == 4)
+    X3C(2, 2, 0, 4);
   else if (win == 2)
-    X3C(2, 2, 0);
+    X3C(2, 2, 0, 8);
   else
-    X3C(0, 0, 0);
+    X3C(0, 0, 0, 8);
 #undef X3C
   return check_x3("x3_combine");
 }
@@ -538,6 +547,73 @@ int launch_conv_x3(const bf16_bits* in_split, const bf16_bits* Bt, float* out, b
 #undef X3P
 #undef X3A
   return check_x3("conv_x3");
+}
+
+// ---- small-M x3 conv (latency plans, gemm_x3_lat.h): 64-column tiles (NCP = 2), one or two
+// chunks per workgroup, chosen so that a frame's layer is ~256 workgroups: two chunks when the
+// one-chunk grid would be >= 512 (conv7: 16 N tiles x 32 chunks), else one (conv6: 16 x 16).
+// DNN_HIP_X3L_CPW=1|2 forces it.
+static int x3_lat_cpw(int N, int K) {
+  const char* e = getenv("DNN_HIP_X3L_CPW");  // (read per call: plans and tests set it per plan)
+  const int force = e ? atoi(e) : 0;
+  const int chunks = K / 288;
+  if (force == 1 || force == 2) return chunks % force == 0 ? force : 1;
+  return chunks % 2 == 0 && (long long)(N / 64) * chunks >= 512 ? 2 : 1;
+}
+
+int x3_lat_splits(int N, int K) { return (K / 288) / x3_lat_cpw(N, K); }
+
+constexpr int X3L_NPR_SMALL = 240;  // one 13x13 frame's tile spans 225 padded rows
+
+bool conv_x3_lat_supported(long long batch, int C, int OC, int H, int W, int OH, int OW, int kh, int kw, int sh,
+                           int sw, int pt, int pl) {
+  if (!(kh == 3 && kw == 3 && sh == 1 && sw == 1 && pt == 1 && pl == 1 && OH == H && OW == W && C % 32 == 0 &&
+        OC % 64 == 0 && x3_enabled() && !getenv_flag_off("DNN_HIP_X3_LAT")))
+    return false;
+  const long long M = batch * H * W;
+  // only where one-chunk slices fill half the chip (conv6 / conv7 of a frame: 256 / 512): with
+  // fewer workgroups the launch, the patch staging and the separate combine (~5-7 us each at
+  // batch 1) outweigh the x3 arithmetic (measured: conv3-conv5 at 64 workgroups, with their
+  // pools in the combine, no faster than the fp32 MFMA's in-GEMM split-K)
+  const long long wgs = (M + X3_BM - 1) / X3_BM * (OC / 64) * (C / 32);
+  const char* e = getenv("DNN_HIP_X3_LAT_MINWG");  // (experiments)
+  if (wgs < (e ? atoll(e) : 128)) return false;
+  return M <= 0x7fffffffLL && x3_span(M, H, W) <= X3_NPR;
+}
+
+int launch_conv_x3_lat(const bf16_bits* in_split, const bf16_bits* Bt, float* part, long long M, int N, int Npad,
+                       int K, int H, int W, int C, int splits, hipStream_t stream) {
+  if (M == 0 || N == 0) return 0;
+  const long long per_img = (long long)H * W, nimg = M / per_img;
+  const long long in_bytes = (long long)x3_act_bytes(nimg, H, W, C);
+  const long long b_bytes = (long long)(Npad / 16) * (K / 32) * 3072;
+  const int cpw = x3_lat_cpw(N, K);
+  const long long span = M <= 0x7fffffffLL ? x3_span(M, H, W) : 1LL << 40;
+  if (M % per_img != 0 || K != 9 * C || C % 32 != 0 || N % 64 != 0 || Npad != N || splits != (K / 288) / cpw ||
+      in_bytes >= 0x80000000LL || b_bytes >= 0x80000000LL || span > X3_NPR || part == nullptr) {
+    set_error("conv_x3_lat: unsupported shape M=%lld N=%d K=%d %dx%dx%d splits=%d", M, N, K, H, W, C, splits);
+    return -2;
+  }
+  const int tilesM = (int)((M + X3_BM - 1) / X3_BM), tilesN = N / 64;
+  const long long blocks = (long long)tilesM * tilesN * splits;
+  if (blocks > 0x7fffffffLL) {
+    set_error("conv_x3_lat: grid too large");
+    return -2;
+  }
+  const X3Geom xg{H, W, C, 2, splits, 0, 0, 0};
+#define X3L(CPW_, NPR_)                                                                                       \
+  hipLaunchKernelGGL((conv3x3_x3_lat_kernel<2, CPW_, NPR_>), dim3((unsigned)blocks), dim3(512), 0, stream, in_split, \
+                     Bt, part, (int)M, N, K, tilesM, xg, (unsigned)in_bytes, (unsigned)b_bytes)
+  if (cpw == 2 && span <= X3L_NPR_SMALL)
+    X3L(2, X3L_NPR_SMALL);
+  else if (cpw == 2)
+    X3L(2, X3_NPR);
+  else if (span <= X3L_NPR_SMALL)
+    X3L(1, X3L_NPR_SMALL);
+  else
+    X3L(1, X3_NPR);
+#undef X3L
+  return check_x3("conv_x3_lat");
 }
 
 }  // namespace dnnhip

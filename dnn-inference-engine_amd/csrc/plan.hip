@@ -102,6 +102,7 @@ struct PlanLayer {
   int K = 0, Kpad = 0, Npad = 0, cfg = 0, epi_flags = 0;
   int splits = 1;  // split-K partial count (> 1: GEMM writes partials, a reduce kernel finishes)
   bool pool = false;  // a 2x2/stride-2 max pool fused into this conv
+  bool x3lat = false;  // MODE_X3 on the small-M kernel (latency plans: launch_conv_x3_lat)
   bool out_padded = false;  // output written zero-bordered (the next layer is MODE_PATCH16 / MODE_X3;
                             // fp32 plans: as x3 split planes)
   size_t pad_off = 0;       // its zero-bordered output region: float offset inside the pad area
@@ -301,7 +302,7 @@ static void set_cfg(dnn_plan* p, PlanLayer& L) {
     L.cfg = 0;
     L.Kpad = L.C == 16 ? 160 : L.K;  // (16 channels: 5 steps of two taps)
     L.Npad = L.OC;  // (a multiple of 256, or of 32 / 64 / 128 for the tile kernels)
-    L.splits = x3_splits(L.OC, L.K);
+    L.splits = L.x3lat ? x3_lat_splits(L.OC, L.K) : x3_splits(L.OC, L.K);
     return;
   }
   if (p->fp16 && L.mode == MODE_PATCH16) {  // one config: 192x256 tiles, no split
@@ -422,13 +423,24 @@ int dnn_plan_add_conv(dnn_plan* p, int kh, int kw, int od, int stride_h, int str
     L.mode = MODE_GEMM;  // may become MODE_DIRECT when a 2x2/s2 pool follows (conv0)
   // fp32 3x3 wide layers fed by a separate pool or another such conv: the x3 conv (its producer
   // writes the split planes).  Batch plans choose it by the layer alone, so a batch-1 plan and a
-  // batch-64 plan run the same arithmetic; latency plans (with the in-GEMM split-K combine) only
-  // where its tiles fill half the chip: at batch 1 a 176 x 256 tile's one-chunk K slice alone
-  // takes ~26 us (measured: conv6/conv7 as 16 / 32 x3 slices 0.053 / 0.056 ms with their
-  // combines, against 0.034 / 0.050 on the fp32 MFMA with split-K 16)
-  if (!p->fp16 && L.mode == MODE_IMPLICIT && !p->layers.empty() &&
-      conv_x3_supported(L.C, od, L.H, L.W, L.OH, L.OW, kh, kw, stride_h, stride_w, L.pt, L.pl) &&
-      (!p->latency || !fused_splitk(p) || x3_tiles(p->batch, L.OH, L.OW, od, L.C, L.K) >= 128)) {
+  // batch-64 plan run the same arithmetic.  Latency plans (with the in-GEMM split-K combine) take
+  // the batch kernel only where its tiles fill half the chip (at batch 1 a 176 x 256 tile's
+  // one-chunk K slice alone takes ~26 us), elsewhere the small-M x3 kernel (gemm_x3_lat.h: 64
+  // columns x one or two chunks per workgroup, 8 waves splitting rows / columns / chunks;
+  // conv6 / conv7 of a one-frame plan) when it makes at least two K slices
+  bool x3_cand = false, x3_lat = false;
+  if (!p->fp16 && L.mode == MODE_IMPLICIT && !p->layers.empty()) {
+    const bool batch_ok = conv_x3_supported(L.C, od, L.H, L.W, L.OH, L.OW, kh, kw, stride_h, stride_w, L.pt, L.pl);
+    if (p->latency && fused_splitk(p) && !(batch_ok && x3_tiles(p->batch, L.OH, L.OW, od, L.C, L.K) >= 128)) {
+      x3_lat = conv_x3_lat_supported(p->batch, L.C, od, L.H, L.W, L.OH, L.OW, kh, kw, stride_h, stride_w, L.pt,
+                                     L.pl) &&
+               x3_lat_splits(od, L.K) >= 2;
+      x3_cand = x3_lat;
+    } else {
+      x3_cand = batch_ok;
+    }
+  }
+  if (x3_cand) {
     // producers that can write the split planes: a separate pool, another x3 conv, a pool-fused
     // implicit GEMM without split-K (its epilogue splits, EPI_OUT_X3) or the pool-fused patch
     // conv (conv1)
@@ -439,6 +451,7 @@ int dnn_plan_add_conv(dnn_plan* p, int kh, int kw, int od, int stride_h, int str
         (prev.type == 0 && prev.mode == MODE_IMPLICIT && prev.pool && prev.splits == 1) ||
         (prev.type == 0 && prev.mode == MODE_PATCH && prev.pool)) {
       L.mode = MODE_X3;
+      L.x3lat = x3_lat;
       prev.out_padded = true;
     }
   }
@@ -829,9 +842,12 @@ int dnn_plan_run(dnn_plan* p, int n, const float* d_in, float* d_out, void* stre
         }
         case MODE_X3:
           if (L.splits > 1) {  // raw partials into the slab; the next pool or a combine kernel finishes
-            rc = launch_conv_x3(reinterpret_cast<const unsigned short*>(cur),
-                                reinterpret_cast<const unsigned short*>(wt), slab, nullptr, Mc, L.OC, L.Npad, L.K, L.H,
-                                L.W, L.C, epi, s, L.splits);
+            rc = L.x3lat ? launch_conv_x3_lat(reinterpret_cast<const unsigned short*>(cur),
+                                              reinterpret_cast<const unsigned short*>(wt), slab, Mc, L.OC, L.Npad, L.K,
+                                              L.H, L.W, L.C, L.splits, s)
+                         : launch_conv_x3(reinterpret_cast<const unsigned short*>(cur),
+                                          reinterpret_cast<const unsigned short*>(wt), slab, nullptr, Mc, L.OC, L.Npad,
+                                          L.K, L.H, L.W, L.C, epi, s, L.splits);
             if (!rc && !(i + 1 < nl && p->layers[i + 1].type == 1)) {
               PoolGeom id{n, L.OH, L.OW, L.OC, L.OH, L.OW, 1, 1, 1, 1, 0, 0, 0};
               if ((rc = record(p, ++k, s))) return rc;
@@ -951,7 +967,7 @@ int dnn_plan_describe(const dnn_plan* p, char* buf, int buf_len) {
       char sk[32] = "";
       if (L.splits > 1) snprintf(sk, sizeof(sk), " splitK=%d", L.splits);
       snprintf(line, sizeof(line), "conv %dx%dx%d -> %dx%dx%d k%dx%d s%d mode=%s cfg=%d K=%d Kpad=%d%s%s%s%s%s\n", L.H,
-               L.W, L.C, L.out_h(), L.out_w(), L.OC, L.kh, L.kw, L.sh, kModeName[L.mode], L.cfg, L.K, L.Kpad,
+               L.W, L.C, L.out_h(), L.out_w(), L.OC, L.kh, L.kw, L.sh, L.x3lat ? "x3_lat" : kModeName[L.mode], L.cfg, L.K, L.Kpad,
                L.pool ? " +pool2x2s2" : "", sk,
                L.splits > 1 ? (L.mode == MODE_X3 ? " x3-combine" : fused_splitk(p) ? " combine" : "") : "",
                p->fp16 ? " fp16" : "", p->latency ? " latency" : "");

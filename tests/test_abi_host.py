@@ -329,9 +329,13 @@ def test_latency_plan_layout():
     assert all(l.endswith(" latency") for l in lat if l.startswith("conv"))
     conv = [l for l in lat if l.startswith("conv")]
     assert "mode=direct" in conv[0] and "mode=patch" in conv[1]
-    for i in (4, 5, 6, 7, 8):
+    for i in (4, 5):
         assert " splitK=" in conv[i] and " combine" in conv[i], conv[i]
     assert "+pool2x2s2" in conv[4]
+    # conv6 / conv7: the small-M x3 kernel in 16 K slices; conv8 split K (in-GEMM combine)
+    for i in (6, 7):
+        assert "mode=x3_lat" in conv[i] and " splitK=16 x3-combine latency" in conv[i], conv[i]
+    assert " splitK=" in conv[8] and " combine latency" in conv[8], conv[8]
     # the batch plan at batch 1: conv1-conv7 on the x3 conv, conv5 in the (N, K) rule's 2 K slices
     assert [l for l in base if " splitK=" in l] == [l for l in base if " splitK=2 x3-combine" in l] and \
         sum(" splitK=2 " in l for l in base) == 1 and sum("patch_x3" in l for l in base) == 7

@@ -888,9 +888,93 @@ def test_yolo_latency_plan_vs_reference_golden(yolo_weights, golden_frames, fram
         g, _ = yolo_graph.build_graph(dnn_hip.DnnGraphBuilder, yolo_weights, in_shape=(1, 416, 416, 3))
         latency_b1_engine.append(dnn_hip.DnnInferenceEngine(g, False, latency=True))
     eng = latency_b1_engine[0]
-    assert eng.plan().describe().count(" combine latency") >= 5
+    desc = eng.plan().describe()
+    conv = [ln for ln in desc.splitlines() if ln.startswith("conv")]
+    assert all(" combine latency" in conv[i] for i in (4, 5, 8)), desc
+    assert "mode=x3_lat" in conv[6] and "mode=x3_lat" in conv[7], desc  # conv6 / conv7: small-M x3
     y = eng.run(synth.frame(frame))
     assert R.normwise_err(y, golden_frames[frame]) < NET_TOL
+
+
+X3_LAT_CASES = [
+    # B, H, W, C, od1, od2, forced chunks per workgroup (DNN_HIP_X3L_CPW) or None, 1x1 outputs
+    # or None: pool (2x2 s1) -> conv3x3 C->od1 -> conv3x3 od1->od2 [-> conv1x1 + bias] in a
+    # latency plan, both 3x3 convs on the small-M x3 kernel (any workgroup count here)
+    (1, 13, 13, 512, 1024, 1024, None, 125),  # conv6 / conv7 / conv8 at batch 1
+    (2, 13, 13, 256, 512, 256, None, None),   # two frames: two 176-row tiles, the second straddling
+    (1, 9, 11, 64, 128, 192, None, 40),       # non-square frame, N = 192, 2 and 4 chunks, small head
+    (1, 13, 13, 128, 256, 256, 2, None),      # two chunks per workgroup forced (4 -> 2 slices; 8 -> 4)
+]
+
+
+@pytest.mark.parametrize("case", X3_LAT_CASES)
+def test_x3_latency_kernel_vs_oracle(monkeypatch, case):
+    """conv3x3_x3_lat_kernel (latency plans): 64-column workgroups over one or two 32-channel
+    chunks, raw slice partials summed in slice order by the combine kernel with the epilogue
+    (then YOLO's conv8-like 1x1 head on the fp32 MFMA).  Each layer within the fp32 LAYER_TOL
+    of the float64 oracle and within 1.25x of the fp32 MFMA latency plan's error
+    (DNN_HIP_X3=0), repeat runs and HIP-graph replays identical."""
+    B, H, W, C, od1, od2, cpw, head = case
+    monkeypatch.setenv("DNN_HIP_X3_LAT_MINWG", "1")
+    if cpw:
+        monkeypatch.setenv("DNN_HIP_X3L_CPW", str(cpw))
+    rng = np.random.default_rng(B + C + od1 + od2)
+    x = rng.standard_normal((B, H, W, C)).astype(np.float32)
+
+    def layer(c, od, kk=3, bn=True):
+        k = (rng.standard_normal((kk, kk, c, od)) * np.sqrt(2.0 / (kk * kk * c))).astype(np.float32)
+        b = rng.standard_normal(od).astype(np.float32) * 0.1
+        if not bn:
+            return k, b, None
+        gam = rng.uniform(0.5, 1.5, od).astype(np.float32)
+        gam[::5] *= -1
+        return k, b, (rng.standard_normal(od).astype(np.float32) * 0.1, rng.uniform(0.5, 1.5, od).astype(np.float32), gam)
+
+    L = [layer(C, od1), layer(od1, od2)] + ([layer(od2, head, 1, False)] if head else [])
+
+    def graph(layers):
+        g = dnn_hip.DnnGraphBuilder()
+        y = g.create_input(list(x.shape))
+        y = g.create_max_pool2d(y, [1, 2, 2, 1], [1, 1, 1, 1], "SAME")
+        for k, b, n in layers:
+            y = g.create_conv2d(y, k, [1, 1, 1, 1], "SAME")
+            y = g.create_bias_add(y, b)
+            if n is not None:  # (the 1x1 head: bias only, as YOLO's conv8)
+                y = g.create_batch_norm(y, *n, 1e-5)
+                y = g.create_leaky_relu(y)
+        g.set_out_node(y)
+        return g
+
+    ref = [R.max_pool2d(x, [1, 2, 2, 1], [1, 1, 1, 1], "SAME")]
+    for k, b, n in L:
+        y = R.bias_add(R.conv2d(ref[-1], k), b)
+        ref.append(y if n is None else R.leaky_relu(R.batch_norm(y, *n, 1e-5)))
+    errs = {}
+    for x3 in ("1", "0"):
+        monkeypatch.setenv("DNN_HIP_X3", x3)
+        e1 = dnn_hip.DnnInferenceEngine(graph(L[:1]), False, latency=True)
+        e2 = dnn_hip.DnnInferenceEngine(graph(L), False, latency=True)
+        desc = e2.plan().describe()
+        assert desc.count("mode=x3_lat") == (2 if x3 == "1" else 0), desc
+        y1, y2 = e1.run(x), e2.run(x)
+        errs[x3] = (R.normwise_err(y1, ref[1]), R.normwise_err(y2, ref[-1]))
+        print("x3=%s layer/chain normwise err %.3e %.3e" % (x3, errs[x3][0], errs[x3][1]))
+        if x3 == "1":
+            assert " x3-combine latency" in desc, desc
+            assert np.array_equal(e2.run(x), y2)
+            import torch
+            plan = e2.plan()
+            xd = torch.from_numpy(x).cuda()
+            yd = torch.empty((B,) + plan.out_shape, device="cuda")
+            st = torch.cuda.Stream()
+            for _ in range(3):
+                plan.run_graph(B, xd.data_ptr(), yd.data_ptr(), st.cuda_stream)
+            st.synchronize()
+            assert np.array_equal(yd.cpu().numpy(), y2)
+    nl = len(L)
+    for x3 in ("0", "1"):
+        assert errs[x3][0] < LAYER_TOL and errs[x3][1] < nl * LAYER_TOL, (x3, errs)
+    assert errs["1"][0] <= 1.25 * errs["0"][0] and errs["1"][1] <= 1.25 * errs["0"][1], errs
 
 
 IM2COL_ROW_CASES = [

@@ -7,7 +7,9 @@
 #   bench [BENCH_ARGS...]      one bench.py line (fp32 forward only unless args say otherwise)
 #   ab VAR V1 V2 [BENCH_ARGS]  bench.py --kernels with env VAR=V1, then VAR=V2, then V1 again
 #   sweep VAR V1 V2 ...        bench.py --kernels (forward only) for each value of env VAR, then V1 again
+#   lat VAR V1 V2 ...          the batch-1 latency plan (latency_b1) for each value of env VAR
 #   trace [BENCH_ARGS...]      rocprofv3 --kernel-trace --stats of a short bench run
+#   lattrace [BENCH_ARGS...]   kernel trace of the batch-1 latency plan's replays, by (kernel, grid)
 #   pmc GROUP [BENCH_ARGS...]  one rocprofv3 --pmc pass: GROUP = fetch | write | sqa | sqb
 #   full                       round evidence: tests, default bench line, trace, fetch/write, SQ a/b
 # Every GPU step runs under its own timeout; the script stops at the first failure.
@@ -65,6 +67,25 @@ case $task in
     for v in "$@" "$first"; do
       export "$var=$v"; run_bench "sweep_$v" --kernels $FAST --steps 20 --warmup 3 || exit 1
     done
+    ;;
+  lat)
+    var=$1; shift
+    for v in "$@"; do
+      export "$var=$v"
+      timeout -k 10 400 python bench.py --no-cpu --no-fp16 --no-unfused --no-e2e --no-fp32-mfma --steps 3 --warmup 1 \
+        > "$O/lat_$v.log" 2>&1 || { tail -20 "$O/lat_$v.log"; exit 1; }
+      tail -1 "$O/lat_$v.log" > "$O/lat_$v.json"
+      python - "$O/lat_$v.json" "$var=$v" <<'EOF2'
+import json, sys
+d = json.loads(open(sys.argv[1]).read())["latency_b1"]
+print(sys.argv[2], "graph_device_ms %.4f graph_ms %.4f" % (d["graph_device_ms"], d["graph_ms"]))
+print("  " + "  ".join("%s %.4f" % (n, v) for n, v in d["kernel_ms"].items()))
+EOF2
+    done
+    ;;
+  lattrace)
+    prof lattrace --kernel-trace -- --steps 1 --warmup 1 --no-cpu --no-fp16 --no-unfused --no-e2e --no-fp32-mfma "$@" || exit 1
+    python tools/trace_by_grid.py $(find "$O/lattrace" -name "*kernel_trace.csv") --min-count 100 > "$O/lattrace.txt" && cat "$O/lattrace.txt"
     ;;
   trace) prof trace --kernel-trace --stats -- --steps 10 --warmup 3 $FAST "$@" ;;
   pmc)
