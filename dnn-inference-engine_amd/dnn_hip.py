@@ -143,15 +143,18 @@ def _precision(p):
 class DnnInferenceEngine(object):
     """proj3/dnn_openblas.py:23-57.  `device` picks the GPU (default $DNN_HIP_DEVICE or 0);
     `precision` "fp32" (default, the reference's arithmetic) or "fp16" (fp16 MFMA conv path,
-    BASELINE config 5; default from $DNN_HIP_PRECISION); `latency` True (default
-    $DNN_HIP_LATENCY=1) builds a latency plan (dnn_plan_set_latency_mode: K splits chosen for
-    the graph's batch, for single-frame inference as proj3/__init__.py:24-26 runs it)."""
+    BASELINE config 5; default from $DNN_HIP_PRECISION); `latency` True builds a latency plan
+    (dnn_plan_set_latency_mode: K splits chosen for the graph's batch, for single-frame
+    inference as proj3/__init__.py:24-26 runs it; fp32 only).  Unset, $DNN_HIP_LATENCY=1 turns
+    it on for fp32 engines and is ignored by fp16 ones; latency=True with fp16 is an error."""
 
     def __init__(self, graph, debug, device=None, precision=None, latency=None):
         self.g = graph
         self.debug = debug
         self.precision = _precision(precision)
-        self.latency = os.environ.get("DNN_HIP_LATENCY") == "1" if latency is None else bool(latency)
+        if latency is None:  # the environment default applies where latency plans exist (fp32)
+            latency = os.environ.get("DNN_HIP_LATENCY") == "1" and self.precision == "fp32"
+        self.latency = bool(latency)
         self.device = int(os.environ.get("DNN_HIP_DEVICE", "0")) if device is None else device
         self.save_dir = os.path.join(os.getcwd(), "intermediate")
         self._plan = None

@@ -96,10 +96,10 @@ class FrameIngest(object):
     def submit_host(self, n):
         """Upload the first n frames of the current pinned slot and preprocess them."""
         torch = self.torch
+        if not 0 <= n <= self.batch:  # (before the slot flips: a rejected call changes nothing)
+            raise ValueError(f"n={n} outside [0, {self.batch}]")
         k = self.slot
         self.slot ^= 1
-        if not 0 <= n <= self.batch:
-            raise ValueError(f"n={n} outside [0, {self.batch}]")
         up = torch.cuda.Event()
         with torch.cuda.stream(self.copy_stream):
             if self.prepped[k] is not None:

@@ -360,3 +360,16 @@ def test_latency_mode_errors():
         assert lib.dnn_plan_set_latency_mode(h, 1) != 0  # after a layer
     finally:
         lib.dnn_plan_destroy(h)
+
+
+def test_latency_env_default_only_for_fp32(monkeypatch):
+    """$DNN_HIP_LATENCY=1 turns latency plans on for fp32 engines only (fp16 plans
+    have none); an explicit latency argument wins."""
+    g = dnn_hip.DnnGraphBuilder()
+    g.set_out_node(g.create_input([1, 4, 4, 8]))
+    monkeypatch.setenv("DNN_HIP_LATENCY", "1")
+    assert dnn_hip.DnnInferenceEngine(g, False).latency
+    assert not dnn_hip.DnnInferenceEngine(g, False, precision="fp16").latency
+    assert not dnn_hip.DnnInferenceEngine(g, False, latency=False).latency
+    monkeypatch.setenv("DNN_HIP_LATENCY", "0")
+    assert not dnn_hip.DnnInferenceEngine(g, False).latency

@@ -797,6 +797,24 @@ def test_frame_ingest_pipeline_double_buffer(yolo_b1):
         assert np.array_equal(o.cpu().numpy(), ref)
 
 
+def test_frame_ingest_rejected_submit_keeps_slot():
+    """submit_host with n outside [0, batch] raises before the slot flips, so the
+    next valid call still uploads the buffer next_host_buffer() handed out."""
+    import ingest
+    import ingest_numpy as IN
+    rng = np.random.default_rng(5)
+    fi = ingest.FrameIngest(2, 60, 80, __import__("torch").device("cuda", 0))
+    frames = rng.integers(0, 256, size=(2, 60, 80, 3), dtype=np.uint8)
+    fi.next_host_buffer()[:2].numpy()[...] = frames
+    slot = fi.slot
+    with pytest.raises(ValueError):
+        fi.submit_host(3)
+    assert fi.slot == slot
+    x = fi.submit_host(2)
+    __import__("torch").cuda.synchronize()
+    assert np.array_equal(x.cpu().numpy(), np.stack([IN.resize_input(f) for f in frames]))
+
+
 def test_frame_ingest_reuse_ordered_without_release():
     """slot reuse must be ordered without release().  Six batches through two
     slots; a frame decoder rewrites the pinned buffer as soon as next_host_buffer() returns,
