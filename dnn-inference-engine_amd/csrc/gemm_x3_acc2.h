@@ -47,7 +47,11 @@ __device__ __forceinline__ void vm_wait() {
 // (the round-2 kernel's XOR swizzle reaches the same count but costs ~5 VALU per fragment:
 // 0.850 vs 0.826 ms conv7 here, same call).  The padding bytes of each LDS row are whatever
 // follows the chunk in global memory, never read.
-template <int BM, int NPR, bool POOL, int LP = 224>
+// PF: the next row block's A fragments are read inside this block's MFMAs, each piece as soon as
+// this block's last MFMA on that piece has issued (correction order a2b0, a1b1, a1b0, a0b2,
+// a0b1 -- a2 and a1 retire early), so their LDS latency is covered by the wave's own MFMAs
+// rather than by the partner wave's alone.
+template <int BM, int NPR, bool POOL, int LP = 224, bool PF = false>
 __global__ void __launch_bounds__(512, 2)
 conv3x3_x3_acc2_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __restrict__ Bt, float* __restrict__ out,
                        bf16_bits* __restrict__ out_split, int M, int N, int K, EpiParams epi, int tilesM, X3Geom g,
@@ -91,6 +95,27 @@ conv3x3_x3_acc2_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __rest
     m = m < M ? m : M - 1;
     prow[i] = (pixrow(m) - P0 - (Wp + 1)) * LP + 16 * fq;
   }
+
+  // (PF) the rows packed three per register, 10-bit fields (a patch row < NPR <= 1023): the
+  // prefetch's extra live fragments need the 7 registers
+  constexpr int NPK = (TM + 2) / 3;
+  unsigned prk[NPK];
+#pragma unroll
+  for (int k = 0; k < NPK; ++k) prk[k] = 0;
+  if constexpr (PF) {
+    static_assert(NPR <= 1023, "10-bit patch rows");
+#pragma unroll
+    for (int i = 0; i < TM; ++i) prk[i / 3] |= (unsigned)((prow[i] - 16 * fq) / LP) << (10 * (i % 3));
+  }
+  auto rowoff = [&](int i) {  // byte offset of block i's tap-(0, 0) fragment (PF: from prk)
+    if constexpr (PF) {
+      unsigned w = prk[i / 3];
+      asm volatile("" : "+v"(w));  // unpacked per use: hoisted out of the tap loop it is 11 registers again
+      return (int)__umul24((w >> (10 * (i % 3))) & 1023u, (unsigned)LP) + 16 * fq;
+    } else {
+      return prow[i];
+    }
+  };
 
   // patch DMA: this wave's piece k lands at LDS byte 1024 (wid + 8 k) + 16 lane = patch row r
   // (LP bytes each: the 192 data bytes of the chunk and, with LP > 192, the next LP - 192 bytes
@@ -145,8 +170,15 @@ conv3x3_x3_acc2_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __rest
   const int nsteps = 9 * nch;
   const unsigned char* P = smem;
   int t = 0, j = 0;
+  bf16x8 af[3];  // (PF) the current block's fragments, read during the previous block
+  auto read_frag = [&](const unsigned char* q, int p) { af[p] = *reinterpret_cast<const bf16x8*>(q + 64 * p); };
+  if constexpr (PF) {
+#pragma unroll
+    for (int p = 0; p < 3; ++p) read_frag(P + rowoff(0), p);
+  }
   for (int s = 0; s < nsteps; ++s) {
     const int toff = (t / 3) * Wp + (t % 3);  // tap (dy, dx) relative to (0, 0)
+    const int toffn = t < 8 ? ((t + 1) / 3) * Wp + ((t + 1) % 3) : 0;  // (PF) the next tap's
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
@@ -159,20 +191,42 @@ conv3x3_x3_acc2_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __rest
       if constexpr (NQW > 9) {  // pieces past NQW rewrite piece NQW - 1
         if (i == 3 * NJ + 1) issue_patch(j + 1, t + 9 < NQW ? t + 9 : NQW - 1, (j + 1) & 1);
       }
-      bf16x8 a[3];
-      const unsigned char* q = P + prow[i] + toff * LP;
+      if constexpr (PF) {
+        // next block: block i + 1 of this tap, or block 0 of the next tap (after tap 8 the read
+        // goes to this chunk's buffer and is repeated from the next one after the barrier)
+        const unsigned char* qn = i + 1 < TM ? P + rowoff(i + 1 < TM ? i + 1 : 0) + toff * LP : P + rowoff(0) + toffn * LP;
+        bf16x8 a[3] = {af[0], af[1], af[2]};
 #pragma unroll
-      for (int p = 0; p < 3; ++p) a[p] = *reinterpret_cast<const bf16x8*>(q + 64 * p);
+        for (int jb = 0; jb < NJ; ++jb) {
+          const bool lastjb = jb == NJ - 1;
+          f32x4 c = accc[i][jb];
+          c = mfma16_bf16(a[2], bq[0][0][jb], c);
+          if (lastjb) read_frag(qn, 2);
+          c = mfma16_bf16(a[1], bq[0][1][jb], c);
+          c = mfma16_bf16(a[1], bq[0][0][jb], c);
+          if (lastjb) read_frag(qn, 1);
+          c = mfma16_bf16(a[0], bq[0][2][jb], c);
+          c = mfma16_bf16(a[0], bq[0][1][jb], c);
+          accc[i][jb] = c;
+          accm[i][jb] = mfma16_bf16(a[0], bq[0][0][jb], accm[i][jb]);
+          if (lastjb) read_frag(qn, 0);
+        }
+      } else {
+        bf16x8 a[3];
+        const unsigned char* q = P + prow[i] + toff * LP;
 #pragma unroll
-      for (int jb = 0; jb < NJ; ++jb) {
-        f32x4 c = accc[i][jb];
-        c = mfma16_bf16(a[2], bq[0][0][jb], c);
-        c = mfma16_bf16(a[1], bq[0][1][jb], c);
-        c = mfma16_bf16(a[0], bq[0][2][jb], c);
-        c = mfma16_bf16(a[1], bq[0][0][jb], c);
-        c = mfma16_bf16(a[0], bq[0][1][jb], c);
-        accc[i][jb] = c;
-        accm[i][jb] = mfma16_bf16(a[0], bq[0][0][jb], accm[i][jb]);
+        for (int p = 0; p < 3; ++p) a[p] = *reinterpret_cast<const bf16x8*>(q + 64 * p);
+#pragma unroll
+        for (int jb = 0; jb < NJ; ++jb) {
+          f32x4 c = accc[i][jb];
+          c = mfma16_bf16(a[2], bq[0][0][jb], c);
+          c = mfma16_bf16(a[1], bq[0][1][jb], c);
+          c = mfma16_bf16(a[0], bq[0][2][jb], c);
+          c = mfma16_bf16(a[1], bq[0][0][jb], c);
+          c = mfma16_bf16(a[0], bq[0][1][jb], c);
+          accc[i][jb] = c;
+          accm[i][jb] = mfma16_bf16(a[0], bq[0][0][jb], accm[i][jb]);
+        }
       }
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -187,6 +241,10 @@ conv3x3_x3_acc2_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __rest
       wait_lgkm0();
       raw_barrier();
       P = smem + (j & 1) * BUFB;
+      if constexpr (PF) {
+#pragma unroll
+        for (int p = 0; p < 3; ++p) read_frag(P + rowoff(0), p);
+      }
     }
   }
   vm_wait<0>();

@@ -522,9 +522,9 @@ int launch_conv_x3(const bf16_bits* in_split, const bf16_bits* Bt, float* out, b
     return e ? atoi(e) : 0;
   }();
   const dim3 grid(tilesM * tilesN * (pool ? 1 : splits));
-#define X3A(NPR_, POOL_, LP_)                                                                                  \
-  hipLaunchKernelGGL((conv3x3_x3_acc2_kernel<X3_BM, NPR_, POOL_, LP_>), grid, dim3(512), 0, stream, in_split, Bt, \
-                     out, out_split, (int)M, N, K, epi, tilesM, xg, (unsigned)in_bytes, (unsigned)b_bytes)
+#define X3A(NPR_, POOL_, LP_, PF_)                                                                              \
+  hipLaunchKernelGGL((conv3x3_x3_acc2_kernel<X3_BM, NPR_, POOL_, LP_, PF_>), grid, dim3(512), 0, stream, in_split,  \
+                     Bt, out, out_split, (int)M, N, K, epi, tilesM, xg, (unsigned)in_bytes, (unsigned)b_bytes)
 #define X3P(NPR_, POOL_)                                                                                       \
   hipLaunchKernelGGL((conv3x3_x3_patch_kernel<X3_BM, NPR_, POOL_>), grid, dim3(512), 0, stream, in_split, Bt, out, \
                      out_split, (int)M, N, K, epi, tilesM, xg, (unsigned)in_bytes, (unsigned)b_bytes)
@@ -535,14 +535,19 @@ int launch_conv_x3(const bf16_bits* in_split, const bf16_bits* Bt, float* out, b
       X3P(X3_NPR, false);
   } else if (var == 2) {
     if (pool)
-      X3A(X3_NPR_POOL, true, 192);
+      X3A(X3_NPR_POOL, true, 192, false);
     else
-      X3A(X3_NPR, false, 192);
+      X3A(X3_NPR, false, 192, false);
+  } else if (var == 3) {
+    if (pool)
+      X3A(X3_NPR_POOL, true, 224, true);
+    else
+      X3A(X3_NPR, false, 224, true);
   } else {
     if (pool)
-      X3A(X3_NPR_POOL, true, 224);
+      X3A(X3_NPR_POOL, true, 224, false);
     else
-      X3A(X3_NPR, false, 224);
+      X3A(X3_NPR, false, 224, false);
   }
 #undef X3P
 #undef X3A

@@ -1438,13 +1438,14 @@ def test_x3_patch_variants(tmp_path):
     """The wide-layer x3 kernels (DNN_HIP_X3V, read once per process: each arm in its own process)
     on the whole net at batch 2 (conv4-conv7): the two-accumulator kernel with 224-B and with
     192-B LDS rows (gemm_x3_acc2.h; same products in the same order) give the same bits; the
-    round-2 kernel (per-step adds: another summation order) agrees within the net tolerance."""
+    round-2 kernel (per-step adds: another summation order) and the fragment-prefetch variant
+    (another correction order) agree within the net tolerance."""
     import subprocess
     import sys
 
     tool = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "x3v_out.py")
     outs = {}
-    for v in ("0", "2", "1"):
+    for v in ("0", "2", "1", "3"):
         f = str(tmp_path / ("out%s.npy" % v))
         env = dict(os.environ, DNN_HIP_X3V=v)
         subprocess.run([sys.executable, tool, f, "2"], env=env, check=True, timeout=110)
@@ -1453,6 +1454,7 @@ def test_x3_patch_variants(tmp_path):
     assert np.isfinite(outs["0"]).all()
     assert np.array_equal(outs["0"], outs["2"])
     assert R.normwise_err(outs["1"], outs["0"]) < NET_TOL
+    assert R.normwise_err(outs["3"], outs["0"]) < NET_TOL
 
 
 @pytest.mark.parametrize("kind", ["huge", "tiny"])

@@ -12,6 +12,9 @@
 #   lattrace [BENCH_ARGS...]   kernel trace of the batch-1 latency plan's replays, by (kernel, grid)
 #   pmc GROUP [BENCH_ARGS...]  one rocprofv3 --pmc pass: GROUP = fetch | write | sqa | sqb
 #   full                       round evidence: tests, default bench line, trace, fetch/write, SQ a/b
+#   profiles                   the profile part of the round evidence for the fused fp32 plan
+#                              (trace, FETCH/WRITE, SQ a/b), the unfused plan and the fp16 plan
+#                              (trace, FETCH/WRITE); tools/summarize_profiles.sh turns it into profiles/
 # Every GPU step runs under its own timeout; the script stops at the first failure.
 set -o pipefail
 export TMPDIR=/tmp
@@ -101,6 +104,22 @@ EOF2
     # beside a profiled dispatch (GRBM_GUI_ACTIVE and the SQ counters sample the whole GPU:
     # a concurrent postprocess inflated round 2's conv4 row 5x)
     prof "pmc_$group" --pmc $C -- --steps 3 --warmup 1 $FAST --gather outputs "$@"
+    ;;
+  profiles)
+    P="--gather outputs"
+    prof fused_trace --kernel-trace --stats -- --steps 10 --warmup 3 $FAST || exit 1
+    prof fused_fetch --pmc FETCH_SIZE -- --steps 3 --warmup 1 $FAST $P || exit 1
+    prof fused_write --pmc WRITE_SIZE -- --steps 3 --warmup 1 $FAST $P || exit 1
+    for g in sqa sqb; do bash "$0" pmc $g || exit 1; done
+    export DNN_HIP_FUSE=0
+    prof unf_trace --kernel-trace --stats -- --steps 10 --warmup 3 $FAST || exit 1
+    prof unf_fetch --pmc FETCH_SIZE -- --steps 3 --warmup 1 $FAST $P || exit 1
+    prof unf_write --pmc WRITE_SIZE -- --steps 3 --warmup 1 $FAST $P || exit 1
+    unset DNN_HIP_FUSE
+    prof f16_trace --kernel-trace --stats -- --steps 10 --warmup 3 $FAST --precision fp16 || exit 1
+    prof f16_fetch --pmc FETCH_SIZE -- --steps 3 --warmup 1 $FAST $P --precision fp16 || exit 1
+    prof f16_write --pmc WRITE_SIZE -- --steps 3 --warmup 1 $FAST $P --precision fp16 || exit 1
+    echo PROFILESOK
     ;;
   full)
     run_tests || exit 1

@@ -1,0 +1,23 @@
+#!/bin/bash
+# Turn a `tools/gpu_job.sh profiles` run (gpurun_out/$2) and its bench line
+# (gpurun_out/$3/bench.json, from `tools/gpu_job.sh bench --kernels`) into the committed
+# round evidence under profiles/:  bash tools/summarize_profiles.sh r03 prof bench
+set -e
+R=$1; D=gpurun_out/$2; B=gpurun_out/${3:-$2}; P=profiles
+python3 tools/prof_summary.py --skip 3 --trace $D/fused_trace/fused_trace_kernel_trace.csv \
+  --fetch $D/fused_fetch/fused_fetch_counter_collection.csv --write $D/fused_write/fused_write_counter_collection.csv \
+  --note "round ${R#r}: fused fp32 plan (x3 conv1-conv7), bench.py --steps 10 --warmup 3 (trace), --steps 3 --warmup 1 --gather outputs (FETCH_SIZE, WRITE_SIZE passes), MI355X" \
+  --out $P/pmc_summary.json
+python3 tools/prof_summary.py --skip 3 --unfused --trace $D/unf_trace/unf_trace_kernel_trace.csv \
+  --fetch $D/unf_fetch/unf_fetch_counter_collection.csv --write $D/unf_write/unf_write_counter_collection.csv \
+  --note "round ${R#r}: DNN_HIP_FUSE=0 plan (explicit im2col + GEMM, separate pools), MI355X" --out $P/pmc_summary_unfused.json
+python3 tools/prof_summary.py --skip 3 --fp16 --trace $D/f16_trace/f16_trace_kernel_trace.csv \
+  --fetch $D/f16_fetch/f16_fetch_counter_collection.csv --write $D/f16_write/f16_write_counter_collection.csv \
+  --note "round ${R#r}: fp16 plan (BASELINE config 5), MI355X" --out $P/pmc_summary_fp16.json
+cp $D/fused_trace/fused_trace_kernel_stats.csv $P/${R}_rocprof_kernel_stats.csv
+cp $D/unf_trace/unf_trace_kernel_stats.csv $P/${R}_rocprof_kernel_stats_unfused.csv
+cp $D/f16_trace/f16_trace_kernel_stats.csv $P/${R}_rocprof_kernel_stats_fp16.csv
+cp $B/bench.json $P/${R}_bench.json
+python3 tools/pmc_table.py $D/pmc_sqa/*counter_collection.csv $D/pmc_sqb/*counter_collection.csv \
+  --out $P/${R}_sq_counters_fp32.json > /dev/null
+echo done
