@@ -1457,6 +1457,24 @@ def test_x3_patch_variants(tmp_path):
     assert R.normwise_err(outs["3"], outs["0"]) < NET_TOL
 
 
+def test_patch16_variants(tmp_path):
+    """fp16 conv6/conv7 (DNN_HIP_P16V, read once per process): the 64-column-wave kernel
+    (gemm_f16_lds.h) and the 16x16x32 patch kernel (gemm_f16_patch.h) run the same products in
+    the same order -- the same bits on the whole net at batch 2."""
+    import subprocess
+    import sys
+
+    tool = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "x3v_out.py")
+    outs = {}
+    for v in ("1", "0"):
+        f = str(tmp_path / ("out%s.npy" % v))
+        env = dict(os.environ, DNN_HIP_P16V=v)
+        subprocess.run([sys.executable, tool, f, "2", "fp16"], env=env, check=True, timeout=110)
+        outs[v] = np.load(f)
+    assert outs["1"].shape == (2, 13, 13, 125) and np.isfinite(outs["1"]).all()
+    assert np.array_equal(outs["1"], outs["0"])
+
+
 @pytest.mark.parametrize("kind", ["huge", "tiny"])
 def test_x3_split_total_over_finite_fp32(monkeypatch, kind):
     """split3 (gemm_f32.h) is total over finite fp32: an operand above the largest bf16

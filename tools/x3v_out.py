@@ -1,5 +1,6 @@
-"""Write the YOLOv2-tiny output (batch argv[2], default 16) of the default fp32 plan to argv[1]
-(.npy), for tests/test_gpu_parity.py::test_x3_patch_variants (one process per DNN_HIP_X3V arm)."""
+"""Write the YOLOv2-tiny output (batch argv[2], default 16; precision argv[3], default fp32) of
+the default plan to argv[1] (.npy), for tests/test_gpu_parity.py::test_x3_patch_variants and
+::test_patch16_variants (one process per DNN_HIP_X3V / DNN_HIP_P16V arm: read once per process)."""
 import os
 import sys
 
@@ -13,5 +14,6 @@ import yolo_graph  # noqa: E402
 
 B = int(sys.argv[2]) if len(sys.argv) > 2 else 16
 g, _ = yolo_graph.build_graph(dnn_hip.DnnGraphBuilder, synth.yolo_weights(), in_shape=(B, 416, 416, 3))
-eng = dnn_hip.DnnInferenceEngine(g, False, device=0)
+prec = sys.argv[3] if len(sys.argv) > 3 else "fp32"
+eng = dnn_hip.DnnInferenceEngine(g, False, device=0, precision=prec)
 np.save(sys.argv[1], eng.run(synth.frames(list(range(B)))))
