@@ -618,8 +618,10 @@ def main():
         dom_layer = [ln for ln in desc if ln.startswith("conv")][int(DOMINANT[4:DOMINANT.index(".")])]
         x3 = "patch_x3" in dom_layer
         mult, peak = (X3_PRODUCTS, BF16_MFMA_PEAK_TFLOPS) if x3 else (1, FP32_MFMA_PEAK_TFLOPS)
+        if args.precision == "fp16":  # (config 5 as the main line: one fp16 MFMA product per product)
+            mult, peak = 1, FP16_MFMA_PEAK_TFLOPS
         achieved = mult * k["flops"] / avg_s / 1e12
-        prof = pmc_entry(DOMINANT)
+        prof = pmc_entry(DOMINANT, "pmc_summary_fp16.json" if args.precision == "fp16" else "pmc_summary.json")
         traffic = prof.get("hbm_bytes_per_launch")
         # split-K layers (conv6/conv7) finish in a separate ordered reduce + epilogue kernel:
         # the conv-level figures below charge its time to the GEMM

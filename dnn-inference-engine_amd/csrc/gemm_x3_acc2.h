@@ -12,8 +12,9 @@
 // main product each) are rounded at their own, 2^-8 smaller, magnitude
 // (tests/test_gpu_parity.py::test_x3_conv_vs_oracle holds the error to <= 1.25x the fp32
 // MFMA path's).  Summation order: per output, accm over the steps (chunk-major, tap-minor) of
-// a0 b0; accc over the same steps of (a2b0, a1b1, a0b2, a1b0, a0b1) in that order; then
-// accm + accc.  It depends on (N, K) only (batch rows are bit-identical to batch-1 runs).
+// a0 b0; accc over the same steps of (a2b0, a1b1, a1b0, a0b2, a0b1) in that order (PF = false:
+// a2b0, a1b1, a0b2, a1b0, a0b1); then accm + accc.  It depends on (N, K) only (batch rows are
+// bit-identical to batch-1 runs).
 #pragma once
 #include "gemm_x3_patch.h"
 
@@ -47,10 +48,11 @@ __device__ __forceinline__ void vm_wait() {
 // (the round-2 kernel's XOR swizzle reaches the same count but costs ~5 VALU per fragment:
 // 0.850 vs 0.826 ms conv7 here, same call).  The padding bytes of each LDS row are whatever
 // follows the chunk in global memory, never read.
-// PF: the next row block's A fragments are read inside this block's MFMAs, each piece as soon as
-// this block's last MFMA on that piece has issued (correction order a2b0, a1b1, a1b0, a0b2,
-// a0b1 -- a2 and a1 retire early), so their LDS latency is covered by the wave's own MFMAs
-// rather than by the partner wave's alone.
+// PF (default): the next row block's A fragments are read inside this block's MFMAs, each piece
+// as soon as this block's last MFMA on that piece has issued (correction order a2b0, a1b1,
+// a1b0, a0b2, a0b1 -- a2 and a1 retire early), so their LDS latency is covered by the wave's
+// own MFMAs rather than by the partner wave's alone; the patch rows are then packed three per
+// register to make room (conv7 -2 %, conv6 -1.5 %, conv4/conv5 -1 %: same-box A/B).
 template <int BM, int NPR, bool POOL, int LP = 224, bool PF = false>
 __global__ void __launch_bounds__(512, 2)
 conv3x3_x3_acc2_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __restrict__ Bt, float* __restrict__ out,

@@ -6,7 +6,6 @@
 #include "dnn_common.h"
 #include "gemm_f16.h"
 #include "gemm_f16_patch.h"
-#include "gemm_f16_lds.h"
 
 namespace dnnhip {
 
@@ -321,17 +320,7 @@ int launch_conv_patch16(const half_t* in_padded, const half_t* Bt, int ldb, half
   const int bm = p16_bm();
   const int tilesM = (int)((M + bm - 1) / bm), tilesN = N / 256;
   const Patch16Geom pg{H, W, C, out_padded};
-  // DNN_HIP_P16V: unset / 1 = the 64-column-wave kernel (gemm_f16_lds.h; same bits as the
-  // 16x16x32 patch kernel), 0 = the patch kernel
-  static const int var = [] {
-    const char* e = getenv("DNN_HIP_P16V");
-    return e ? atoi(e) : 1;
-  }();
-  const long long b_bytes = (long long)N * ldb * 2;
-  if (bm == 176 && var == 1 && b_bytes < 0x80000000LL)
-    hipLaunchKernelGGL((conv3x3_f16_lds_kernel<P16_NPR>), dim3(tilesM * tilesN), dim3(512), 0, stream, in_padded, Bt,
-                       ldb, out, (int)M, N, K, epi, tilesM, pg, (unsigned)in_bytes, (unsigned)b_bytes);
-  else if (bm == 176)
+  if (bm == 176)
     hipLaunchKernelGGL((conv3x3_f16_patch_kernel<176, P16_NPR, half_t, 16>), dim3(tilesM * tilesN), dim3(512), 0,
                        stream, in_padded, Bt, ldb, out, (int)M, N, K, epi, tilesM, pg, (unsigned)in_bytes);
   else

@@ -514,9 +514,11 @@ int launch_conv_x3(const bf16_bits* in_split, const bf16_bits* Bt, float* out, b
   const int tilesM = (int)((M + X3_BM - 1) / X3_BM), tilesN = N / 256;
   // splits > 1: `out` receives the raw partials [splits][M][N] (x3_combine_kernel finishes)
   const X3Geom xg{H, W, C, splits > 1 ? 2 : out_split ? 1 : 0, splits, PH, PW, 0};
-  // DNN_HIP_X3V: unset / 0 = the two-accumulator kernel (gemm_x3_acc2.h) with 224-B LDS rows,
-  // 2 = the same with 192-B rows, 1 = the round-2 kernel (conv3x3_x3_patch_kernel: per-step adds;
-  // a different summation order, so not the same bits)
+  // DNN_HIP_X3V: unset / 0 = the two-accumulator kernel (gemm_x3_acc2.h) with 224-B LDS rows
+  // and the next block's fragments read during this block's MFMAs (PF; measured conv7 -2 %,
+  // conv6 -1.5 % against 3, same box), 2 = the same with 192-B rows (same bits), 3 = without the
+  // fragment prefetch (another correction order), 1 = the round-2 kernel (conv3x3_x3_patch_kernel:
+  // per-step adds; another summation order)
   static const int var = [] {
     const char* e = getenv("DNN_HIP_X3V");
     return e ? atoi(e) : 0;
@@ -535,19 +537,19 @@ int launch_conv_x3(const bf16_bits* in_split, const bf16_bits* Bt, float* out, b
       X3P(X3_NPR, false);
   } else if (var == 2) {
     if (pool)
-      X3A(X3_NPR_POOL, true, 192, false);
+      X3A(X3_NPR_POOL, true, 192, true);
     else
-      X3A(X3_NPR, false, 192, false);
+      X3A(X3_NPR, false, 192, true);
   } else if (var == 3) {
-    if (pool)
-      X3A(X3_NPR_POOL, true, 224, true);
-    else
-      X3A(X3_NPR, false, 224, true);
-  } else {
     if (pool)
       X3A(X3_NPR_POOL, true, 224, false);
     else
       X3A(X3_NPR, false, 224, false);
+  } else {
+    if (pool)
+      X3A(X3_NPR_POOL, true, 224, true);
+    else
+      X3A(X3_NPR, false, 224, true);
   }
 #undef X3P
 #undef X3A
