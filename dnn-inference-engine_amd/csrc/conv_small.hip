@@ -197,7 +197,9 @@ conv0_mfma_pool_kernel(const float* __restrict__ in, const float* __restrict__ w
 constexpr int C0_RS = 56;  // patch row stride (floats) >= 18 * CIN
 constexpr int C0_ROWS_PER_WAVE = 5;  // 20 row DMAs per tile over 4 waves (rows 18, 19 dummies)
 
-template <int CIN>
+// FL: the epilogue flag set at compile time (-1: runtime `epi.flags`); EVEN: OH and OW even, so
+// no pool window is ragged (YOLO's 416 x 416: the per-window edge selects drop out)
+template <int CIN, int FL = -1, bool EVEN = false>
 __global__ void __launch_bounds__(256)
 conv0_packed_pool_kernel(const float* __restrict__ in, const float* __restrict__ w, float* __restrict__ out,
                          DirectGeom g, int tilesX, int tilesY, int ntiles, const float* __restrict__ zero,
@@ -302,11 +304,13 @@ conv0_packed_pool_kernel(const float* __restrict__ in, const float* __restrict__
     // pool + epilogue into the wave's LDS stage, then 16-B coalesced stores
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int wy = (y0 >> 1) + 2 * wid + (i >> 1), wx = (x0 >> 1) + 4 * (i & 1) + fp;
-      const bool x1 = 2 * wx + 1 < g.OW, y1 = 2 * wy + 1 < g.OH;
-      const f32x4 v = {acc[i][0], x1 ? acc[i][1] : acc[i][0], y1 ? acc[i][2] : acc[i][0],
-                       x1 && y1 ? acc[i][3] : acc[i][0]};
-      stage[wid][i >> 1][4 * (i & 1) + fp][n] = pool_then_epilogue(v, pb_, pm, ps, pg, epi.flags);
+      f32x4 v = acc[i];
+      if constexpr (!EVEN) {
+        const int wy = (y0 >> 1) + 2 * wid + (i >> 1), wx = (x0 >> 1) + 4 * (i & 1) + fp;
+        const bool x1 = 2 * wx + 1 < g.OW, y1 = 2 * wy + 1 < g.OH;
+        v = f32x4{acc[i][0], x1 ? acc[i][1] : acc[i][0], y1 ? acc[i][2] : acc[i][0], x1 && y1 ? acc[i][3] : acc[i][0]};
+      }
+      stage[wid][i >> 1][4 * (i & 1) + fp][n] = pool_then_epilogue_t<FL>(v, pb_, pm, ps, pg, epi.flags);
     }
     wait_lgkm0();  // the stage is wave-private
     {  // one 16-B store per lane (2 window rows x 8 windows x 16 channels per wave)
@@ -374,8 +378,21 @@ int launch_conv0_mfma(const float* in, const float* w, float* out, const DirectG
   int sx, sy;
   magic_u32(tilesX, &mx, &sx);
   magic_u32(tilesY, &my, &sy);
-  hipLaunchKernelGGL((conv0_packed_pool_kernel<3>), dim3(grid), dim3(256), 0, s, in, w, out, g, tilesX, tilesY,
-                     (int)blocks, zero, epi, make_uint4(mx, (unsigned)sx, my, (unsigned)sy));
+  // YOLO's flag set (bias, BatchNorm, the reference's double-rounded leaky) and even frames
+  // compiled in; anything else takes the runtime-flag instantiation
+  constexpr int YOLO = EPI_BIAS | EPI_BN | EPI_LEAKY_F64;
+  const bool even = g.OH % 2 == 0 && g.OW % 2 == 0;
+  const uint4 mags = make_uint4(mx, (unsigned)sx, my, (unsigned)sy);
+#define C0P(FL_, EV_)                                                                                        \
+  hipLaunchKernelGGL((conv0_packed_pool_kernel<3, FL_, EV_>), dim3(grid), dim3(256), 0, s, in, w, out, g, tilesX, \
+                     tilesY, (int)blocks, zero, epi, mags)
+  if (epi.flags == YOLO && even)
+    C0P(YOLO, true);
+  else if (even)
+    C0P(-1, true);
+  else
+    C0P(-1, false);
+#undef C0P
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
     set_error("launch conv0_packed: %s", hipGetErrorString(e));

@@ -44,8 +44,11 @@ __device__ __forceinline__ void store_out(half_t* p, float v) { *p = (half_t)v; 
 // conversions and one f64 multiply.
 __device__ __forceinline__ float div_rn(float x, float d) {
   const double y = 1.0 / (double)d;
-  const float q = (float)((double)x * y);
-  if (__builtin_amdgcn_classf(q, 0x0F0)) return x / d;  // +-0, +-denormal
+  float q = (float)((double)x * y);
+  // +-0, +-denormal: the IEEE division, behind a wave-uniform branch (if-converted, its ~10
+  // VALU ran for every output: conv0's epilogue spent 40 of its 245 VALU per tile there)
+  const bool bad = __builtin_amdgcn_classf(q, 0x0F0);
+  if (__builtin_amdgcn_ballot_w64(bad)) q = bad ? x / d : q;
   return q;
 }
 
@@ -375,6 +378,32 @@ __device__ __forceinline__ void lds_dma4_opaque(const float* src, const float* d
 // for gamma < 0 (alpha < 0 for the avx alpha/beta form).  So max_i f(v_i) == f(max_i v_i)
 // (resp. f(min_i v_i)) value for value: the reference's epilogue-then-pool result
 // (dnn_openblas.c:220-254) with one epilogue per pooled output instead of four.
+// the epilogue with the flag set known at compile time (FL >= 0; FL < 0: the runtime `flags`)
+template <int FL>
+__device__ __forceinline__ float apply_epilogue_t(float v, float bias, float mean, float sq, float gamma, int flags) {
+  if constexpr (FL < 0) {
+    return apply_epilogue(v, bias, mean, sq, gamma, flags);
+  } else {
+    if constexpr ((FL & EPI_BIAS) != 0) v = v + bias;
+    if constexpr ((FL & EPI_BN) != 0) v = div_rn(v - mean, sq) * gamma;
+    if constexpr ((FL & EPI_BN_AB) != 0) v = v * mean - sq;
+    if constexpr ((FL & EPI_LEAKY_F64) != 0) v = v < 0.f ? (float)(0.1 * (double)v) : v;
+    if constexpr ((FL & EPI_LEAKY_F32) != 0) {
+      const float t = v * 0.1f;
+      v = v > t ? v : t;
+    }
+    return v;
+  }
+}
+template <int FL>
+__device__ __forceinline__ float pool_then_epilogue_t(f32x4 v, float pb, float pm, float ps, float pg, int flags) {
+  const int f = FL < 0 ? flags : FL;
+  const bool dec = ((f & EPI_BN) && pg < 0.f) || ((f & EPI_BN_AB) && pm < 0.f);
+  const float hi = __builtin_fmaxf(__builtin_fmaxf(v[0], v[1]), __builtin_fmaxf(v[2], v[3]));
+  const float lo = __builtin_fminf(__builtin_fminf(v[0], v[1]), __builtin_fminf(v[2], v[3]));
+  return apply_epilogue_t<FL>(dec ? lo : hi, pb, pm, ps, pg, flags);
+}
+
 __device__ __forceinline__ float pool_then_epilogue(f32x4 v, float pb, float pm, float ps, float pg, int flags) {
   const bool dec = ((flags & EPI_BN) && pg < 0.f) || ((flags & EPI_BN_AB) && pm < 0.f);
   const float hi = __builtin_fmaxf(__builtin_fmaxf(v[0], v[1]), __builtin_fmaxf(v[2], v[3]));
