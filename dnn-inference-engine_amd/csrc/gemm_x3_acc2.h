@@ -18,6 +18,14 @@
 #pragma once
 #include "gemm_x3_patch.h"
 
+// X3DIAG (diagnostic builds only, tools/build_diag.sh; wrong results): bit 1 drops the loop's
+// patch DMA (the patch keeps chunk 0), 2 its weight loads (tap 0's weights throughout), 4 the
+// epilogue of fp32-output layers, 8 the chunk barrier.  Operand data stays random: zero operands
+// clock higher and would flatter the variant (MI355X_MICROARCH, DVFS)
+#ifndef X3DIAG
+#define X3DIAG 0
+#endif
+
 namespace dnnhip {
 
 template <int I, int N, class F>
@@ -53,7 +61,9 @@ __device__ __forceinline__ void vm_wait() {
 // a1b0, a0b2, a0b1 -- a2 and a1 retire early), so their LDS latency is covered by the wave's
 // own MFMAs rather than by the partner wave's alone; the patch rows are then packed three per
 // register to make room (conv7 -2 %, conv6 -1.5 %, conv4/conv5 -1 %: same-box A/B).
-template <int BM, int NPR, bool POOL, int LP = 224, bool PF = false>
+// FL: the epilogue flag set at compile time (-1: runtime `epi.flags`; the launcher compiles in
+// YOLO's bias + BatchNorm + double-rounded leaky set), same arithmetic either way.
+template <int BM, int NPR, bool POOL, int LP = 224, bool PF = false, int FL = -1>
 __global__ void __launch_bounds__(512, 2)
 conv3x3_x3_acc2_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __restrict__ Bt, float* __restrict__ out,
                        bf16_bits* __restrict__ out_split, int M, int N, int K, EpiParams epi, int tilesM, X3Geom g,
@@ -188,10 +198,15 @@ conv3x3_x3_acc2_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __rest
       // lone wave stalls ~60 cycles per issue, and waves in step after the chunk barrier would
       // otherwise all stall at once): the next tap's 6 weight fragments, then the DMA pieces
       static_assert(TM >= 3 * NJ + 2, "row blocks to spread the tap's loads over");
-      if (i < 3 * NJ) load_b1(s + 1, i / NJ, i % NJ, bq[1][i / NJ][i % NJ]);
-      if (i == 3 * NJ) issue_patch(j + 1, t < NQW ? t : NQW - 1, (j + 1) & 1);  // (uniform count per tap)
+      if (i < 3 * NJ) {
+        if constexpr ((X3DIAG & 2) != 0)
+          bq[1][i / NJ][i % NJ] = bq[0][i / NJ][i % NJ];  // (the same random weights every tap)
+        else
+          load_b1(s + 1, i / NJ, i % NJ, bq[1][i / NJ][i % NJ]);
+      }
+      if (i == 3 * NJ && !(X3DIAG & 1)) issue_patch(j + 1, t < NQW ? t : NQW - 1, (j + 1) & 1);  // (uniform count per tap)
       if constexpr (NQW > 9) {  // pieces past NQW rewrite piece NQW - 1
-        if (i == 3 * NJ + 1) issue_patch(j + 1, t + 9 < NQW ? t + 9 : NQW - 1, (j + 1) & 1);
+        if (i == 3 * NJ + 1 && !(X3DIAG & 1)) issue_patch(j + 1, t + 9 < NQW ? t + 9 : NQW - 1, (j + 1) & 1);
       }
       if constexpr (PF) {
         // next block: block i + 1 of this tap, or block 0 of the next tap (after tap 8 the read
@@ -241,7 +256,7 @@ conv3x3_x3_acc2_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __rest
       ++j;
       vm_wait<0>();  // this wave's DMA pieces landed (issued mid-tap: ~5 row blocks ago)
       wait_lgkm0();
-      raw_barrier();
+      if (!(X3DIAG & 8)) raw_barrier();
       P = smem + (j & 1) * BUFB;
       if constexpr (PF) {
 #pragma unroll
@@ -260,6 +275,16 @@ conv3x3_x3_acc2_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __rest
 #pragma unroll
       for (int r = 0; r < 4; ++r) accm[i][jb][r] = accm[i][jb][r] + accc[i][jb][r];
   int* orow = reinterpret_cast<int*>(smem);
+  if ((X3DIAG & 4) != 0 && g.out_mode == 0) {  // keep the sums live without storing them (fp32-out
+    // layers only: a skipped producer would hand its consumer zeros, which clock higher)
+    float z = 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int jb = 0; jb < NJ; ++jb) z += accm[i][jb][0] + accm[i][jb][1] + accm[i][jb][2] + accm[i][jb][3];
+    if (z == 1.2345f) out[0] = z;
+    return;
+  }
   __syncthreads();
   if constexpr (POOL) {
     if (threadIdx.x < BM / 4) {
@@ -280,7 +305,7 @@ conv3x3_x3_acc2_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __rest
         constexpr int i = decltype(ic)::value;
         const int o = orow[4 * i + fq];
         if (o < 0) return;
-        const float e = pool_then_epilogue(accm[i][jb], pb, pm, ps, pg, epi.flags);
+        const float e = pool_then_epilogue_t<FL>(accm[i][jb], pb, pm, ps, pg, epi.flags);
         if (g.out_mode == 1) {
           unsigned short s0, s1, s2;
           split3(e, s0, s1, s2);
@@ -300,38 +325,60 @@ conv3x3_x3_acc2_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __rest
     orow[threadIdx.x] = m >= M ? -1 : (g.out_mode == 1 ? padded(m) : m);
   }
   __syncthreads();
-  static_for<0, NJ>([&](auto jbc) {
-    constexpr int jb = decltype(jbc)::value;
+  // Each row block's 16 x 32 outputs of the wave pass through a wave-private LDS stage (fp32 rows
+  // of 36: the MFMA-layout writes are conflict-free) and leave as 16-B stores: lane l takes row
+  // l / 4, columns 8 (l % 4) .. + 7 -- 2 stores of fp32, or 3 of split planes (one per piece), per
+  // row block where the MFMA layout stored one scalar per output (3 per output as split planes).
+  // Same epilogue arithmetic and split per value as before.
+  static_assert(BM * 4 <= 1024, "row table below the stages");
+  float* const stg = reinterpret_cast<float*>(smem + 1024) + wid * (16 * 36);
+  float pb[NJ], pm[NJ], ps[NJ], pg[NJ];
+#pragma unroll
+  for (int jb = 0; jb < NJ; ++jb) {
+    const int f = FL < 0 ? epi.flags : FL;
     const int n = n0 + 16 * jb + fr;
-    const float pb = (epi.flags & EPI_BIAS) ? epi.bias[n] : 0.f;
-    const float pm = (epi.flags & (EPI_BN | EPI_BN_AB)) ? epi.mean[n] : 0.f;
-    const float ps = (epi.flags & (EPI_BN | EPI_BN_AB)) ? epi.sq[n] : 1.f;
-    const float pg = (epi.flags & EPI_BN) ? epi.gamma[n] : 1.f;
-    const int cofs = (n >> 5) * 96 + (n & 31);
-    static_for<0, TM>([&](auto ic) {
-      constexpr int i = decltype(ic)::value;
-      static_for<0, 4>([&](auto rc) {
-        constexpr int r = decltype(rc)::value;
-        const int o = orow[16 * i + 4 * fq + r];
-        if (o < 0) return;
+    pb[jb] = (f & EPI_BIAS) ? epi.bias[n] : 0.f;
+    pm[jb] = (f & (EPI_BN | EPI_BN_AB)) ? epi.mean[n] : 0.f;
+    ps[jb] = (f & (EPI_BN | EPI_BN_AB)) ? epi.sq[n] : 1.f;
+    pg[jb] = (f & EPI_BN) ? epi.gamma[n] : 1.f;
+  }
+  const int rr = lane >> 2, c8 = 8 * (lane & 3);
+  static_for<0, TM>([&](auto ic) {
+    constexpr int i = decltype(ic)::value;
+#pragma unroll
+    for (int jb = 0; jb < NJ; ++jb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
         const float v = accm[i][jb][r];
-        if (g.out_mode == 2) {
-          out[((size_t)split * M + o) * N + n] = v;
-          return;
+        stg[(4 * fq + r) * 36 + 16 * jb + fr] =
+            g.out_mode == 2 ? v : apply_epilogue_t<FL>(v, pb[jb], pm[jb], ps[jb], pg[jb], epi.flags);
+      }
+    wait_lgkm0();
+    const f32x4 lo = *reinterpret_cast<const f32x4*>(stg + rr * 36 + c8);
+    const f32x4 hi = *reinterpret_cast<const f32x4*>(stg + rr * 36 + c8 + 4);
+    const int o = orow[16 * i + rr];
+    wait_lgkm0();  // (the stage is rewritten by the next row block)
+    if (o >= 0) {
+      if (g.out_mode == 1) {
+        u32x4 q[3];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          unsigned short a0, a1, a2, b0, b1, b2;
+          split3(e < 2 ? lo[2 * e] : hi[2 * e - 4], a0, a1, a2);
+          split3(e < 2 ? lo[2 * e + 1] : hi[2 * e - 3], b0, b1, b2);
+          q[0][e] = (unsigned)a0 | ((unsigned)b0 << 16);
+          q[1][e] = (unsigned)a1 | ((unsigned)b1 << 16);
+          q[2][e] = (unsigned)a2 | ((unsigned)b2 << 16);
         }
-        const float e = apply_epilogue(v, pb, pm, ps, pg, epi.flags);
-        if (g.out_mode == 1) {
-          unsigned short s0, s1, s2;
-          split3(e, s0, s1, s2);
-          bf16_bits* d = out_split + (size_t)o * (3 * N) + cofs;
-          d[0] = s0;
-          d[32] = s1;
-          d[64] = s2;
-        } else {
-          out[(size_t)o * N + n] = e;
-        }
-      });
-    });
+        bf16_bits* d = out_split + (size_t)o * (3 * N) + (n0 >> 5) * 96 + c8;
+#pragma unroll
+        for (int pc = 0; pc < 3; ++pc) *reinterpret_cast<u32x4*>(d + 32 * pc) = q[pc];
+      } else {
+        float* d = out + ((size_t)(g.out_mode == 2 ? split * M : 0) + o) * N + n0 + c8;
+        *reinterpret_cast<f32x4*>(d) = lo;
+        *reinterpret_cast<f32x4*>(d + 4) = hi;
+      }
+    }
   });
 }
 

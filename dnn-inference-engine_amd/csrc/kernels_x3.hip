@@ -524,9 +524,10 @@ int launch_conv_x3(const bf16_bits* in_split, const bf16_bits* Bt, float* out, b
     return e ? atoi(e) : 0;
   }();
   const dim3 grid(tilesM * tilesN * (pool ? 1 : splits));
-#define X3A(NPR_, POOL_, LP_, PF_)                                                                              \
-  hipLaunchKernelGGL((conv3x3_x3_acc2_kernel<X3_BM, NPR_, POOL_, LP_, PF_>), grid, dim3(512), 0, stream, in_split,  \
-                     Bt, out, out_split, (int)M, N, K, epi, tilesM, xg, (unsigned)in_bytes, (unsigned)b_bytes)
+#define X3AF(NPR_, POOL_, LP_, PF_, FL_)                                                                          \
+  hipLaunchKernelGGL((conv3x3_x3_acc2_kernel<X3_BM, NPR_, POOL_, LP_, PF_, FL_>), grid, dim3(512), 0, stream,      \
+                     in_split, Bt, out, out_split, (int)M, N, K, epi, tilesM, xg, (unsigned)in_bytes, (unsigned)b_bytes)
+#define X3A(NPR_, POOL_, LP_, PF_) X3AF(NPR_, POOL_, LP_, PF_, -1)
 #define X3P(NPR_, POOL_)                                                                                       \
   hipLaunchKernelGGL((conv3x3_x3_patch_kernel<X3_BM, NPR_, POOL_>), grid, dim3(512), 0, stream, in_split, Bt, out, \
                      out_split, (int)M, N, K, epi, tilesM, xg, (unsigned)in_bytes, (unsigned)b_bytes)
@@ -545,6 +546,11 @@ int launch_conv_x3(const bf16_bits* in_split, const bf16_bits* Bt, float* out, b
       X3A(X3_NPR_POOL, true, 224, false);
     else
       X3A(X3_NPR, false, 224, false);
+  } else if (epi.flags == (EPI_BIAS | EPI_BN | EPI_LEAKY_F64) && xg.out_mode != 2) {  // YOLO's set compiled in
+    if (pool)
+      X3AF(X3_NPR_POOL, true, 224, true, EPI_BIAS | EPI_BN | EPI_LEAKY_F64);
+    else
+      X3AF(X3_NPR, false, 224, true, EPI_BIAS | EPI_BN | EPI_LEAKY_F64);
   } else {
     if (pool)
       X3A(X3_NPR_POOL, true, 224, true);
@@ -553,6 +559,7 @@ int launch_conv_x3(const bf16_bits* in_split, const bf16_bits* Bt, float* out, b
   }
 #undef X3P
 #undef X3A
+#undef X3AF
   return check_x3("conv_x3");
 }
 
