@@ -293,6 +293,24 @@ conv3x3_x3_acc2_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __rest
       orow[threadIdx.x] = 4 * w >= M ? -1 : g.out_mode == 1 ? (b * (g.PH + 2) + py + 1) * (g.PW + 2) + px + 1 : w;
     }
     __syncthreads();
+    if (g.out_mode == 1) {  // staged 16-B split-plane stores (x3_pool_split_store)
+      static_assert(1024 + NW * TM * 4 * X3_STG_ROW * 4 <= 2 * BUFB && BM <= 1024, "stage");
+      float* stg = reinterpret_cast<float*>(smem + 1024) + wid * (TM * 4 * X3_STG_ROW);
+#pragma unroll
+      for (int jb = 0; jb < NJ; ++jb) {
+        const int f = FL < 0 ? epi.flags : FL;
+        const int n = n0 + 16 * jb + fr;
+        const float pb = (f & EPI_BIAS) ? epi.bias[n] : 0.f;
+        const float pm = (f & (EPI_BN | EPI_BN_AB)) ? epi.mean[n] : 0.f;
+        const float ps = (f & (EPI_BN | EPI_BN_AB)) ? epi.sq[n] : 1.f;
+        const float pg = (f & EPI_BN) ? epi.gamma[n] : 1.f;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+          stg[(4 * i + fq) * X3_STG_ROW + 16 * jb + fr] = pool_then_epilogue_t<FL>(accm[i][jb], pb, pm, ps, pg, epi.flags);
+      }
+      x3_pool_split_store<TM>(stg, orow, BM / 4, 0, out_split, 3 * (size_t)N, (n0 >> 5) * 96, lane);
+      return;
+    }
     static_for<0, NJ>([&](auto jbc) {
       constexpr int jb = decltype(jbc)::value;
       const int n = n0 + 16 * jb + fr;

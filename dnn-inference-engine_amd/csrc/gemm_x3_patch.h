@@ -82,6 +82,41 @@ __device__ __forceinline__ void x3_fold(f32x4 (&acc)[TM][NB], const f32x4 (&accc
       for (int r = 0; r < 4; ++r) acc[i][j][r] = acc[i][j][r] + accc[i][j][r];
 }
 
+// Pooled split-plane store through LDS (the narrow x3 kernels' epilogue): a wave's pooled values
+// of TM row blocks (4 windows x 32 columns each) are written to a wave-private stage in the MFMA
+// layout (lane (fr, fq) of block i: window 4 i + fq, column 16 jb + fr; 48-float rows, so the
+// two lane halves of a ds_write_b32 fall on disjoint banks), then each lane takes (window, 8
+// columns) tasks: two 16-B stage reads, the exact split of the 8 values and one 16-B store per
+// piece into the window's 192-B record (3 x 32 bf16 at out_split + o n3 + col0).  The values and
+// splits are those of one scalar store per piece and output.
+constexpr int X3_STG_ROW = 48;
+template <int TM>
+__device__ __forceinline__ void x3_pool_split_store(const float* stg, const int* orow, int no, int wbase,
+                                                    bf16_bits* __restrict__ out_split, size_t n3, int col0,
+                                                    int lane) {
+  wait_lgkm0();  // the stage is wave-private
+  for (int task = lane; task < 16 * TM; task += 64) {
+    const int wl = task >> 2, c8 = 8 * (task & 3), w = wbase + wl;
+    const int o = w < no ? orow[w] : -1;
+    if (o < 0) continue;
+    const f32x4 lo = *reinterpret_cast<const f32x4*>(stg + wl * X3_STG_ROW + c8);
+    const f32x4 hi = *reinterpret_cast<const f32x4*>(stg + wl * X3_STG_ROW + c8 + 4);
+    u32x4 q[3];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      unsigned short a0, a1, a2, b0, b1, b2;
+      split3(e < 2 ? lo[2 * e] : hi[2 * e - 4], a0, a1, a2);
+      split3(e < 2 ? lo[2 * e + 1] : hi[2 * e - 3], b0, b1, b2);
+      q[0][e] = (unsigned)a0 | ((unsigned)b0 << 16);
+      q[1][e] = (unsigned)a1 | ((unsigned)b1 << 16);
+      q[2][e] = (unsigned)a2 | ((unsigned)b2 << 16);
+    }
+    bf16_bits* d = out_split + (size_t)o * n3 + col0 + c8;
+#pragma unroll
+    for (int pc = 0; pc < 3; ++pc) *reinterpret_cast<u32x4*>(d + 32 * pc) = q[pc];
+  }
+}
+
 // POOL: a fused 2x2/s2 max pool -- GEMM rows pool-window-major (row 4 w + 2 dy + dx = cell (dy,
 // dx) of pooled pixel w; cells past an odd edge repeat cell (0, 0)), so a lane's 4 accumulator
 // registers (rows 4 q .. 4 q + 3 of its 16 x 16 block) are one window: pooled before the
@@ -555,6 +590,25 @@ conv3x3_x3_tile_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __rest
     orow[r] = o;
   }
   __syncthreads();
+  if constexpr (POOL) {
+    if (g.out_mode == 1) {  // staged 16-B split-plane stores (x3_pool_split_store)
+      static_assert(1024 + NT / 64 * TM * 4 * X3_STG_ROW * 4 <= NBUF * PR * RB && NO * 4 <= 1024, "stage");
+      float* stg = reinterpret_cast<float*>(smem + 1024) + wid * (TM * 4 * X3_STG_ROW);
+#pragma unroll
+      for (int jb = 0; jb < 2; ++jb) {
+        const int n = n0 + 16 * jb + fr;
+        const float pb = (epi.flags & EPI_BIAS) ? epi.bias[n] : 0.f;
+        const float pm = (epi.flags & (EPI_BN | EPI_BN_AB)) ? epi.mean[n] : 0.f;
+        const float ps = (epi.flags & (EPI_BN | EPI_BN_AB)) ? epi.sq[n] : 1.f;
+        const float pg = (epi.flags & EPI_BN) ? epi.gamma[n] : 1.f;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+          stg[(4 * i + fq) * X3_STG_ROW + 16 * jb + fr] = pool_then_epilogue(acc[i][jb], pb, pm, ps, pg, epi.flags);
+      }
+      x3_pool_split_store<TM>(stg, orow, NO, 4 * wm * TM, out_split, 3 * (size_t)N, (n0 >> 5) * 96, lane);
+      return;
+    }
+  }
 #pragma unroll
   for (int jb = 0; jb < 2; ++jb) {
     const int n = n0 + 16 * jb + fr;  // < N: N % (32 WN) == 0 (launcher)
@@ -762,6 +816,25 @@ conv3x3_x3_c16_kernel(const float* __restrict__ in, const bf16_bits* __restrict_
     orow[r] = o;
   }
   __syncthreads();
+  if constexpr (POOL) {
+    if (g.out_mode == 1) {  // staged 16-B split-plane stores (x3_pool_split_store)
+      static_assert(1024 + WM * TM * 4 * X3_STG_ROW * 4 <= BB + PR * PB && NO * 4 <= 1024, "stage");
+      float* stg = reinterpret_cast<float*>(smem + 1024) + wm * (TM * 4 * X3_STG_ROW);
+#pragma unroll
+      for (int jb = 0; jb < 2; ++jb) {
+        const int n = 16 * jb + fr;
+        const float pb = (epi.flags & EPI_BIAS) ? epi.bias[n] : 0.f;
+        const float pm = (epi.flags & (EPI_BN | EPI_BN_AB)) ? epi.mean[n] : 0.f;
+        const float ps = (epi.flags & (EPI_BN | EPI_BN_AB)) ? epi.sq[n] : 1.f;
+        const float pg = (epi.flags & EPI_BN) ? epi.gamma[n] : 1.f;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+          stg[(4 * i + fq) * X3_STG_ROW + 16 * jb + fr] = pool_then_epilogue(acc[i][jb], pb, pm, ps, pg, epi.flags);
+      }
+      x3_pool_split_store<TM>(stg, orow, NO, 4 * wm * TM, out_split, 96, 0, lane);
+      return;
+    }
+  }
 #pragma unroll
   for (int jb = 0; jb < 2; ++jb) {
     const int n = 16 * jb + fr;
