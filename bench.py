@@ -646,8 +646,8 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": ("fp32 (conv1-conv7: fp32 operands split exactly into 3 bf16 pieces, 6 bf16 MFMA "
-                      "products, fp32 accumulate; error <= the fp32 MFMA path's; conv0, conv8: fp32 MFMA)"
+            "dtype": ("fp32 (conv1-conv8: fp32 operands split exactly into 3 bf16 pieces, 6 bf16 MFMA "
+                      "products, fp32 accumulate; error <= the fp32 MFMA path's; conv0: fp32 MFMA)"
                       if x3 else args.precision),
             "data": "synthetic (uniform [0,1) frames, random-init weights, tiny-yolo-voc channel plan)",
             "config": {"workload": "YOLOv2-tiny forward, 416x416x3 NHWC fp32, 64 frames per GPU in HBM, "

@@ -245,6 +245,10 @@ long long x3_tiles(long long batch, int OH, int OW, int OC, int C, int K);
 bool conv_x3_lat_supported(long long batch, int C, int OC, int H, int W, int OH, int OW, int kh, int kw, int sh,
                            int sw, int pt, int pl);
 int x3_lat_splits(int N, int K);
+// 1x1 x3 conv (gemm_x3_1x1.h: conv8) on the producer's zero-bordered split planes, fp32 out [M][N]
+bool conv_x3_1x1_supported(int C, int OC, int H, int W);
+int launch_conv_x3_1x1(const unsigned short* in_split, const unsigned short* Bt, float* out, long long M, int N,
+                       int Npad, int K, int H, int W, int C, const EpiParams& epi, hipStream_t stream);
 int launch_conv_x3_lat(const unsigned short* in_split, const unsigned short* Bt, float* part, long long M, int N,
                        int Npad, int K, int H, int W, int C, int splits, hipStream_t stream);
 int launch_x3_combine(const float* part, int splits, long long slab, const EpiParams& epi, const PoolGeom& g,

@@ -5,6 +5,7 @@
 #include "gemm_x3_patch.h"
 #include "gemm_x3_acc2.h"
 #include "gemm_x3_lat.h"
+#include "gemm_x3_1x1.h"
 
 #include <cfloat>
 #include <cstdlib>
@@ -272,7 +273,7 @@ int launch_x3_combine(const float* part, int splits, long long slab, const EpiPa
 // ---- weights: HWIO fp32 [K = tap * C + c][N] -> split pieces in the kernel's fragment order
 // [n/16][step = chunk * 9 + tap][piece][lane][8], k inside a step = 8 (lane >> 4) + e
 __global__ void pack_weights_x3_kernel(const float* __restrict__ w, bf16_bits* __restrict__ out, int K, int N, int Npad,
-                                       int C) {
+                                       int C, int taps) {  // taps: 9 (3x3) or 1 (1x1: step = chunk)
   const int nk = K / 32;
   const long long total = (long long)(Npad / 16) * nk * 3 * 512;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
@@ -283,7 +284,7 @@ __global__ void pack_weights_x3_kernel(const float* __restrict__ w, bf16_bits* _
     const long long r = q / 3;
     const int s = (int)(r % nk), nb = (int)(r / nk);
     const int n = nb * 16 + (lane & 15);
-    const int chunk = s / 9, tap = s - chunk * 9, c = chunk * 32 + 8 * (lane >> 4) + e;
+    const int chunk = s / taps, tap = s - chunk * taps, c = chunk * 32 + 8 * (lane >> 4) + e;
     const float v = n < N ? w[((size_t)tap * C + c) * N + n] : 0.f;
     unsigned short s0, s1, s2;
     split3(v, s0, s1, s2);
@@ -316,12 +317,13 @@ int launch_pack_weights_x3(const float* w, bf16_bits* out, int K, int N, int Npa
     hipLaunchKernelGGL(pack_weights_x3c16_kernel, dim3(grid_x3(total)), dim3(256), 0, s, w, out, N, Npad);
     return check_x3("pack_weights_x3 (c16)");
   }
-  if (K != 9 * C || C % 32 != 0 || Npad % 64 != 0 || Npad < N) {
+  if ((K != 9 * C && K != C) || C % 32 != 0 || Npad % 64 != 0 || Npad < N) {
     set_error("pack_weights_x3: unsupported K=%d N=%d Npad=%d C=%d", K, N, Npad, C);
     return -2;
   }
   const long long total = (long long)(Npad / 16) * (K / 32) * 3 * 512;
-  hipLaunchKernelGGL(pack_weights_x3_kernel, dim3(grid_x3(total)), dim3(256), 0, s, w, out, K, N, Npad, C);
+  hipLaunchKernelGGL(pack_weights_x3_kernel, dim3(grid_x3(total)), dim3(256), 0, s, w, out, K, N, Npad, C,
+                     K == C ? 1 : 9);
   return check_x3("pack_weights_x3");
 }
 
@@ -628,6 +630,51 @@ int launch_conv_x3_lat(const bf16_bits* in_split, const bf16_bits* Bt, float* pa
     X3L(1, X3_NPR);
 #undef X3L
   return check_x3("conv_x3_lat");
+}
+
+}  // namespace dnnhip
+
+namespace dnnhip {
+
+// ---- 1x1 x3 conv (gemm_x3_1x1.h): YOLOv2-tiny conv8 on its producer's split planes
+bool conv_x3_1x1_supported(int C, int OC, int H, int W) {
+  return C % 32 == 0 && C >= 32 && OC >= 1 && H >= 1 && W >= 1 && x3_enabled() && !getenv_flag_off("DNN_HIP_X3_1X1");
+}
+
+int launch_conv_x3_1x1(const bf16_bits* in_split, const bf16_bits* Bt, float* out, long long M, int N, int Npad, int K,
+                       int H, int W, int C, const EpiParams& epi, hipStream_t stream) {
+  if (M == 0 || N == 0) return 0;
+  const long long per_img = (long long)H * W, nimg = M / per_img;
+  const long long in_bytes = (long long)x3_act_bytes(nimg, H, W, C);
+  const long long b_bytes = (long long)(Npad / 16) * (K / 32) * 3072;
+  if (M % per_img != 0 || K != C || C % 32 != 0 || Npad % X3_1X1_BN != 0 || Npad < N || in_bytes >= 0x80000000LL ||
+      b_bytes >= 0x80000000LL || M > 0x7fffffffLL || out == nullptr) {
+    set_error("conv_x3_1x1: unsupported shape M=%lld N=%d K=%d %dx%dx%d", M, N, K, H, W, C);
+    return -2;
+  }
+  // 16 TMW-row tiles: 2 (32 rows, 338 workgroups at batch 64) or 4 (DNN_HIP_X3_1X1_TM=4: 64 rows)
+  static const int tmw = [] {
+    const char* e = getenv("DNN_HIP_X3_1X1_TM");
+    return e && atoi(e) == 4 ? 4 : 2;
+  }();
+  const long long tilesM = (M + 16 * tmw - 1) / (16 * tmw), blocks = tilesM * (Npad / X3_1X1_BN);
+  if (blocks > 0x7fffffffLL) {
+    set_error("conv_x3_1x1: grid too large");
+    return -2;
+  }
+  const X3Geom xg{H, W, C, 0, 1, 0, 0, 0};
+  constexpr int BIAS = EPI_BIAS;
+#define X1(FL_, TM_)                                                                                             \
+  hipLaunchKernelGGL((conv1x1_x3_kernel<FL_, TM_>), dim3((unsigned)blocks), dim3(256), 0, stream, in_split, Bt, \
+                     out, (int)M, N, K, epi, (int)tilesM, xg, (unsigned)in_bytes, (unsigned)b_bytes)
+  if (epi.flags == BIAS && tmw == 4)  // YOLO's detection layer: bias, linear
+    X1(BIAS, 4);
+  else if (epi.flags == BIAS)
+    X1(BIAS, 2);
+  else
+    X1(-1, 2);
+#undef X1
+  return check_x3("conv_x3_1x1");
 }
 
 }  // namespace dnnhip

@@ -88,9 +88,11 @@ using namespace dnnhip;
 // MODE_PATCH16: fp16 3x3 conv on a zero-bordered input (conv3x3_f16_patch_kernel; conv6/conv7)
 // MODE_X3: fp32 3x3 conv on the bf16 MFMA with exact 3-way splits, split zero-bordered input
 // (conv3x3_x3_patch_kernel; conv6/conv7 of the fp32 path)
+// MODE_X3_1X1: fp32 1x1 conv with the same arithmetic on its producer's split planes
+// (conv1x1_x3_kernel; conv8 of the fp32 path)
 enum ConvMode : int { MODE_GEMM = 0, MODE_DIRECT_A = 1, MODE_IMPLICIT = 2, MODE_DIRECT = 3, MODE_PATCH = 4,
-                      MODE_PATCH16 = 5, MODE_X3 = 6 };
-static const char* kModeName[] = {"gemm", "direct_a", "implicit", "direct", "patch", "patch16", "patch_x3"};
+                      MODE_PATCH16 = 5, MODE_X3 = 6, MODE_X3_1X1 = 7 };
+static const char* kModeName[] = {"gemm", "direct_a", "implicit", "direct", "patch", "patch16", "patch_x3", "x3_1x1"};
 
 struct PlanLayer {
   int type = 0;  // 0 conv, 1 pool
@@ -185,7 +187,7 @@ static void layout(dnn_plan* p) {
       L.w_off = off;
       // fp16 GEMM layers hold Bt in halves (2 per float slot); conv0's direct kernel reads fp32
       const bool half_w = p->fp16 && L.mode != MODE_DIRECT;
-      if (L.mode == MODE_X3)  // three bf16 pieces per weight
+      if (L.mode == MODE_X3 || L.mode == MODE_X3_1X1)  // three bf16 pieces per weight
         off = align_up(off + (size_t)L.Npad * L.Kpad * 3 / 2, 64);
       else
         off = align_up(off + ((size_t)L.Npad * L.Kpad + (half_w ? 1 : 0)) / (half_w ? 2 : 1), 64);
@@ -298,6 +300,13 @@ void dnn_plan_destroy(dnn_plan* p) {
 
 static void set_cfg(dnn_plan* p, PlanLayer& L) {
   const long long M = (long long)p->batch * L.OH * L.OW;
+  if (!p->fp16 && L.mode == MODE_X3_1X1) {  // one config: 32 x 128 tiles over all of K
+    L.cfg = 0;
+    L.Kpad = L.K;
+    L.Npad = (int)align_up(L.OC, 128);
+    L.splits = 1;
+    return;
+  }
   if (!p->fp16 && L.mode == MODE_X3) {  // one config per width (kernels_x3.hip); split-K by (N, K) only
     L.cfg = 0;
     L.Kpad = L.C == 16 ? 160 : L.K;  // (16 channels: 5 steps of two taps)
@@ -439,6 +448,18 @@ int dnn_plan_add_conv(dnn_plan* p, int kh, int kw, int od, int stride_h, int str
     } else {
       x3_cand = batch_ok;
     }
+  }
+  // fp32 1x1 layers right after an x3 conv (conv8 after conv7): the 1x1 x3 conv on the split
+  // planes that producer writes instead of its fp32 output.  Chosen by the layer alone (batch
+  // plans of any size run the same arithmetic).  Latency plans keep the fp32 GEMM split over the
+  // chip where this kernel's 32 x 128 tiles would not fill it (one frame's 169 rows are 6 tiles:
+  // 21 us against 14)
+  const long long t1x1 = ((long long)p->batch * L.OH * L.OW + 31) / 32 * ((od + 127) / 128);
+  if (!p->fp16 && !(p->latency && fused_splitk(p) && t1x1 < 256) && L.mode == MODE_DIRECT_A && !p->layers.empty() &&
+      p->layers.back().type == 0 &&
+      p->layers.back().mode == MODE_X3 && conv_x3_1x1_supported(L.C, od, L.H, L.W)) {
+    L.mode = MODE_X3_1X1;
+    p->layers.back().out_padded = true;
   }
   if (x3_cand) {
     // producers that can write the split planes: a separate pool, another x3 conv, a pool-fused
@@ -600,7 +621,7 @@ static int upload_weights(dnn_plan* p) {
         if (!rc)
           rc = launch_f32_to_f16(packed32, reinterpret_cast<half_t*>(p->weights + L.w_off),
                                  (long long)L.Npad * L.Kpad, 0);
-      } else if (!rc && L.mode == MODE_X3) {
+      } else if (!rc && (L.mode == MODE_X3 || L.mode == MODE_X3_1X1)) {
         rc = launch_pack_weights_x3(tmp, reinterpret_cast<unsigned short*>(p->weights + L.w_off), L.K, L.OC, L.Npad,
                                     L.C, 0);
       } else if (!rc) {
@@ -840,6 +861,11 @@ int dnn_plan_run(dnn_plan* p, int n, const float* d_in, float* d_out, void* stre
           rc = launch_conv3x3_patch_pool(cur, wt, L.Kpad, dst, g, L.C, L.OC, zero, epi, s, dsplit);
           break;
         }
+        case MODE_X3_1X1:
+          rc = launch_conv_x3_1x1(reinterpret_cast<const unsigned short*>(cur),
+                                  reinterpret_cast<const unsigned short*>(wt), dst, Mc, L.OC, L.Npad, L.K, L.H, L.W,
+                                  L.C, epi, s);
+          break;
         case MODE_X3:
           if (L.splits > 1) {  // raw partials into the slab; the next pool or a combine kernel finishes
             rc = L.x3lat ? launch_conv_x3_lat(reinterpret_cast<const unsigned short*>(cur),

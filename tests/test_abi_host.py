@@ -182,7 +182,8 @@ def test_plan_x3_structure_host_only(monkeypatch):
     """Default fp32 batch plan: conv1-conv7 on the x3 conv (exact 3-way bf16 splits; conv1 on the
     16-channel kernel reading conv0's fp32 output, conv2 and conv3 on the 2-D tile kernel, N = 64 /
     128), conv1-conv4 with their 2x2 pools fused, pool5 writing split planes; conv5 (N = 512) in
-    2 K slices whose partials pool5 combines; weights of those layers in 3 bf16 pieces."""
+    2 K slices whose partials pool5 combines; conv8 (1x1) on the 1x1 x3 conv reading conv7's split
+    planes; weights of those layers in 3 bf16 pieces."""
     monkeypatch.delenv("DNN_HIP_X3", raising=False)
     monkeypatch.delenv("DNN_HIP_X3_TILE", raising=False)
     monkeypatch.delenv("DNN_HIP_X3_C16", raising=False)
@@ -191,23 +192,28 @@ def test_plan_x3_structure_host_only(monkeypatch):
     entries = dnn_hip.lower_graph(g)
     wb, sb = dnn_hip.Plan.memory(64, (416, 416, 3), entries)
     nparams = sum(w["kernel"].size for w in ws)
-    x3params = 9 * (16 * 32 + 32 * 64 + 64 * 128 + 128 * 256 + 256 * 512 + 512 * 1024 + 1024 * 1024)
+    x3params = 9 * (16 * 32 + 32 * 64 + 64 * 128 + 128 * 256 + 256 * 512 + 512 * 1024 + 1024 * 1024) + 1024 * 125
     assert wb >= 4 * nparams + 2 * x3params and wb < (4 * nparams + 2 * x3params) * 1.2
     act2 = 2 * 64 * 208 * 208 * 16 * 4
     # one zero-bordered split-plane region per producer: conv1 (pooled 104x104x32), conv2
     # (pooled 52x52x64), conv3 (pooled 26x26x128), conv4 (pooled 13x13x256), pool5 (13x13x512),
-    # conv6 (13x13x1024), 6 B per element
-    pad = sum(64 * 6 * (h + 2) ** 2 * c for h, c in ((104, 32), (52, 64), (26, 128), (13, 256), (13, 512), (13, 1024)))
+    # conv6 and conv7 (13x13x1024 each), 6 B per element
+    pad = sum(64 * 6 * (h + 2) ** 2 * c
+              for h, c in ((104, 32), (52, 64), (26, 128), (13, 256), (13, 512), (13, 1024), (13, 1024)))
     slab = 2 * 64 * 13 * 13 * 512 * 4  # conv5's two raw K-slice partials
     assert act2 + pad + slab <= sb < act2 + pad + slab + 16384
     lines = _describe_yolo(64, False)
     conv = [ln for ln in lines if ln.startswith("conv")]
     assert [i for i, ln in enumerate(conv) if "patch_x3" in ln] == [1, 2, 3, 4, 5, 6, 7]
+    assert "mode=x3_1x1" in conv[8]
     assert "splitK=2 x3-combine" in conv[5] and sum("splitK" in ln for ln in lines) == 1
     assert all("+pool2x2s2" in conv[i] for i in (1, 2, 3, 4))  # pools fused into the x3 convs
     assert sum(ln.startswith("pool") for ln in lines) == 1  # pool5 (s1, combines conv5's slices)
-    # latency plans keep the fp32 MFMA (split-K over the idle chip)
-    assert not any("patch_x3" in ln for ln in _describe_yolo(1, True))
+    # latency plans keep the fp32 MFMA (split-K over the idle chip) but for conv6/conv7 (the
+    # small-M x3 kernel)
+    lat = [ln for ln in _describe_yolo(1, True) if ln.startswith("conv")]
+    assert not any("patch_x3" in ln for ln in lat)
+    assert [i for i, ln in enumerate(lat) if "mode=x3" in ln] == [6, 7]
     # DNN_HIP_X3_TILE=0: conv2/conv3 back on the fp32 MFMA, conv3's pooled epilogue splits;
     # DNN_HIP_X3_C16=0: conv1 on the fp32 patch kernel (its pooled epilogue splits for conv2)
     monkeypatch.setenv("DNN_HIP_X3_TILE", "0")
@@ -322,8 +328,9 @@ def _describe_yolo(batch, latency, env=None):
 
 
 def test_latency_plan_layout():
-    """dnn_plan_set_latency_mode: at batch 1 conv4-conv8 split K (combined in the GEMM, conv4
-    with its pool), conv0/conv1 keep their direct/patch kernels; batch plans are unchanged."""
+    """dnn_plan_set_latency_mode: at batch 1 conv4-conv5 split K (combined in the GEMM, conv4
+    with its pool), conv6/conv7 on the small-M x3 kernel, conv8 split K, conv0/conv1
+    keep their direct/patch kernels; batch plans are unchanged."""
     lat = _describe_yolo(1, True)
     base = _describe_yolo(1, False)
     assert all(l.endswith(" latency") for l in lat if l.startswith("conv"))

@@ -1206,6 +1206,66 @@ def test_x3_conv_vs_oracle(monkeypatch, case):
     assert errs["1"][0] <= 1.25 * errs["0"][0] and errs["1"][1] <= 1.25 * errs["0"][1], errs
 
 
+X3_1X1_CASES = [
+    # B, H, W, C, od1, N: pool (2x2 s1) -> conv3x3 C->od1 (x3, writing split planes) -> conv1x1
+    # od1->N + bias (the 1x1 x3 conv: YOLOv2-tiny's conv8 is 1024->125 on 13x13)
+    (64, 13, 13, 256, 1024, 125),  # conv8's shape at batch 64 (338 row tiles, ragged N panel)
+    (3, 9, 11, 64, 256, 200),      # non-square frame, two N panels (the second ragged), few rows
+]
+
+
+@pytest.mark.parametrize("case", X3_1X1_CASES)
+def test_x3_1x1_conv_vs_oracle(monkeypatch, case):
+    """conv1x1_x3_kernel (MODE_X3_1X1): the 1x1 conv after an x3 conv reads that producer's
+    split planes and runs the x3 arithmetic (two accumulators, six bf16 products per step).
+    Within the fp32 LAYER_TOL of the float64 oracle and at most 1.25x the fp32-MFMA plan's error
+    (DNN_HIP_X3=0: the same layers on the fp32 MFMA), batch rows bit-equal to batch-1 runs,
+    repeat runs identical, and the mode as planned (DNN_HIP_X3_1X1=0 keeps the fp32 GEMM)."""
+    B, H, W, C, od1, N = case
+    rng = np.random.default_rng(B + C + N)
+    x = rng.standard_normal((B, H, W, C)).astype(np.float32)
+    k1 = (rng.standard_normal((3, 3, C, od1)) * np.sqrt(2.0 / (9 * C))).astype(np.float32)
+    k2 = (rng.standard_normal((1, 1, od1, N)) * np.sqrt(2.0 / od1)).astype(np.float32)
+    b1 = rng.standard_normal(od1).astype(np.float32) * 0.1
+    bn1 = (rng.standard_normal(od1).astype(np.float32) * 0.1, rng.uniform(0.5, 1.5, od1).astype(np.float32),
+           rng.uniform(0.5, 1.5, od1).astype(np.float32))
+    b2 = rng.standard_normal(N).astype(np.float32) * 0.1
+
+    def graph(shape):
+        g = dnn_hip.DnnGraphBuilder()
+        y = g.create_input(list(shape))
+        y = g.create_max_pool2d(y, [1, 2, 2, 1], [1, 1, 1, 1], "SAME")
+        y = g.create_conv2d(y, k1, [1, 1, 1, 1], "SAME")
+        y = g.create_bias_add(y, b1)
+        y = g.create_batch_norm(y, *bn1, 1e-5)
+        y = g.create_leaky_relu(y)
+        y = g.create_conv2d(y, k2, [1, 1, 1, 1], "SAME")
+        y = g.create_bias_add(y, b2)
+        g.set_out_node(y)
+        return g
+
+    pooled = R.max_pool2d(x, [1, 2, 2, 1], [1, 1, 1, 1], "SAME")
+    ref1 = R.leaky_relu(R.batch_norm(R.bias_add(R.conv2d(pooled, k1), b1), *bn1, 1e-5))
+    ref = R.bias_add(R.conv2d(ref1, k2), b2)
+    errs = {}
+    for x3, x1 in (("1", "1"), ("0", "1"), ("1", "0")):
+        monkeypatch.setenv("DNN_HIP_X3", x3)
+        monkeypatch.setenv("DNN_HIP_X3_1X1", x1)
+        eng = dnn_hip.DnnInferenceEngine(graph(x.shape), False)
+        desc = eng.plan().describe()
+        assert desc.count("mode=x3_1x1") == (1 if x3 == "1" and x1 == "1" else 0), desc
+        y = eng.run(x)
+        errs[x3 + x1] = R.normwise_err(y, ref)
+        print("x3=%s 1x1=%s normwise err %.3e" % (x3, x1, errs[x3 + x1]))
+        if x3 == "1" and x1 == "1":
+            y0 = dnn_hip.DnnInferenceEngine(graph((1,) + x.shape[1:]), False).run(x[:1])
+            assert np.array_equal(y0, y[:1])
+            assert np.array_equal(eng.run(x), y)
+    for k, e in errs.items():
+        assert e < 2 * LAYER_TOL, (k, errs)
+    assert errs["11"] <= 1.25 * errs["01"], errs
+
+
 X3_CHAIN_CASES = [
     # B, H, W, C0: conv3x3 C0->128 + pool 2x2 s2 (fp32 implicit GEMM writing the x3 split planes)
     # -> conv3x3 128->512 (x3, 2 K slices) -> then "pool" (2x2 s1: pool5's combine) or "conv"
