@@ -200,7 +200,7 @@ constexpr int C0_ROWS_PER_WAVE = 5;  // 20 row DMAs per tile over 4 waves (rows 
 // FL: the epilogue flag set at compile time (-1: runtime `epi.flags`); EVEN: OH and OW even, so
 // no pool window is ragged (YOLO's 416 x 416: the per-window edge selects drop out)
 template <int CIN, int FL = -1, bool EVEN = false>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(256, 7)  // 7 waves per SIMD (<= 72 registers): latency-bound, occupancy pays
 conv0_packed_pool_kernel(const float* __restrict__ in, const float* __restrict__ w, float* __restrict__ out,
                          DirectGeom g, int tilesX, int tilesY, int ntiles, const float* __restrict__ zero,
                          EpiParams epi, uint4 mags) {  // mags: magic numbers of tilesX, tilesY (div_magic)
@@ -241,22 +241,26 @@ conv0_packed_pool_kernel(const float* __restrict__ in, const float* __restrict__
     return Tile{b, tt - b * tilesY, t - tt * tilesX};
   };
   // lane l of a patch row DMA copies float l of the row's 18 * CIN (the row is contiguous in
-  // the NHWC frame); lanes past the frame's edges read the zero page.  Every wave issues
-  // exactly C0_ROWS_PER_WAVE DMAs per tile (rows 18, 19 and the tiles past the end are dummies
-  // from the zero page), so the counted waits below are exact.
+  // the NHWC frame), through a buffer descriptor with 32-bit offsets: lanes past the frame's
+  // edges take an offset past its range, which reads zero.  Every wave issues exactly
+  // C0_ROWS_PER_WAVE DMAs per tile (rows 18, 19 and the tiles past the end are dummies), so
+  // the counted waits below are exact.
+  const auto rsIn = __builtin_amdgcn_make_buffer_rsrc((void*)in, 0, (int)((size_t)g.B * g.H * g.W * CIN * 4), 0x00020000);
+  (void)zero;
   auto issue = [&](const Tile& c, bool valid, int buf) {
     const int x0 = c.tx * SC_T - g.pl, y0 = c.ty * SC_T - g.pt;
     const int px = x0 + lane / CIN;
     const bool xok = valid && (unsigned)px < (unsigned)g.W;
-    const float* rowp = in + (((size_t)c.b * g.H + y0) * g.W + x0) * CIN + lane;
-    const size_t rstride = (size_t)g.W * CIN;
+    const int row0 = (c.b * g.H + y0) * g.W * CIN;  // float index of the tile's patch row 0 (may be < 0)
+    const unsigned lo = (unsigned)((row0 + x0 * CIN + lane) * 4);
+    const unsigned rstride = (unsigned)(g.W * CIN * 4);
 #pragma unroll
     for (int u = 0; u < C0_ROWS_PER_WAVE; ++u) {
       const int r = wid + 4 * u;
-      if (lane < RW) {
-        const bool ok = xok && r < SC_P && (unsigned)(y0 + r) < (unsigned)g.H;
-        lds_dma4_opaque(ok ? rowp + r * rstride : zero, &patch[buf][r * RS]);
-      }
+      const bool ok = xok && r < SC_P && (unsigned)(y0 + r) < (unsigned)g.H;
+      if (lane < RW)  // (lanes past the row would land in the next row's LDS)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsIn, (__attribute__((address_space(3))) void*)&patch[buf][r * RS],
+                                                 4, (int)(ok ? lo + (unsigned)r * rstride : OOB_OFF), 0, 0, 0);
     }
   };
 
@@ -365,15 +369,13 @@ int launch_conv0_mfma(const float* in, const float* w, float* out, const DirectG
   if (g.B == 0) return 0;
   const int tilesX = (g.OW + SC_T - 1) / SC_T, tilesY = (g.OH + SC_T - 1) / SC_T;
   const long long blocks = (long long)g.B * tilesX * tilesY;
-  if ((size_t)g.B * g.PH * g.PW * 16 * sizeof(float) >= OOB_OFF)  // 32-bit store offsets
+  if ((size_t)g.B * g.PH * g.PW * 16 * sizeof(float) >= OOB_OFF ||
+      (size_t)g.B * g.H * g.W * cin * sizeof(float) >= OOB_OFF)  // 32-bit load / store offsets
     return launch_conv0<false, float>(in, w, out, g, cin, epi, s);
   if (blocks > 0x7fffffffLL || g.PH != (g.OH + 1) / 2 || g.PW != (g.OW + 1) / 2) {
     set_error("conv0_packed: unsupported shape");
     return -2;
   }
-  // persistent: 8 workgroups per CU loop over the tiles
-  const long long slots = 8LL * device_cu_count();
-  const unsigned grid = (unsigned)(blocks < slots ? blocks : slots);
   unsigned mx, my;
   int sx, sy;
   magic_u32(tilesX, &mx, &sx);
@@ -383,9 +385,25 @@ int launch_conv0_mfma(const float* in, const float* w, float* out, const DirectG
   constexpr int YOLO = EPI_BIAS | EPI_BN | EPI_LEAKY_F64;
   const bool even = g.OH % 2 == 0 && g.OW % 2 == 0;
   const uint4 mags = make_uint4(mx, (unsigned)sx, my, (unsigned)sy);
-#define C0P(FL_, EV_)                                                                                        \
-  hipLaunchKernelGGL((conv0_packed_pool_kernel<3, FL_, EV_>), dim3(grid), dim3(256), 0, s, in, w, out, g, tilesX, \
-                     tilesY, (int)blocks, zero, epi, mags)
+  // persistent workgroups loop over the tiles: 4 rounds of the occupancy the compiled kernel
+  // allows (7 per CU at 72 registers: 28 per CU, ~6 tiles each), so the dispatcher refills CUs
+  // that finish early.  Measured at batch 64 (workgroups per CU: ms): one resident round 7:
+  // 0.185, 8 (the 8th as a lone second round): 0.168, 14: 0.153, 28: 0.1485, 56: 0.153, one tile
+  // per workgroup (169): 0.184.  DNN_HIP_CONV0_WGS overrides the per-CU count (experiments)
+  auto slots_of = [](const void* kern) {
+    int v = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, kern, 256, 0) != hipSuccess || v < 1) v = 1;
+    v = 4 * (v < 8 ? v : 8);
+    if (const char* e = getenv("DNN_HIP_CONV0_WGS")) v = atoi(e) > 0 ? atoi(e) : v;
+    return (long long)v * device_cu_count();
+  };
+#define C0P(FL_, EV_)                                                                                            \
+  do {                                                                                                           \
+    static const long long slots = slots_of(reinterpret_cast<const void*>(conv0_packed_pool_kernel<3, FL_, EV_>)); \
+    const unsigned grid = (unsigned)(blocks < slots ? blocks : slots);                                           \
+    hipLaunchKernelGGL((conv0_packed_pool_kernel<3, FL_, EV_>), dim3(grid), dim3(256), 0, s, in, w, out, g,     \
+                       tilesX, tilesY, (int)blocks, zero, epi, mags);                                            \
+  } while (0)
   if (epi.flags == YOLO && even)
     C0P(YOLO, true);
   else if (even)
