@@ -76,6 +76,36 @@ __device__ __forceinline__ void split3(float x, unsigned short& s0, unsigned sho
   s2 = bf16_rn(r1 - bf16_f(s1));
 }
 
+// split3 of two values at once, packed (value a in the low half of each word): the same pieces as
+// split3 for every |x| below the bf16 rounding threshold 0x1.ffp127 (x3_split_ok), where the top
+// piece is finite: one v_cvt_pk_bf16_f32 per piece for both values.  Callers check x3_split_ok
+// for a whole wave's values and take split3 otherwise (a wave-uniform branch).
+typedef float x3_f2 __attribute__((ext_vector_type(2)));
+typedef __bf16 x3_b2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ unsigned x3_cvt_pk(float a, float b) {
+  return __builtin_bit_cast(unsigned, __builtin_convertvector((x3_f2){a, b}, x3_b2));
+}
+__device__ __forceinline__ bool x3_split_ok(float x) { return __builtin_fabsf(x) < 0x1.ffp127f; }  // false for NaN
+__device__ __forceinline__ void split3_pair(float a, float b, unsigned& p0, unsigned& p1, unsigned& p2) {
+  p0 = x3_cvt_pk(a, b);
+  const float ra = a - __builtin_bit_cast(float, p0 << 16), rb = b - __builtin_bit_cast(float, p0 & 0xffff0000u);
+  p1 = x3_cvt_pk(ra, rb);
+  p2 = x3_cvt_pk(ra - __builtin_bit_cast(float, p1 << 16), rb - __builtin_bit_cast(float, p1 & 0xffff0000u));
+}
+// the three packed piece words of values (a, b): split3_pair when `fast` (wave-uniform), else split3
+__device__ __forceinline__ void split3_pack2(bool fast, float a, float b, unsigned& p0, unsigned& p1, unsigned& p2) {
+  if (fast) {
+    split3_pair(a, b, p0, p1, p2);
+  } else {
+    unsigned short a0, a1, a2, b0, b1, b2;
+    split3(a, a0, a1, a2);
+    split3(b, b0, b1, b2);
+    p0 = (unsigned)a0 | ((unsigned)b0 << 16);
+    p1 = (unsigned)a1 | ((unsigned)b1 << 16);
+    p2 = (unsigned)a2 | ((unsigned)b2 << 16);
+  }
+}
+
 __device__ __forceinline__ float apply_epilogue(float v, float bias, float mean, float sq, float gamma,
                                                 int flags) {
   if (flags & EPI_BIAS) v = v + bias;

@@ -25,6 +25,12 @@
 #ifndef X3DIAG
 #define X3DIAG 0
 #endif
+// X3STAG (experiments): waves 4-7 (each the SIMD partner of wave w - 4) issue the tap's vector-
+// memory instructions X3STAG row blocks later than waves 0-3, so the two waves of a SIMD do not
+// stall on their issue at the same time (MI355X_MICROARCH "try a stagger")
+#ifndef X3STAG
+#define X3STAG 0
+#endif
 
 namespace dnnhip {
 
@@ -197,16 +203,30 @@ conv3x3_x3_acc2_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __rest
       // the tap's vector-memory instructions spread over its first row blocks (one each: a
       // lone wave stalls ~60 cycles per issue, and waves in step after the chunk barrier would
       // otherwise all stall at once): the next tap's 6 weight fragments, then the DMA pieces
-      static_assert(TM >= 3 * NJ + 2, "row blocks to spread the tap's loads over");
-      if (i < 3 * NJ) {
-        if constexpr ((X3DIAG & 2) != 0)
-          bq[1][i / NJ][i % NJ] = bq[0][i / NJ][i % NJ];  // (the same random weights every tap)
-        else
-          load_b1(s + 1, i / NJ, i % NJ, bq[1][i / NJ][i % NJ]);
-      }
-      if (i == 3 * NJ && !(X3DIAG & 1)) issue_patch(j + 1, t < NQW ? t : NQW - 1, (j + 1) & 1);  // (uniform count per tap)
-      if constexpr (NQW > 9) {  // pieces past NQW rewrite piece NQW - 1
-        if (i == 3 * NJ + 1 && !(X3DIAG & 1)) issue_patch(j + 1, t + 9 < NQW ? t + 9 : NQW - 1, (j + 1) & 1);
+      static_assert(TM >= 3 * NJ + 2 + X3STAG, "row blocks to spread the tap's loads over");
+      auto tap_loads = [&](auto ic) {  // the tap's loads of row-block slot ic
+        constexpr int q = decltype(ic)::value;
+        if constexpr (q < 3 * NJ) {
+          if constexpr ((X3DIAG & 2) != 0)
+            bq[1][q / NJ][q % NJ] = bq[0][q / NJ][q % NJ];  // (the same random weights every tap)
+          else
+            load_b1(s + 1, q / NJ, q % NJ, bq[1][q / NJ][q % NJ]);
+        }
+        if constexpr (q == 3 * NJ && !(X3DIAG & 1)) issue_patch(j + 1, t < NQW ? t : NQW - 1, (j + 1) & 1);  // (uniform count per tap)
+        if constexpr (NQW > 9 && q == 3 * NJ + 1 && !(X3DIAG & 1))  // pieces past NQW rewrite piece NQW - 1
+          issue_patch(j + 1, t + 9 < NQW ? t + 9 : NQW - 1, (j + 1) & 1);
+      };
+      if constexpr (X3STAG == 0) {
+        static_for<0, 3 * NJ + 2>([&](auto qc) {
+          if (i == decltype(qc)::value) tap_loads(qc);
+        });
+      } else {
+        const bool late = wid >= 4;
+        static_for<0, 3 * NJ + 2>([&](auto qc) {
+          constexpr int q = decltype(qc)::value;
+          if (i == q && !late) tap_loads(qc);
+          if (i == q + X3STAG && late) tap_loads(qc);
+        });
       }
       if constexpr (PF) {
         // next block: block i + 1 of this tap, or block 0 of the next tap (after tap 8 the read
@@ -378,15 +398,18 @@ conv3x3_x3_acc2_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __rest
     wait_lgkm0();  // (the stage is rewritten by the next row block)
     if (o >= 0) {
       if (g.out_mode == 1) {
+        bool ok = true;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) ok = ok && x3_split_ok(lo[e]) && x3_split_ok(hi[e]);
+        const bool fast = __builtin_amdgcn_ballot_w64(!ok) == 0;  // (over the active lanes: uniform among them)
         u32x4 q[3];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          unsigned short a0, a1, a2, b0, b1, b2;
-          split3(e < 2 ? lo[2 * e] : hi[2 * e - 4], a0, a1, a2);
-          split3(e < 2 ? lo[2 * e + 1] : hi[2 * e - 3], b0, b1, b2);
-          q[0][e] = (unsigned)a0 | ((unsigned)b0 << 16);
-          q[1][e] = (unsigned)a1 | ((unsigned)b1 << 16);
-          q[2][e] = (unsigned)a2 | ((unsigned)b2 << 16);
+          unsigned w0, w1, w2;
+          split3_pack2(fast, e < 2 ? lo[2 * e] : hi[2 * e - 4], e < 2 ? lo[2 * e + 1] : hi[2 * e - 3], w0, w1, w2);
+          q[0][e] = w0;
+          q[1][e] = w1;
+          q[2][e] = w2;
         }
         bf16_bits* d = out_split + (size_t)o * (3 * N) + (n0 >> 5) * 96 + c8;
 #pragma unroll

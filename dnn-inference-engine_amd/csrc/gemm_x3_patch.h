@@ -101,15 +101,18 @@ __device__ __forceinline__ void x3_pool_split_store(const float* stg, const int*
     if (o < 0) continue;
     const f32x4 lo = *reinterpret_cast<const f32x4*>(stg + wl * X3_STG_ROW + c8);
     const f32x4 hi = *reinterpret_cast<const f32x4*>(stg + wl * X3_STG_ROW + c8 + 4);
+    bool ok = true;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) ok = ok && x3_split_ok(lo[e]) && x3_split_ok(hi[e]);
+    const bool fast = __builtin_amdgcn_ballot_w64(!ok) == 0;  // (pairs of one v_cvt_pk per piece)
     u32x4 q[3];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      unsigned short a0, a1, a2, b0, b1, b2;
-      split3(e < 2 ? lo[2 * e] : hi[2 * e - 4], a0, a1, a2);
-      split3(e < 2 ? lo[2 * e + 1] : hi[2 * e - 3], b0, b1, b2);
-      q[0][e] = (unsigned)a0 | ((unsigned)b0 << 16);
-      q[1][e] = (unsigned)a1 | ((unsigned)b1 << 16);
-      q[2][e] = (unsigned)a2 | ((unsigned)b2 << 16);
+      unsigned w0, w1, w2;
+      split3_pack2(fast, e < 2 ? lo[2 * e] : hi[2 * e - 4], e < 2 ? lo[2 * e + 1] : hi[2 * e - 3], w0, w1, w2);
+      q[0][e] = w0;
+      q[1][e] = w1;
+      q[2][e] = w2;
     }
     bf16_bits* d = out_split + (size_t)o * n3 + col0 + c8;
 #pragma unroll
@@ -715,18 +718,19 @@ conv3x3_x3_c16_kernel(const float* __restrict__ in, const bf16_bits* __restrict_
         v[d] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsA, vo, 0, 0));
         dst[d] = pr * PB + 8 * q;
       }
+      bool ok = true;
+#pragma unroll
+      for (int d = 0; d < SB; ++d)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) ok = ok && x3_split_ok(v[d][c]);
+      const bool fast = __builtin_amdgcn_ballot_w64(!ok) == 0;  // (pairs of one v_cvt_pk per piece)
 #pragma unroll
       for (int d = 0; d < SB; ++d) {
-        unsigned short sp[3][4];
+        uint2 w[3];
+        split3_pack2(fast, v[d][0], v[d][1], w[0].x, w[1].x, w[2].x);
+        split3_pack2(fast, v[d][2], v[d][3], w[0].y, w[1].y, w[2].y);
 #pragma unroll
-        for (int c = 0; c < 4; ++c) split3(v[d][c], sp[0][c], sp[1][c], sp[2][c]);
-#pragma unroll
-        for (int p = 0; p < 3; ++p) {
-          uint2 w;
-          w.x = (unsigned)sp[p][0] | ((unsigned)sp[p][1] << 16);
-          w.y = (unsigned)sp[p][2] | ((unsigned)sp[p][3] << 16);
-          *reinterpret_cast<uint2*>(patch + dst[d] + 32 * p) = w;
-        }
+        for (int p = 0; p < 3; ++p) *reinterpret_cast<uint2*>(patch + dst[d] + 32 * p) = w[p];
       }
     }
   }
