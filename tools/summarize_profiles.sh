@@ -6,7 +6,7 @@ set -e
 R=$1; D=gpurun_out/$2; B=gpurun_out/${3:-$2}; P=profiles
 python3 tools/prof_summary.py --skip 3 --trace $D/fused_trace/fused_trace_kernel_trace.csv \
   --fetch $D/fused_fetch/fused_fetch_counter_collection.csv --write $D/fused_write/fused_write_counter_collection.csv \
-  --note "round ${R#r}: fused fp32 plan (x3 conv1-conv7), bench.py --steps 10 --warmup 3 (trace), --steps 3 --warmup 1 --gather outputs (FETCH_SIZE, WRITE_SIZE passes), MI355X" \
+  --note "round ${R#r}: fused fp32 plan (x3 conv1-conv8), bench.py --steps 10 --warmup 3 (trace), --steps 3 --warmup 1 --gather outputs (FETCH_SIZE, WRITE_SIZE passes), MI355X" \
   --out $P/pmc_summary.json
 python3 tools/prof_summary.py --skip 3 --unfused --trace $D/unf_trace/unf_trace_kernel_trace.csv \
   --fetch $D/unf_fetch/unf_fetch_counter_collection.csv --write $D/unf_write/unf_write_counter_collection.csv \
