@@ -662,7 +662,10 @@ conv3x3_x3_tile_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __rest
 // streaming them from L2 (73 B per MFMA at 2 waves per tile).  One chunk: no double buffer;
 // two workgroups per CU overlap each other's staging.  Same product order per step as the
 // kernels above; 32 columns (WN = 1), WM waves of TM 16-row blocks.
-template <int TH, int TW, int WM, int TM, bool POOL, bool A2 = true>  // A2: as the tile kernel
+// PRE: the input is already split ([B][H+2][W+2][3][16] bf16, zero-bordered: conv0's SPL output),
+// and each patch row (TW + 2 padded pixels x 96 B, contiguous) is LDS-DMA'd as is (the LDS layout
+// is the global one): no staging registers and no split VALU.
+template <int TH, int TW, int WM, int TM, bool POOL, bool A2 = true, bool PRE = false>  // A2: as the tile kernel
 __global__ void __launch_bounds__(64 * WM, 2)  // (waves per SIMD) two: <= 256 registers
 conv3x3_x3_c16_kernel(const float* __restrict__ in, const bf16_bits* __restrict__ Bt, float* __restrict__ out,
                       bf16_bits* __restrict__ out_split, int N, EpiParams epi, int tilesX, int tilesY, X3Geom g,
@@ -699,8 +702,28 @@ conv3x3_x3_c16_kernel(const float* __restrict__ in, const bf16_bits* __restrict_
       *reinterpret_cast<u32x4*>(smem + 16 * e) = w[u];
     }
   }
-  // patch: 16-B fp32 channel quad -> three 8-B bf16 quads (pieces at 32 p + 8 q of the pixel)
-  {
+  if constexpr (PRE) {
+    // one patch row = PW2 padded pixels x 96 B = RQ 16-B units, contiguous in global memory and
+    // in LDS: DMA instruction h of row py moves units 64 h + lane (rows past TH + 2: the last row
+    // again, same bytes to the same place)
+    constexpr int RQ = PW2 * 6, HPR = (RQ + 63) / 64, NROW = TH + 2, RPW = (NROW + WM - 1) / WM;
+    static_assert((PW2 * PB) % 16 == 0, "rows of whole units");
+    const auto rsA = __builtin_amdgcn_make_buffer_rsrc((void*)in, 0, (int)in_bytes, 0x00020000);
+    const unsigned base = (unsigned)(((b * (g.H + 2) + y0) * (g.W + 2) + x0) * 96);  // patch pixel (0, 0)
+#pragma unroll
+    for (int rr = 0; rr < RPW; ++rr) {
+      int py = wm + WM * rr;
+      py = py < NROW ? py : NROW - 1;
+#pragma unroll
+      for (int h = 0; h < HPR; ++h) {
+        if (64 * h + lane < RQ)  // (the DMA's LDS side is lane-linear: lanes past the row stay off)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(
+              rsA, (__attribute__((address_space(3))) void*)(patch + py * PW2 * PB + 1024 * h), 16,
+              (int)(base + (unsigned)(py * (g.W + 2) * 96 + 16 * (64 * h + lane))), 0, 0, 0);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else {  // patch: 16-B fp32 channel quad -> three 8-B bf16 quads (pieces at 32 p + 8 q of the pixel)
     const auto rsA = __builtin_amdgcn_make_buffer_rsrc((void*)in, 0, (int)in_bytes, 0x00020000);
     constexpr int SB = 4;  // items in flight per thread
 #pragma unroll

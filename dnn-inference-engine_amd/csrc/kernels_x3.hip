@@ -421,7 +421,7 @@ int x3_splits(int N, int K) { return (N % 256 == 0 && N > 256 && N <= 512 && (K 
 
 int launch_conv_x3(const bf16_bits* in_split, const bf16_bits* Bt, float* out, bf16_bits* out_split, long long M,
                    int N, int Npad, int K, int H, int W, int C, const EpiParams& epi, hipStream_t stream, int splits,
-                   int pool) {
+                   int pool, bool c16_pre) {
   if (M == 0 || N == 0) return 0;
   // pool: M counts GEMM rows, 4 per pooled pixel
   const int PH = pool ? (H + 1) / 2 : 0, PW = pool ? (W + 1) / 2 : 0;
@@ -450,7 +450,23 @@ int launch_conv_x3(const bf16_bits* in_split, const bf16_bits* Bt, float* out, b
 #define X3C(POOL_, A2_)                                                                                      \
   hipLaunchKernelGGL((conv3x3_x3_c16_kernel<16, 26, 4, 7, POOL_, A2_>), dim3((unsigned)blocks), dim3(256), 0, stream, \
                      in32p, Bt, out, out_split, N, epi, tilesX, tilesY, xg, (unsigned)in32)
-    if (pool && x3_narrow_a2())
+#define X3CP(POOL_, A2_)                                                                                     \
+  hipLaunchKernelGGL((conv3x3_x3_c16_kernel<16, 26, 4, 7, POOL_, A2_, true>), dim3((unsigned)blocks), dim3(256), 0, \
+                     stream, in32p, Bt, out, out_split, N, epi, tilesX, tilesY, xg, (unsigned)in_bytes)
+    if (c16_pre) {  // the producer wrote split planes (conv0's SPL output): DMA-staged patch
+      if (in_bytes >= 0x80000000LL) {
+        set_error("conv_x3 (c16, split input): input too large");
+        return -2;
+      }
+      if (pool && x3_narrow_a2())
+        X3CP(true, true);
+      else if (pool)
+        X3CP(true, false);
+      else if (x3_narrow_a2())
+        X3CP(false, true);
+      else
+        X3CP(false, false);
+    } else if (pool && x3_narrow_a2())
       X3C(true, true);
     else if (pool)
       X3C(true, false);
@@ -459,6 +475,7 @@ int launch_conv_x3(const bf16_bits* in_split, const bf16_bits* Bt, float* out, b
     else
       X3C(false, false);
 #undef X3C
+#undef X3CP
     return check_x3("conv_x3 (c16)");
   }
   if (kind > 0) {

@@ -1494,6 +1494,67 @@ def test_x3_tile_kernel_vs_oracle(monkeypatch, case):
     assert errs["1"] <= 1.25 * errs["0"], errs
 
 
+C16PRE_CASES = [
+    # B, H, W: conv 3->16 + pool 2x2 s2 (conv0's packed kernel) -> 16->32 + pool (the 16-channel
+    # x3 kernel) -> 32->64 (tile kernel)
+    (2, 96, 104),  # whole 16 x 26 tiles of the 16-channel kernel after the pool (48 x 52)
+    (3, 60, 84),   # ragged tiles (30 x 42 after the pool)
+]
+
+
+@pytest.mark.parametrize("case", C16PRE_CASES)
+def test_conv0_split_planes_feed_c16(monkeypatch, case):
+    """conv0's packed kernel storing exact split planes (SPL) and conv1's 16-channel x3 kernel
+    DMA-staging them (PRE): the same pieces as conv1 splitting conv0's fp32 output while staging,
+    so DNN_HIP_X3_C16PRE=1 (off by default) is bit-identical to the default; within the fp32 tolerance of
+    the float64 oracle; batch rows bit-equal to batch-1 runs; negative-gamma channels."""
+    B, H, W = case
+    rng = np.random.default_rng(B * 13 + H + W)
+    x = rng.uniform(0.0, 1.0, (B, H, W, 3)).astype(np.float32)
+
+    def layer(c, od):
+        k = (rng.standard_normal((3, 3, c, od)) * np.sqrt(2.0 / (9 * c))).astype(np.float32)
+        b = rng.standard_normal(od).astype(np.float32) * 0.1
+        gam = rng.uniform(0.5, 1.5, od).astype(np.float32)
+        gam[::5] *= -1
+        return k, b, (rng.standard_normal(od).astype(np.float32) * 0.1, rng.uniform(0.5, 1.5, od).astype(np.float32),
+                      gam)
+
+    layers = [(layer(3, 16), True), (layer(16, 32), True), (layer(32, 64), False)]
+
+    def graph(shape):
+        g = dnn_hip.DnnGraphBuilder()
+        y = g.create_input(list(shape))
+        for (k, b, n), pool in layers:
+            y = g.create_conv2d(y, k, [1, 1, 1, 1], "SAME")
+            y = g.create_bias_add(y, b)
+            y = g.create_batch_norm(y, *n, 1e-5)
+            y = g.create_leaky_relu(y)
+            if pool:
+                y = g.create_max_pool2d(y, [1, 2, 2, 1], [1, 2, 2, 1], "SAME")
+        g.set_out_node(y)
+        return g
+
+    ref = x
+    for (k, b, n), pool in layers:
+        ref = R.leaky_relu(R.batch_norm(R.bias_add(R.conv2d(ref, k), b), *n, 1e-5))
+        if pool:
+            ref = R.max_pool2d(ref, [1, 2, 2, 1], [1, 2, 2, 1], "SAME")
+    outs = {}
+    for pre in ("1", "0"):
+        monkeypatch.setenv("DNN_HIP_X3_C16PRE", pre)
+        eng = dnn_hip.DnnInferenceEngine(graph(x.shape), False)
+        conv = [ln for ln in eng.plan().describe().splitlines() if ln.startswith("conv")]
+        assert "mode=direct" in conv[0] and "mode=patch_x3" in conv[1] and "mode=patch_x3" in conv[2], conv
+        outs[pre] = eng.run(x)
+        if pre == "1":
+            y0 = dnn_hip.DnnInferenceEngine(graph((1,) + x.shape[1:]), False).run(x[:1])
+            assert np.array_equal(y0, outs[pre][:1])
+            assert np.array_equal(eng.run(x), outs[pre])
+    assert np.array_equal(outs["1"], outs["0"])
+    assert R.normwise_err(outs["1"], ref) < 3 * LAYER_TOL
+
+
 def test_x3_patch_variants(tmp_path):
     """The wide-layer x3 kernels (DNN_HIP_X3V, read once per process: each arm in its own process)
     on the whole net at batch 2 (conv4-conv7): the two-accumulator kernel with 224-B and with
