@@ -69,7 +69,15 @@ __device__ __forceinline__ void vm_wait() {
 // register to make room (conv7 -2 %, conv6 -1.5 %, conv4/conv5 -1 %: same-box A/B).
 // FL: the epilogue flag set at compile time (-1: runtime `epi.flags`; the launcher compiles in
 // YOLO's bias + BatchNorm + double-rounded leaky set), same arithmetic either way.
-template <int BM, int NPR, bool POOL, int LP = 224, bool PF = false, int FL = -1>
+// SK (row skew, with PF, 224-B rows, no pool): patch row P (padded position relative to the
+// tile's first) sits at LDS unit 14 P + 4 y, y = (q0 + P) / Wp its image row (q0 = the first
+// row's column): the 3-position step of an image-row wrap then lands on the same bank quad as a
+// 1-position step, so a 16-row fragment's rows keep the conflict-free pattern of consecutive
+// rows across wraps (tools/lds_conflict_model.py: 3.75 -> 0.36 extra cycles per ds_read_b128
+// at 13-wide frames; 4 spare units per image row).  A tap still adds a uniform offset, 224 (dy
+// Wp + dx) + 64 dy bytes: a tap-(0, 0) row's column is < W, so dx never crosses a row.  Costs
+// the image row of each fragment row per use (a float multiply) and a division at DMA issue.
+template <int BM, int NPR, bool POOL, int LP = 224, bool PF = false, int FL = -1, bool SK = false>
 __global__ void __launch_bounds__(512, 2)
 conv3x3_x3_acc2_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __restrict__ Bt, float* __restrict__ out,
                        bf16_bits* __restrict__ out_split, int M, int N, int K, EpiParams epi, int tilesM, X3Geom g,
@@ -78,6 +86,7 @@ conv3x3_x3_acc2_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __rest
   constexpr int NQW = (NPR * LP + NW * 1024 - 1) / (NW * 1024);  // 1-KiB DMA pieces per wave per patch
   constexpr int BUFB = NQW * NW * 1024;                            // one patch buffer (>= NPR LP)
   static_assert(BM % 16 == 0 && LP % 16 == 0 && LP >= RB && NQW <= 18, "shape");
+  static_assert(!SK || (PF && !POOL && LP == 224), "row skew: the prefetching 224-B-row kernel");
   __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * BUFB];
 
   const int lane = threadIdx.x & 63;
@@ -125,11 +134,20 @@ conv3x3_x3_acc2_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __rest
 #pragma unroll
     for (int i = 0; i < TM; ++i) prk[i / 3] |= (unsigned)((prow[i] - 16 * fq) / LP) << (10 * (i % 3));
   }
+  // (SK) q0 and magicW = ceil(2^16 / Wp): floor(n / Wp) = (n magicW) >> 16 for n < 2^16 / Wp
+  // (n = q0 + P < Wp + 1024; the launcher takes SK only for Wp <= 62)
+  const int q0 = SK ? P0 % Wp : 0;
+  const unsigned magicW = SK ? (65536u + (unsigned)Wp - 1u) / (unsigned)Wp : 0u;
   auto rowoff = [&](int i) {  // byte offset of block i's tap-(0, 0) fragment (PF: from prk)
     if constexpr (PF) {
       unsigned w = prk[i / 3];
       asm volatile("" : "+v"(w));  // unpacked per use: hoisted out of the tap loop it is 11 registers again
-      return (int)__umul24((w >> (10 * (i % 3))) & 1023u, (unsigned)LP) + 16 * fq;
+      const unsigned pr = (w >> (10 * (i % 3))) & 1023u;
+      if constexpr (SK) {
+        const unsigned y = __umul24(pr + (unsigned)q0, magicW) >> 16;
+        return (int)(__umul24(pr, (unsigned)LP) + 64u * y) + 16 * fq;
+      }
+      return (int)__umul24(pr, (unsigned)LP) + 16 * fq;
     } else {
       return prow[i];
     }
@@ -143,9 +161,26 @@ conv3x3_x3_acc2_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __rest
   const int rowB = 6 * g.C;
   const auto rsA = __builtin_amdgcn_make_buffer_rsrc((void*)in, 0, (int)in_bytes, 0x00020000);
   const unsigned dsoff = (unsigned)(P0 * rowB + cb * RB);
+  // (SK) LDS unit U holds row P = Wp j + x - q0, unit u, where U + 14 q0 = (14 Wp + 4) j + 14 x + u;
+  // units past a row's 14 (x = Wp: the 4 spare units of an image row) take row P's last unit
+  const unsigned RBU = 14u * (unsigned)Wp + 4u;
+  const float rinvR = SK ? 1.0f / (float)RBU : 0.f;
   auto issue_patch = [&](int chunk, int k, int buf) {
     const unsigned b = 1024u * (unsigned)(wid + NW * k) + 16u * (unsigned)lane;
-    const unsigned r = b / LP, u = (b - r * LP) >> 4;
+    unsigned r, u;
+    if constexpr (SK) {
+      const unsigned V = (b >> 4) + 14u * (unsigned)q0;
+      unsigned jr = (unsigned)((float)V * rinvR);
+      jr = jr * RBU > V ? jr - 1 : (jr + 1) * RBU <= V ? jr + 1 : jr;
+      const unsigned rem = V - jr * RBU;
+      unsigned x = rem / 14u;
+      u = rem - 14u * x;
+      if (x >= (unsigned)Wp) x = Wp - 1, u = 13;
+      r = (unsigned)Wp * jr + x - (unsigned)q0;
+    } else {
+      r = b / LP;
+      u = (b - r * LP) >> 4;
+    }
     __builtin_amdgcn_raw_ptr_buffer_load_lds(
         rsA, (__attribute__((address_space(3))) void*)(smem + buf * BUFB + 1024 * (wid + NW * k)), 16,
         (int)(__umul24(r, (unsigned)rowB) + 16 * u), (int)(dsoff + chunk * RB), 0, 0);
@@ -197,6 +232,8 @@ conv3x3_x3_acc2_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __rest
   for (int s = 0; s < nsteps; ++s) {
     const int toff = (t / 3) * Wp + (t % 3);  // tap (dy, dx) relative to (0, 0)
     const int toffn = t < 8 ? ((t + 1) / 3) * Wp + ((t + 1) % 3) : 0;  // (PF) the next tap's
+    const int toffB = toff * LP + (SK ? 64 * (t / 3) : 0);  // ... in LDS bytes
+    const int toffnB = toffn * LP + (SK && t < 8 ? 64 * ((t + 1) / 3) : 0);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
@@ -231,7 +268,7 @@ conv3x3_x3_acc2_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __rest
       if constexpr (PF) {
         // next block: block i + 1 of this tap, or block 0 of the next tap (after tap 8 the read
         // goes to this chunk's buffer and is repeated from the next one after the barrier)
-        const unsigned char* qn = i + 1 < TM ? P + rowoff(i + 1 < TM ? i + 1 : 0) + toff * LP : P + rowoff(0) + toffn * LP;
+        const unsigned char* qn = i + 1 < TM ? P + rowoff(i + 1 < TM ? i + 1 : 0) + toffB : P + rowoff(0) + toffnB;
         bf16x8 a[3] = {af[0], af[1], af[2]};
 #pragma unroll
         for (int jb = 0; jb < NJ; ++jb) {

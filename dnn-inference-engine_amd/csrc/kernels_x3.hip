@@ -546,6 +546,21 @@ int launch_conv_x3(const bf16_bits* in_split, const bf16_bits* Bt, float* out, b
 #define X3AF(NPR_, POOL_, LP_, PF_, FL_)                                                                          \
   hipLaunchKernelGGL((conv3x3_x3_acc2_kernel<X3_BM, NPR_, POOL_, LP_, PF_, FL_>), grid, dim3(512), 0, stream,      \
                      in_split, Bt, out, out_split, (int)M, N, K, epi, tilesM, xg, (unsigned)in_bytes, (unsigned)b_bytes)
+#define X3AS(FL_)                                                                                                \
+  hipLaunchKernelGGL((conv3x3_x3_acc2_kernel<X3_BM, X3_NPR, false, 224, true, FL_, true>), grid, dim3(512), 0,     \
+                     stream, in_split, Bt, out, out_split, (int)M, N, K, epi, tilesM, xg, (unsigned)in_bytes,     \
+                     (unsigned)b_bytes)
+  // DNN_HIP_X3_SKEW=1: the row-skewed patch layout (gemm_x3_acc2.h SK) where its 14 span + 4 (span /
+  // Wp + 2) units fit the buffer.  Off: it takes the modelled bank conflicts from 3.75 to 0.36
+  // extra cycles per fragment read, but its per-use image-row arithmetic (64 -> 142 VALU per tap)
+  // measured conv7 0.758 -> 0.786 ms, conv6 0.394 -> 0.408 (same box, same bits)
+  static const bool skew_on = [] {
+    const char* e = getenv("DNN_HIP_X3_SKEW");
+    return e && atoi(e) == 1;
+  }();
+  const long long span = skew_on ? x3_span(M, H, W, pool != 0) : 0;
+  const bool skew = skew_on && !pool && W + 2 <= 62 &&
+                    14 * span + 4 * (span / (W + 2) + 2) <= (long long)((X3_NPR * 224 + 8191) / 8192) * 512;
 #define X3A(NPR_, POOL_, LP_, PF_) X3AF(NPR_, POOL_, LP_, PF_, -1)
 #define X3P(NPR_, POOL_)                                                                                       \
   hipLaunchKernelGGL((conv3x3_x3_patch_kernel<X3_BM, NPR_, POOL_>), grid, dim3(512), 0, stream, in_split, Bt, out, \
@@ -565,6 +580,10 @@ int launch_conv_x3(const bf16_bits* in_split, const bf16_bits* Bt, float* out, b
       X3A(X3_NPR_POOL, true, 224, false);
     else
       X3A(X3_NPR, false, 224, false);
+  } else if (skew && epi.flags == (EPI_BIAS | EPI_BN | EPI_LEAKY_F64) && xg.out_mode != 2) {
+    X3AS(EPI_BIAS | EPI_BN | EPI_LEAKY_F64);
+  } else if (skew) {
+    X3AS(-1);
   } else if (epi.flags == (EPI_BIAS | EPI_BN | EPI_LEAKY_F64) && xg.out_mode != 2) {  // YOLO's set compiled in
     if (pool)
       X3AF(X3_NPR_POOL, true, 224, true, EPI_BIAS | EPI_BN | EPI_LEAKY_F64);
@@ -579,6 +598,7 @@ int launch_conv_x3(const bf16_bits* in_split, const bf16_bits* Bt, float* out, b
 #undef X3P
 #undef X3A
 #undef X3AF
+#undef X3AS
   return check_x3("conv_x3");
 }
 
