@@ -199,16 +199,13 @@ constexpr int C0_RS = 56;  // patch row stride (floats) >= 18 * CIN
 constexpr int C0_ROWS_PER_WAVE = 5;  // 20 row DMAs per tile over 4 waves (rows 18, 19 dummies)
 
 // FL: the epilogue flag set at compile time (-1: runtime `epi.flags`); EVEN: OH and OW even, so
-// no pool window is ragged (YOLO's 416 x 416: the per-window edge selects drop out); SPL: store
-// the pooled outputs as exact 3-way bf16 split planes of a zero-bordered [B][PH+2][PW+2][3][16]
-// buffer (96 B per pixel: the layout conv3x3_x3_c16_kernel<PRE> stages by plain LDS-DMA), the
-// same pieces conv1's kernel would otherwise split from the fp32 output while staging
-template <int CIN, int FL = -1, bool EVEN = false, bool SPL = false>
+// no pool window is ragged (YOLO's 416 x 416: the per-window edge selects drop out).  (Round 3's
+// SPL form stored conv1's split planes here: conv1 -15 us, conv0 +23 us; removed, git history.)
+template <int CIN, int FL = -1, bool EVEN = false>
 __global__ void __launch_bounds__(256, 7)  // 7 waves per SIMD (<= 72 registers): latency-bound, occupancy pays
 conv0_packed_pool_kernel(const float* __restrict__ in, const float* __restrict__ w, float* __restrict__ out,
                          DirectGeom g, int tilesX, int tilesY, int ntiles, const float* __restrict__ zero,
-                         EpiParams epi, uint4 mags,  // mags: magic numbers of tilesX, tilesY (div_magic)
-                         bf16_bits* __restrict__ out_split) {
+                         EpiParams epi, uint4 mags) {  // mags: magic numbers of tilesX, tilesY (div_magic)
   constexpr int K = 9 * CIN, KS = (K + 3) / 4, RW = SC_P * CIN, RS = C0_RS;
   static_assert(RW <= RS && RW <= 64, "patch row");
   __shared__ __attribute__((aligned(16))) float patch[3][(4 * C0_ROWS_PER_WAVE) * RS];  // triple buffer
@@ -272,9 +269,8 @@ conv0_packed_pool_kernel(const float* __restrict__ in, const float* __restrict__
   // Two tiles in flight: tile t's rows were issued two iterations ago.  Per wave and tile the
   // VMEM stream is C0_ROWS_PER_WAVE DMAs then ST stores, so when tile t is consumed the ops
   // issued after its DMAs are at most: stores(t-2), DMAs(t+1), stores(t-1).
-  constexpr int ST = SPL ? 3 : 1;
-  const auto orsrc = SPL ? out_rsrc(out_split, (unsigned)((size_t)g.B * (g.PH + 2) * (g.PW + 2) * 96))
-                         : out_rsrc(out, (unsigned)((size_t)g.B * g.PH * g.PW * 16 * sizeof(float)));
+  constexpr int ST = 1;
+  const auto orsrc = out_rsrc(out, (unsigned)((size_t)g.B * g.PH * g.PW * 16 * sizeof(float)));
   const int G = gridDim.x;
   int t = blockIdx.x;
   Tile cur = coords(t < ntiles ? t : 0);
@@ -324,23 +320,7 @@ conv0_packed_pool_kernel(const float* __restrict__ in, const float* __restrict__
       stage[wid][i >> 1][4 * (i & 1) + fp][n] = pool_then_epilogue_t<FL>(v, pb_, pm, ps, pg, epi.flags);
     }
     wait_lgkm0();  // the stage is wave-private
-    if constexpr (SPL) {  // per lane 4 channels of one window: three 8-B stores (one per piece)
-      const int lr = lane >> 5, f = (lane & 31) * 4;
-      const int wy = (y0 >> 1) + 2 * wid + lr, wx = (x0 >> 1) + f / 16;
-      const f32x4 v = *reinterpret_cast<const f32x4*>(&stage[wid][lr][0][0] + f);
-      const bool fast = __builtin_amdgcn_ballot_w64(!(x3_split_ok(v[0]) && x3_split_ok(v[1]) && x3_split_ok(v[2]) &&
-                                                      x3_split_ok(v[3]))) == 0;
-      unsigned q[3][2];
-      split3_pack2(fast, v[0], v[1], q[0][0], q[1][0], q[2][0]);
-      split3_pack2(fast, v[2], v[3], q[0][1], q[1][1], q[2][1]);
-      const unsigned off = (wy < g.PH && wx < g.PW)
-                               ? (unsigned)((((b * (g.PH + 2) + wy + 1) * (g.PW + 2) + wx + 1) * 48 + (f & 15)) * 2)
-                               : OOB_OFF;
-#pragma unroll
-      for (int p = 0; p < 3; ++p)
-        __builtin_amdgcn_raw_buffer_store_b64((u32x2){q[p][0], q[p][1]}, orsrc, off == OOB_OFF ? OOB_OFF : off + 32 * p, 0,
-                                              0);
-    } else {  // one 16-B store per lane (2 window rows x 8 windows x 16 channels per wave)
+    {  // one 16-B store per lane (2 window rows x 8 windows x 16 channels per wave)
       const int lr = lane >> 5, f = (lane & 31) * 4;
       const int wy = (y0 >> 1) + 2 * wid + lr, wxs = (x0 >> 1) + f / 16;
       const unsigned off = (wy < g.PH && wxs < g.PW)
@@ -386,12 +366,7 @@ static int launch_conv0(const float* in, const float* w, OutT* out, const Direct
 }
 
 int launch_conv0_mfma(const float* in, const float* w, float* out, const DirectGeom& g, int cin, const float* zero,
-                      const EpiParams& epi, hipStream_t s, unsigned short* out_split) {
-  if (out_split && (cin != 3 || !zero || (size_t)g.B * (g.PH + 2) * (g.PW + 2) * 96 >= OOB_OFF ||
-                    (size_t)g.B * g.H * g.W * cin * sizeof(float) >= OOB_OFF)) {
-    set_error("conv0_packed: split-plane output needs the packed kernel (cin = 3, < 2 GiB)");
-    return -2;
-  }
+                      const EpiParams& epi, hipStream_t s) {
   if (cin != 3 || !zero || getenv_flag_off("DNN_HIP_CONV0_PACKED"))
     return launch_conv0<false, float>(in, w, out, g, cin, epi, s);
   if (g.B == 0) return 0;
@@ -418,32 +393,32 @@ int launch_conv0_mfma(const float* in, const float* w, float* out, const DirectG
   // that finish early.  Measured at batch 64 (workgroups per CU: ms): one resident round 7:
   // 0.185, 8 (the 8th as a lone second round): 0.168, 14: 0.153, 28: 0.1485, 56: 0.153, one tile
   // per workgroup (169): 0.184.  DNN_HIP_CONV0_WGS overrides the per-CU count (experiments)
-  auto slots_of = [](const void* kern) {
+  // (cached per instantiation and device: the occupancy query and DNN_HIP_CONV0_WGS are read on a
+  // device's first launch, so the grid is fixed per process and device)
+  auto slots_of = [](const void* kern, long long (&cache)[64]) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+    if (cache[dev] > 0) return cache[dev];
     int v = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, kern, 256, 0) != hipSuccess || v < 1) v = 1;
     v = 4 * (v < 8 ? v : 8);
     if (const char* e = getenv("DNN_HIP_CONV0_WGS")) v = atoi(e) > 0 ? atoi(e) : v;
-    return (long long)v * device_cu_count();
+    return cache[dev] = (long long)v * device_cu_count();
   };
-#define C0P(FL_, EV_, SPL_)                                                                                     \
+#define C0P(FL_, EV_)                                                                                           \
   do {                                                                                                           \
-    static const long long slots =                                                                               \
-        slots_of(reinterpret_cast<const void*>(conv0_packed_pool_kernel<3, FL_, EV_, SPL_>));                    \
+    static long long cache[64] = {};                                                                             \
+    const long long slots = slots_of(reinterpret_cast<const void*>(conv0_packed_pool_kernel<3, FL_, EV_>), cache); \
     const unsigned grid = (unsigned)(blocks < slots ? blocks : slots);                                           \
-    hipLaunchKernelGGL((conv0_packed_pool_kernel<3, FL_, EV_, SPL_>), dim3(grid), dim3(256), 0, s, in, w, out, g, \
-                       tilesX, tilesY, (int)blocks, zero, epi, mags, out_split);                                 \
+    hipLaunchKernelGGL((conv0_packed_pool_kernel<3, FL_, EV_>), dim3(grid), dim3(256), 0, s, in, w, out, g, tilesX, \
+                       tilesY, (int)blocks, zero, epi, mags);                                                    \
   } while (0)
-  if (out_split) {
-    if (epi.flags == YOLO && even)
-      C0P(YOLO, true, true);
-    else
-      C0P(-1, false, true);
-  } else if (epi.flags == YOLO && even) {
-    C0P(YOLO, true, false);
+  if (epi.flags == YOLO && even) {
+    C0P(YOLO, true);
   } else if (even) {
-    C0P(-1, true, false);
+    C0P(-1, true);
   } else {
-    C0P(-1, false, false);
+    C0P(-1, false);
   }
 #undef C0P
   hipError_t e = hipGetLastError();

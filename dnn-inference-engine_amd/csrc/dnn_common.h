@@ -236,9 +236,7 @@ int launch_pack_weights_x3(const float* w, unsigned short* out, int K, int N, in
 int x3_splits(int N, int K);  // split-K of an x3 batch-plan layer: a function of (N, K) only
 int launch_conv_x3(const unsigned short* in_split, const unsigned short* Bt, float* out, unsigned short* out_split,
                    long long M, int N, int Npad, int K, int H, int W, int C, const EpiParams& epi, hipStream_t stream,
-                   int splits = 1, int pool = 0, bool c16_pre = false);
-// c16_pre (C = 16): in_split holds the producer's split planes [B][H+2][W+2][3][16] (conv0's
-// SPL output) instead of its fp32 NHWC output
+                   int splits = 1, int pool = 0);
 bool conv_x3_pool_supported(int OC, int C, int H, int W);  // an x3 conv of this size can fuse a 2x2/s2 pool
 // x3 workgroups of a layer (batch-1 latency plans take x3 only where they fill half the chip)
 long long x3_tiles(long long batch, int OH, int OW, int OC, int C, int K);
@@ -265,10 +263,8 @@ int launch_conv3x3_pool2_direct_f16out(const float* in, const float* w, half_t* 
 // conv_small.hip: conv0 on MFMA (cin <= 3, 16 outputs, fp32 frames in, pool fused) and the
 // fp16 path's conv1 patch kernel (C = 16 -> 32, pool fused)
 bool conv0_mfma_supported(int cin, int nout, int kh, int kw, int sh, int sw);
-// out_split != nullptr: the pooled outputs as exact 3-way bf16 split planes of a zero-bordered
-// [B][PH+2][PW+2][3][16] buffer (the next layer is the 16-channel x3 conv; `out` unused)
 int launch_conv0_mfma(const float* in, const float* w, float* out, const DirectGeom& g, int cin, const float* zero,
-                      const EpiParams& epi, hipStream_t s, unsigned short* out_split = nullptr);
+                      const EpiParams& epi, hipStream_t s);
 int launch_conv0_mfma_f16(const float* in, const float* w, half_t* out, const DirectGeom& g, int cin,
                           const EpiParams& epi, hipStream_t s);
 bool conv1_patch_f16_supported(int C, int OC, int H, int W, int OH, int OW, int kh, int kw, int sh, int sw, int pt,

@@ -2,37 +2,36 @@
 // two accumulators per output and no per-step adds: the default kernel of the wide-N layers of
 // the fp32 path (YOLOv2-tiny conv4-conv7), device code only.
 //
-// The round-2 kernel (conv3x3_x3_patch_kernel, DNN_HIP_X3V=1) sums each 32-channel step's five
-// correction products from zero and adds them into the accumulator: 4 v_add per 6 MFMAs, with
-// two waves per SIMD sharing the vector issue of v_mfma_f32_16x16x32_bf16's 16-cycle slot.
-// Here every output keeps TWO accumulators over the whole K range: `accm` takes the main
+// Round 2's kernel summed each 32-channel step's five correction products from zero and added
+// them into the accumulator: 4 v_add per 6 MFMAs, with two waves per SIMD sharing the vector
+// issue of v_mfma_f32_16x16x32_bf16's 16-cycle slot.  Here every output keeps TWO accumulators over the whole K range: `accm` takes the main
 // product a0*b0 of every step, `accc` the five corrections a2b0 + a1b1 + a0b2 + a1b0 + a0b1;
 // the output is accm + accc, one add per output at the end.  The main accumulator still sees
 // one MFMA rounding per step and no longer the per-step add; the corrections (<= 2^-7 of the
 // main product each) are rounded at their own, 2^-8 smaller, magnitude
 // (tests/test_gpu_parity.py::test_x3_conv_vs_oracle holds the error to <= 1.25x the fp32
 // MFMA path's).  Summation order: per output, accm over the steps (chunk-major, tap-minor) of
-// a0 b0; accc over the same steps of (a2b0, a1b1, a1b0, a0b2, a0b1) in that order (PF = false:
-// a2b0, a1b1, a0b2, a1b0, a0b1); then accm + accc.  It depends on (N, K) only (batch rows are
+// a0 b0; accc over the same steps of (a2b0, a1b1, a1b0, a0b2, a0b1) in that order; then
+// accm + accc.  It depends on (N, K) only (batch rows are
 // bit-identical to batch-1 runs).
 #pragma once
 #include "gemm_x3_patch.h"
 
-// X3DIAG (diagnostic builds only, tools/build_diag.sh; wrong results): bit 1 drops the loop's
-// patch DMA (the patch keeps chunk 0), 2 its weight loads (tap 0's weights throughout), 4 the
-// epilogue of fp32-output layers, 8 the chunk barrier.  Operand data stays random: zero operands
-// clock higher and would flatter the variant (MI355X_MICROARCH, DVFS)
+// X3DIAG (diagnostic builds only, tools/build_diag.sh; wrong results unless noted): bit 1 drops
+// the loop's patch DMA (the patch keeps chunk 0), 2 its weight loads (tap 0's weights
+// throughout), 4 the epilogue of fp32-output layers, 8 the chunk barrier; bit 16 (results
+// unchanged) records per workgroup s_memtime / s_memrealtime at the main loop's start and end in
+// x3_diag_stamps (read by dnn_x3_diag_stamps): the in-kernel clock (MI355X_MICROARCH, DVFS item
+// 6).  Operand data stays random: zero operands clock higher and would flatter the variant.
 #ifndef X3DIAG
 #define X3DIAG 0
 #endif
-// X3STAG (experiments): waves 4-7 (each the SIMD partner of wave w - 4) issue the tap's vector-
-// memory instructions X3STAG row blocks later than waves 0-3, so the two waves of a SIMD do not
-// stall on their issue at the same time (MI355X_MICROARCH "try a stagger")
-#ifndef X3STAG
-#define X3STAG 0
-#endif
-
 namespace dnnhip {
+
+#if (X3DIAG & 16) != 0
+constexpr int X3_DIAG_WGS = 8192;
+__device__ unsigned long long x3_diag_stamps[X3_DIAG_WGS * 4];  // [workgroup][t0, r0, t1, r1]
+#endif
 
 template <int I, int N, class F>
 __device__ __forceinline__ void static_for(F&& f) {
@@ -47,53 +46,59 @@ __device__ __forceinline__ void vm_wait() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
+// Tile placement.  L = the XCD-contiguous tile index (xcd_tile: the ~T/8 consecutive values of
+// L run on one XCD).  The M tiles are cut into mg groups of sm = ceil(tilesM / mg), and inside
+// a group the tiles run N-panel-major: with mg = 1 an XCD's range is ~31 M tiles of one N panel
+// (every M row's patch fetched from beyond L2 by the 4 XCDs of its 4 panels); with mg = 4 (the
+// default for 4-panel layers) it is 2 panels x ~16 M tiles: each patch is read by 2 XCDs and each
+// XCD streams 2 panels' weights (tools: per XCD and chunk 1.9 MB from beyond L2 against 2.3).
+// Placement only: any mg gives the same products in the same order.
+__device__ __forceinline__ void x3_tile_of(int L, int tilesM, int mg, int& tm, int& tn, int tilesN) {
+  const int sm = (tilesM + mg - 1) / mg, gsz = sm * tilesN;
+  const int gi = L / gsz, r = L - gi * gsz;
+  const int gm = tilesM - gi * sm < sm ? tilesM - gi * sm : sm;  // >= 1: L < tilesM tilesN
+  tn = r / gm;
+  tm = gi * sm + (r - tn * gm);
+}
+
 // Structure: BM x 256 tiles, 8 waves of BM x 32 (two per SIMD, 256 registers each: the two
 // accumulator sets take 176), the weights of the next tap loaded while this one runs (48), the
-// A fragments read at each row block's start (the partner wave's MFMAs cover the LDS latency),
-// the patch of one 32-channel chunk staged by LDS-DMA into a double buffer (no staging
-// registers), one barrier per chunk.  Why two waves per SIMD: a one-wave-per-SIMD form (4 waves
-// of 176 x 64 with 512 registers, round 3, git history) lost its MFMA pipe to the issue cost of
-// every vector-memory instruction (~60 cycles each: the weight loads alone 12 % of the kernel,
+// patch of one 32-channel chunk staged by LDS-DMA into a double buffer (no staging registers),
+// one barrier per chunk.  Why two waves per SIMD: a one-wave-per-SIMD form (4 waves of 176 x 64
+// with 512 registers, round 3, git history) lost its MFMA pipe to the issue cost of every
+// vector-memory instruction (~60 cycles each: the weight loads alone 12 % of the kernel,
 // measured with diagnostic builds that dropped them), which only a partner wave can cover.
-// LP: LDS bytes per patch row.  192 (the data) costs 7 bank-conflict cycles per fragment read at
-// 13-wide frames, 224 about 4 (tools/lds_conflict_model.py: the two 8-lane halves of each
-// ds_read_b128 lane group then fall on even / odd bank quads for any 8 rows distinct mod 8;
-// the image-row wraps inside a 16-row fragment leave the rest) with plain row-offset addresses
-// (the round-2 kernel's XOR swizzle reaches the same count but costs ~5 VALU per fragment:
-// 0.850 vs 0.826 ms conv7 here, same call).  The padding bytes of each LDS row are whatever
-// follows the chunk in global memory, never read.
-// PF (default): the next row block's A fragments are read inside this block's MFMAs, each piece
-// as soon as this block's last MFMA on that piece has issued (correction order a2b0, a1b1,
-// a1b0, a0b2, a0b1 -- a2 and a1 retire early), so their LDS latency is covered by the wave's
-// own MFMAs rather than by the partner wave's alone; the patch rows are then packed three per
-// register to make room (conv7 -2 %, conv6 -1.5 %, conv4/conv5 -1 %: same-box A/B).
+// LDS rows of LP = 224 bytes (the 192 data bytes; the padding bytes are whatever follows the
+// chunk in global memory, never read): 192-B rows cost 7 bank-conflict cycles per fragment read
+// at 13-wide frames, 224 about 4 (tools/lds_conflict_model.py: the two 8-lane halves of each
+// ds_read_b128 lane group fall on even / odd bank quads for any 8 rows distinct mod 8; the
+// image-row wraps inside a 16-row fragment leave the rest) with plain row-offset addresses.
+// (Measured and removed in round 4, in git history: 192-B rows, an XOR swizzle (~5 VALU per
+// fragment), a row-skewed layout without the wrap conflicts (+64 -> 142 VALU per tap: conv7
+// +3.7 %), a stagger of waves 4-7's loads (+1.6-2.6 %).)
+// The next row block's A fragments are read inside this block's MFMAs, each piece as soon as
+// this block's last MFMA on that piece has issued (correction order a2b0, a1b1, a1b0, a0b2, a0b1
+// -- a2 and a1 retire early), so their LDS latency is covered by the wave's own MFMAs; the patch
+// rows are packed three per register to make room (conv7 -2 %, conv6 -1.5 %).
 // FL: the epilogue flag set at compile time (-1: runtime `epi.flags`; the launcher compiles in
 // YOLO's bias + BatchNorm + double-rounded leaky set), same arithmetic either way.
-// SK (row skew, with PF, 224-B rows, no pool): patch row P (padded position relative to the
-// tile's first) sits at LDS unit 14 P + 4 y, y = (q0 + P) / Wp its image row (q0 = the first
-// row's column): the 3-position step of an image-row wrap then lands on the same bank quad as a
-// 1-position step, so a 16-row fragment's rows keep the conflict-free pattern of consecutive
-// rows across wraps (tools/lds_conflict_model.py: 3.75 -> 0.36 extra cycles per ds_read_b128
-// at 13-wide frames; 4 spare units per image row).  A tap still adds a uniform offset, 224 (dy
-// Wp + dx) + 64 dy bytes: a tap-(0, 0) row's column is < W, so dx never crosses a row.  Costs
-// the image row of each fragment row per use (a float multiply) and a division at DMA issue.
-template <int BM, int NPR, bool POOL, int LP = 224, bool PF = false, int FL = -1, bool SK = false>
+template <int BM, int NPR, bool POOL, int FL = -1>
 __global__ void __launch_bounds__(512, 2)
 conv3x3_x3_acc2_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __restrict__ Bt, float* __restrict__ out,
                        bf16_bits* __restrict__ out_split, int M, int N, int K, EpiParams epi, int tilesM, X3Geom g,
                        unsigned in_bytes, unsigned b_bytes) {
-  constexpr int BN = 256, TM = BM / 16, RB = 192, NJ = 2, NW = 8;
+  constexpr int BN = 256, TM = BM / 16, RB = 192, NJ = 2, NW = 8, LP = 224;
   constexpr int NQW = (NPR * LP + NW * 1024 - 1) / (NW * 1024);  // 1-KiB DMA pieces per wave per patch
   constexpr int BUFB = NQW * NW * 1024;                            // one patch buffer (>= NPR LP)
-  static_assert(BM % 16 == 0 && LP % 16 == 0 && LP >= RB && NQW <= 18, "shape");
-  static_assert(!SK || (PF && !POOL && LP == 224), "row skew: the prefetching 224-B-row kernel");
+  static_assert(BM % 16 == 0 && NQW <= 18 && NPR <= 1023, "shape");
   __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * BUFB];
 
   const int lane = threadIdx.x & 63;
   const int wid = wave_uniform(threadIdx.x >> 6);
   const int tile_s = xcd_tile(blockIdx.x, gridDim.x), ntiles = gridDim.x / g.splits;
-  const int split = tile_s / ntiles, tile = tile_s - split * ntiles;
-  const int tn = tile / tilesM, tm = tile - tn * tilesM;
+  const int split = tile_s / ntiles;
+  int tm, tn;
+  x3_tile_of(tile_s - split * ntiles, tilesM, g.mgroups, tm, tn, N / BN);
   const int m0 = tm * BM, n0 = tn * BN + wid * 32;  // this wave's 32 columns
   const int Wp = g.W + 2, HWo = g.H * g.W;
   auto padded = [&](int m) {
@@ -113,74 +118,36 @@ conv3x3_x3_acc2_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __rest
   };
   const int P0 = pixrow(m0) - (Wp + 1);  // first patch row
 
-  // A fragment of row-block i: byte offset (in a patch buffer) of the lane's tap (0, 0) row + 16 fq
+  // A fragment of row-block i: patch row of the lane's tap (0, 0) (rows past M repeat row M - 1),
+  // packed three per register (10-bit fields: a patch row < NPR <= 1023); unpacked per use
   const int fr = lane & 15, fq = lane >> 4;
-  int prow[TM];
-#pragma unroll
-  for (int i = 0; i < TM; ++i) {
-    int m = m0 + 16 * i + fr;
-    m = m < M ? m : M - 1;
-    prow[i] = (pixrow(m) - P0 - (Wp + 1)) * LP + 16 * fq;
-  }
-
-  // (PF) the rows packed three per register, 10-bit fields (a patch row < NPR <= 1023): the
-  // prefetch's extra live fragments need the 7 registers
   constexpr int NPK = (TM + 2) / 3;
   unsigned prk[NPK];
 #pragma unroll
   for (int k = 0; k < NPK; ++k) prk[k] = 0;
-  if constexpr (PF) {
-    static_assert(NPR <= 1023, "10-bit patch rows");
 #pragma unroll
-    for (int i = 0; i < TM; ++i) prk[i / 3] |= (unsigned)((prow[i] - 16 * fq) / LP) << (10 * (i % 3));
+  for (int i = 0; i < TM; ++i) {
+    int m = m0 + 16 * i + fr;
+    m = m < M ? m : M - 1;
+    prk[i / 3] |= (unsigned)(pixrow(m) - P0 - (Wp + 1)) << (10 * (i % 3));
   }
-  // (SK) q0 and magicW = ceil(2^16 / Wp): floor(n / Wp) = (n magicW) >> 16 for n < 2^16 / Wp
-  // (n = q0 + P < Wp + 1024; the launcher takes SK only for Wp <= 62)
-  const int q0 = SK ? P0 % Wp : 0;
-  const unsigned magicW = SK ? (65536u + (unsigned)Wp - 1u) / (unsigned)Wp : 0u;
-  auto rowoff = [&](int i) {  // byte offset of block i's tap-(0, 0) fragment (PF: from prk)
-    if constexpr (PF) {
-      unsigned w = prk[i / 3];
-      asm volatile("" : "+v"(w));  // unpacked per use: hoisted out of the tap loop it is 11 registers again
-      const unsigned pr = (w >> (10 * (i % 3))) & 1023u;
-      if constexpr (SK) {
-        const unsigned y = __umul24(pr + (unsigned)q0, magicW) >> 16;
-        return (int)(__umul24(pr, (unsigned)LP) + 64u * y) + 16 * fq;
-      }
-      return (int)__umul24(pr, (unsigned)LP) + 16 * fq;
-    } else {
-      return prow[i];
-    }
+  auto rowoff = [&](int i) {  // byte offset of block i's tap-(0, 0) fragment
+    unsigned w = prk[i / 3];
+    asm volatile("" : "+v"(w));  // unpacked per use: hoisted out of the tap loop it is 11 registers again
+    const unsigned pr = (w >> (10 * (i % 3))) & 1023u;
+    return (int)__umul24(pr, (unsigned)LP) + 16 * fq;
   };
 
   // patch DMA: this wave's piece k lands at LDS byte 1024 (wid + 8 k) + 16 lane = patch row r
-  // (LP bytes each: the 192 data bytes of the chunk and, with LP > 192, the next LP - 192 bytes
-  // of global memory as never-read padding), unit u; one 16-B unit from (P0 + r) rowB + chunk
-  // 192 + 16 u.  Per-lane part computed at issue (a few VALU per tap)
+  // (LP bytes each: the 192 data bytes of the chunk and the next LP - 192 bytes of global memory
+  // as never-read padding), unit u; one 16-B unit from (P0 + r) rowB + chunk 192 + 16 u
   const int nk = K / 32, nch = nk / 9 / g.splits, cb = split * nch;
   const int rowB = 6 * g.C;
   const auto rsA = __builtin_amdgcn_make_buffer_rsrc((void*)in, 0, (int)in_bytes, 0x00020000);
   const unsigned dsoff = (unsigned)(P0 * rowB + cb * RB);
-  // (SK) LDS unit U holds row P = Wp j + x - q0, unit u, where U + 14 q0 = (14 Wp + 4) j + 14 x + u;
-  // units past a row's 14 (x = Wp: the 4 spare units of an image row) take row P's last unit
-  const unsigned RBU = 14u * (unsigned)Wp + 4u;
-  const float rinvR = SK ? 1.0f / (float)RBU : 0.f;
   auto issue_patch = [&](int chunk, int k, int buf) {
     const unsigned b = 1024u * (unsigned)(wid + NW * k) + 16u * (unsigned)lane;
-    unsigned r, u;
-    if constexpr (SK) {
-      const unsigned V = (b >> 4) + 14u * (unsigned)q0;
-      unsigned jr = (unsigned)((float)V * rinvR);
-      jr = jr * RBU > V ? jr - 1 : (jr + 1) * RBU <= V ? jr + 1 : jr;
-      const unsigned rem = V - jr * RBU;
-      unsigned x = rem / 14u;
-      u = rem - 14u * x;
-      if (x >= (unsigned)Wp) x = Wp - 1, u = 13;
-      r = (unsigned)Wp * jr + x - (unsigned)q0;
-    } else {
-      r = b / LP;
-      u = (b - r * LP) >> 4;
-    }
+    const unsigned r = b / LP, u = (b - r * LP) >> 4;
     __builtin_amdgcn_raw_ptr_buffer_load_lds(
         rsA, (__attribute__((address_space(3))) void*)(smem + buf * BUFB + 1024 * (wid + NW * k)), 16,
         (int)(__umul24(r, (unsigned)rowB) + 16 * u), (int)(dsoff + chunk * RB), 0, 0);
@@ -215,6 +182,9 @@ conv3x3_x3_acc2_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __rest
   load_b(0, bq[0]);
   vm_wait<0>();
   __syncthreads();
+#if (X3DIAG & 16) != 0
+  const unsigned long long st0 = __builtin_amdgcn_s_memtime(), sr0 = __builtin_amdgcn_s_memrealtime();
+#endif
 
   // Per tap: TM row blocks of 12 MFMAs (per column block the five corrections back to back,
   // then the main product), the first ones also issuing the next tap's weights and DMA pieces
@@ -223,26 +193,24 @@ conv3x3_x3_acc2_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __rest
   const int nsteps = 9 * nch;
   const unsigned char* P = smem;
   int t = 0, j = 0;
-  bf16x8 af[3];  // (PF) the current block's fragments, read during the previous block
+  bf16x8 af[3];  // the current block's fragments, read during the previous block
   auto read_frag = [&](const unsigned char* q, int p) { af[p] = *reinterpret_cast<const bf16x8*>(q + 64 * p); };
-  if constexpr (PF) {
 #pragma unroll
-    for (int p = 0; p < 3; ++p) read_frag(P + rowoff(0), p);
-  }
+  for (int p = 0; p < 3; ++p) read_frag(P + rowoff(0), p);
   for (int s = 0; s < nsteps; ++s) {
     const int toff = (t / 3) * Wp + (t % 3);  // tap (dy, dx) relative to (0, 0)
-    const int toffn = t < 8 ? ((t + 1) / 3) * Wp + ((t + 1) % 3) : 0;  // (PF) the next tap's
-    const int toffB = toff * LP + (SK ? 64 * (t / 3) : 0);  // ... in LDS bytes
-    const int toffnB = toffn * LP + (SK && t < 8 ? 64 * ((t + 1) / 3) : 0);
+    const int toffn = t < 8 ? ((t + 1) / 3) * Wp + ((t + 1) % 3) : 0;  // the next tap's
+    const int toffB = toff * LP, toffnB = toffn * LP;                  // ... in LDS bytes
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       // the tap's vector-memory instructions spread over its first row blocks (one each: a
       // lone wave stalls ~60 cycles per issue, and waves in step after the chunk barrier would
       // otherwise all stall at once): the next tap's 6 weight fragments, then the DMA pieces
-      static_assert(TM >= 3 * NJ + 2 + X3STAG, "row blocks to spread the tap's loads over");
-      auto tap_loads = [&](auto ic) {  // the tap's loads of row-block slot ic
-        constexpr int q = decltype(ic)::value;
+      static_assert(TM >= 3 * NJ + 2, "row blocks to spread the tap's loads over");
+      static_for<0, 3 * NJ + 2>([&](auto qc) {
+        constexpr int q = decltype(qc)::value;
+        if (i != q) return;
         if constexpr (q < 3 * NJ) {
           if constexpr ((X3DIAG & 2) != 0)
             bq[1][q / NJ][q % NJ] = bq[0][q / NJ][q % NJ];  // (the same random weights every tap)
@@ -252,55 +220,25 @@ conv3x3_x3_acc2_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __rest
         if constexpr (q == 3 * NJ && !(X3DIAG & 1)) issue_patch(j + 1, t < NQW ? t : NQW - 1, (j + 1) & 1);  // (uniform count per tap)
         if constexpr (NQW > 9 && q == 3 * NJ + 1 && !(X3DIAG & 1))  // pieces past NQW rewrite piece NQW - 1
           issue_patch(j + 1, t + 9 < NQW ? t + 9 : NQW - 1, (j + 1) & 1);
-      };
-      if constexpr (X3STAG == 0) {
-        static_for<0, 3 * NJ + 2>([&](auto qc) {
-          if (i == decltype(qc)::value) tap_loads(qc);
-        });
-      } else {
-        const bool late = wid >= 4;
-        static_for<0, 3 * NJ + 2>([&](auto qc) {
-          constexpr int q = decltype(qc)::value;
-          if (i == q && !late) tap_loads(qc);
-          if (i == q + X3STAG && late) tap_loads(qc);
-        });
-      }
-      if constexpr (PF) {
-        // next block: block i + 1 of this tap, or block 0 of the next tap (after tap 8 the read
-        // goes to this chunk's buffer and is repeated from the next one after the barrier)
-        const unsigned char* qn = i + 1 < TM ? P + rowoff(i + 1 < TM ? i + 1 : 0) + toffB : P + rowoff(0) + toffnB;
-        bf16x8 a[3] = {af[0], af[1], af[2]};
+      });
+      // next block: block i + 1 of this tap, or block 0 of the next tap (after tap 8 the read
+      // goes to this chunk's buffer and is repeated from the next one after the barrier)
+      const unsigned char* qn = i + 1 < TM ? P + rowoff(i + 1 < TM ? i + 1 : 0) + toffB : P + rowoff(0) + toffnB;
+      bf16x8 a[3] = {af[0], af[1], af[2]};
 #pragma unroll
-        for (int jb = 0; jb < NJ; ++jb) {
-          const bool lastjb = jb == NJ - 1;
-          f32x4 c = accc[i][jb];
-          c = mfma16_bf16(a[2], bq[0][0][jb], c);
-          if (lastjb) read_frag(qn, 2);
-          c = mfma16_bf16(a[1], bq[0][1][jb], c);
-          c = mfma16_bf16(a[1], bq[0][0][jb], c);
-          if (lastjb) read_frag(qn, 1);
-          c = mfma16_bf16(a[0], bq[0][2][jb], c);
-          c = mfma16_bf16(a[0], bq[0][1][jb], c);
-          accc[i][jb] = c;
-          accm[i][jb] = mfma16_bf16(a[0], bq[0][0][jb], accm[i][jb]);
-          if (lastjb) read_frag(qn, 0);
-        }
-      } else {
-        bf16x8 a[3];
-        const unsigned char* q = P + prow[i] + toff * LP;
-#pragma unroll
-        for (int p = 0; p < 3; ++p) a[p] = *reinterpret_cast<const bf16x8*>(q + 64 * p);
-#pragma unroll
-        for (int jb = 0; jb < NJ; ++jb) {
-          f32x4 c = accc[i][jb];
-          c = mfma16_bf16(a[2], bq[0][0][jb], c);
-          c = mfma16_bf16(a[1], bq[0][1][jb], c);
-          c = mfma16_bf16(a[0], bq[0][2][jb], c);
-          c = mfma16_bf16(a[1], bq[0][0][jb], c);
-          c = mfma16_bf16(a[0], bq[0][1][jb], c);
-          accc[i][jb] = c;
-          accm[i][jb] = mfma16_bf16(a[0], bq[0][0][jb], accm[i][jb]);
-        }
+      for (int jb = 0; jb < NJ; ++jb) {
+        const bool lastjb = jb == NJ - 1;
+        f32x4 c = accc[i][jb];
+        c = mfma16_bf16(a[2], bq[0][0][jb], c);
+        if (lastjb) read_frag(qn, 2);
+        c = mfma16_bf16(a[1], bq[0][1][jb], c);
+        c = mfma16_bf16(a[1], bq[0][0][jb], c);
+        if (lastjb) read_frag(qn, 1);
+        c = mfma16_bf16(a[0], bq[0][2][jb], c);
+        c = mfma16_bf16(a[0], bq[0][1][jb], c);
+        accc[i][jb] = c;
+        accm[i][jb] = mfma16_bf16(a[0], bq[0][0][jb], accm[i][jb]);
+        if (lastjb) read_frag(qn, 0);
       }
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -315,13 +253,23 @@ conv3x3_x3_acc2_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __rest
       wait_lgkm0();
       if (!(X3DIAG & 8)) raw_barrier();
       P = smem + (j & 1) * BUFB;
-      if constexpr (PF) {
 #pragma unroll
-        for (int p = 0; p < 3; ++p) read_frag(P + rowoff(0), p);
-      }
+      for (int p = 0; p < 3; ++p) read_frag(P + rowoff(0), p);
     }
   }
   vm_wait<0>();
+#if (X3DIAG & 16) != 0
+  {
+    const unsigned long long st1 = __builtin_amdgcn_s_memtime(), sr1 = __builtin_amdgcn_s_memrealtime();
+    if (threadIdx.x == 0 && blockIdx.x < X3_DIAG_WGS) {  // (vector stores from lane 0)
+      unsigned long long* d = x3_diag_stamps + 4 * blockIdx.x;
+      d[0] = st0;
+      d[1] = sr0;
+      d[2] = st1;
+      d[3] = sr1;
+    }
+  }
+#endif
 
   // epilogue: the reference's fp32 epilogue on accm + accc, then fp32 [M][N], the split planes of
   // the next x3 layer's zero-bordered input, or the raw partial of split-K slice `split`

@@ -16,15 +16,15 @@
 // bf16 (192 B per chunk).  Weights (pack_weights_x3_kernel): [n/16][step][piece][lane][8]
 // with step = chunk * 9 + tap over 32-channel chunks, i.e. MFMA fragment order of
 // v_mfma_f32_16x16x32_bf16 (n = 16 nb + (lane & 15), k = 8 (lane >> 4) + e).
-// Per output and 32-channel step: the corrections a2b0 + a1b1 + a0b2 + a1b0 + a0b1 summed from
-// zero, then (acc + a0b0) + corrections; steps chunk-major, tap-minor.  The order depends on
-// (N, K) only, so batch rows are bit-identical to batch-1 runs; it is not the fp32 MFMA
-// path's order (DNN_HIP_X3=0 selects that path).
+// Per output and 32-channel step: the corrections a2b0 + a1b1 + a0b2 + a1b0 + a0b1 and the main
+// product a0b0 (x3_step: two accumulators, or the round-2 form: corrections summed from zero and
+// added per step); steps chunk-major, tap-minor.  The order depends on (N, K) only, so batch rows
+// are bit-identical to batch-1 runs; it is not the fp32 MFMA path's order (DNN_HIP_X3=0 selects
+// that path).
 //
-// Structure (as conv3x3_f16_patch_kernel, MF = 16): BM x 256 tiles, 8 waves of BM x 32; a tile
-// of BM consecutive output pixels reads one contiguous run of <= NPR padded rows per chunk,
-// staged once into a double-buffered LDS patch (NPR x 192 B) and reused by all 9 taps; the
-// weight fragments go straight from L2 to registers two taps ahead.
+// This file: the layout, the step, the pooled split-plane store and the narrow-layer kernels
+// (2-D output tiles: conv2/conv3; 16 channels: conv1).  The wide-N layers' kernel (conv4-conv7)
+// is conv3x3_x3_acc2_kernel (gemm_x3_acc2.h).
 #pragma once
 #include "gemm_f16.h"
 
@@ -39,7 +39,7 @@ struct X3Geom {
                    // s at out + s*M*N (no epilogue; x3_combine_kernel finishes)
   int splits;      // K split into this many contiguous chunk ranges (grid = tiles x splits)
   int PH, PW;      // POOL kernels: the 2x2/s2 pooled output (rows are pool-window-major)
-  int prio = 0;    // patch kernel: waves 4-7 (the second-dispatched half) at s_setprio 1
+  int mgroups = 1; // wide kernel: tiles placed as mgroups M ranges x all N panels (x3_tile_of)
 };
 
 __device__ __forceinline__ f32x4 mfma16_bf16(bf16x8 a, bf16x8 b, f32x4 c) {
@@ -120,297 +120,14 @@ __device__ __forceinline__ void x3_pool_split_store(const float* stg, const int*
   }
 }
 
-// POOL: a fused 2x2/s2 max pool -- GEMM rows pool-window-major (row 4 w + 2 dy + dx = cell (dy,
-// dx) of pooled pixel w; cells past an odd edge repeat cell (0, 0)), so a lane's 4 accumulator
-// registers (rows 4 q .. 4 q + 3 of its 16 x 16 block) are one window: pooled before the
-// epilogue (pool_then_epilogue, as the fp32 GEMMs' fused pools)
-// Weight ring of 2 steps, patch rows packed three per register (10-bit fields): at 256
-// registers a row table is what the compiler spills, and every reload's vmcnt(0) also drained
-// the weight loads in flight (round 2 measured a 3-step ring with one row per register and an
-// LDS row table: conv7 0.840 / 0.811 ms against 0.791 for this form).  Since round 3 the
-// default for these layers is conv3x3_x3_acc2_kernel (gemm_x3_acc2.h); DNN_HIP_X3V=1 keeps this.
-template <int BM, int NPR, bool POOL = false>
-__global__ void __launch_bounds__(512, 1)
-conv3x3_x3_patch_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __restrict__ Bt, float* __restrict__ out,
-                        bf16_bits* __restrict__ out_split, int M, int N, int K, EpiParams epi, int tilesM, X3Geom g,
-                        unsigned in_bytes, unsigned b_bytes) {
-  constexpr int BN = 256, TM = BM / 16, RB = 192;  // 8 waves of BM x 32; patch row bytes
-  constexpr int SR = 32, PPT = NPR / SR;           // staging: 384 threads = 32 rows x 12 slots
-  static_assert(BM % 16 == 0 && NPR % SR == 0 && PPT >= 1 && PPT <= 16, "shape");
-  constexpr int BD = 2;
-  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * NPR * RB];
-
-  const int lane = threadIdx.x & 63;
-  const int wid = wave_uniform(threadIdx.x >> 6);
-  // tiles N-major inside each XCD's contiguous range: the XCD's CUs share one weight panel
-  const int tile_s = xcd_tile(blockIdx.x, gridDim.x), ntiles = gridDim.x / g.splits;
-  const int split = tile_s / ntiles, tile = tile_s - split * ntiles;
-  const int tn = tile / tilesM, tm = tile - tn * tilesM;
-  const int m0 = tm * BM, n0 = tn * BN + wid * 32;  // this wave's 32 columns
-  const int Wp = g.W + 2, HWo = g.H * g.W;
-  auto padded = [&](int m) {
-    const int b = m / HWo, r = m - b * HWo, oy = r / g.W, ox = r - oy * g.W;
-    return (b * (g.H + 2) + oy + 1) * Wp + ox + 1;
-  };
-  // GEMM row -> padded row of its conv output pixel (raster, or pool-window-major)
-  auto pixrow = [&](int m) {
-    if constexpr (!POOL) {
-      return padded(m);
-    } else {
-      const int w = m >> 2, q = m & 3, PHW = g.PH * g.PW;
-      const int b = w / PHW, r = w - b * PHW, py = r / g.PW, px = r - py * g.PW;
-      int oy = 2 * py + (q >> 1), ox = 2 * px + (q & 1);
-      if (oy >= g.H || ox >= g.W) oy = 2 * py, ox = 2 * px;
-      return (b * (g.H + 2) + oy + 1) * Wp + ox + 1;
-    }
-  };
-  // first patch row (>= 0: p(0) = Wp + 1); row m0 is the tile's smallest in both orders
-  const int P0 = pixrow(m0) - (Wp + 1);
-
-  // A fragment of row-block i: lane's output row 16 i + fr -> patch row of tap (1, 1); its k
-  // slot fq (8 channels) of piece p sits at row*192 + 64 p + 16 (fq ^ ((row >> 1) & 2)).
-  // ds_read_b128 serves lanes in four 16-lane groups, e.g. {0-3, 12-15, 20-27} = rows
-  // r+0..3 and r+12..15 of slot 0 and r+4..11 of slot 1 (MI355X_MICROARCH §LDS); the bank
-  // group (16 B of 64 banks) is 12 row + 4 p + slot mod 16, so the 4 lanes of each row class
-  // mod 4 (rows x, x+4, x+8, x+12: two per slot) must differ in slot: bit 2 of the row flips
-  // from x to x+4, and XOR-ing it into slot bit 1 separates them for any first row (no
-  // conflict for 16 consecutive rows; an image-row wrap inside a fragment costs a few 2-ways)
-  const int fr = lane & 15, fq = lane >> 4;
-  // the patch rows (< NPR <= 1024) packed three per register (10-bit fields)
-  static_assert(NPR <= 1024, "packed patch rows");
-  constexpr int NPW = (TM + 2) / 3;
-  int prow[NPW];
-#pragma unroll
-  for (int i = 0; i < NPW; ++i) prow[i] = 0;
-#pragma unroll
-  for (int i = 0; i < TM; ++i) {
-    int m = m0 + 16 * i + fr;
-    m = m < M ? m : M - 1;
-    prow[i / 3] |= (pixrow(m) - P0) << (10 * (i % 3));
-  }
-
-  // patch staging: thread (tid % 384) owns slot ss = t % 12 of rows t / 12 + 32 u (waves 6, 7
-  // repeat waves 0, 1: no branch, same bytes to the same LDS address)
-  // this split's chunks: [split * nch, (split + 1) * nch) of the K / 288 (the launcher checks
-  // that splits divides them); its first chunk folded into both per-lane offsets
-  const int nk = K / 32, nch = nk / 9 / g.splits, cb = split * nch;
-  const int st = threadIdx.x % 384, srow = st / 12, ss = st - srow * 12;
-  const int rowB = 6 * g.C;  // bytes per padded row (all chunks)
-  const unsigned pvo = (unsigned)((P0 + srow) * rowB + ss * 16 + cb * RB);
-  const int pdst = srow * RB + (ss >> 2) * 64 + 16 * ((ss & 3) ^ ((srow >> 1) & 2));
-  const auto rsA = __builtin_amdgcn_make_buffer_rsrc((void*)in, 0, (int)in_bytes, 0x00020000);
-  u32x4 pst[PPT];
-  auto load_piece = [&](int chunk, int u) {
-    pst[u] = __builtin_amdgcn_raw_buffer_load_b128(rsA, pvo, chunk * RB + u * SR * rowB, 0);
-  };
-  auto store_piece = [&](int buf, int u) {
-    *reinterpret_cast<u32x4*>(smem + buf * NPR * RB + pdst + u * SR * RB) = pst[u];
-  };
-
-  // weight fragments: per (16-column block, step) 3 pieces x 1 KiB, BD - 1 taps ahead (BD = 2:
-  // one tap, ~4k cycles at 2 waves per SIMD, frees 24 registers).  With BD = 2 the ring's
-  // parity flips every chunk (9 taps), so the slot holding the next chunk's first step is
-  // moved into slot 0 after tap 8.
-  static_assert(BD == 2 || BD == 3, "weight ring depth");
-  const unsigned bvo = (unsigned)((n0 / 16) * nk * 3072 + lane * 16 + cb * 9 * 3072);
-  const int bjs = nk * 3072;  // second 16-column block of the wave
-  const auto rsB = __builtin_amdgcn_make_buffer_rsrc((void*)Bt, 0, (int)b_bytes, 0x00020000);
-  bf16x8 bq[BD][3][2];  // [step % BD][piece][column block]
-#pragma unroll
-  for (int a = 0; a < BD; ++a)
-#pragma unroll
-    for (int p = 0; p < 3; ++p)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) bq[a][p][j] = bf16x8{};
-  // unconditional (past the last step: the descriptor's zeros or another panel, never used):
-  // a conditional load would leave every later wait to drain the fresh loads too
-  auto load_b = [&](int s, bf16x8 (&dst)[3][2]) {
-#pragma unroll
-    for (int p = 0; p < 3; ++p)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-        dst[p][j] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rsB, bvo, s * 3072 + p * 1024 + j * bjs, 0));
-  };
-
-  f32x4 acc[TM][2];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-#pragma unroll
-  for (int u = 0; u < PPT; ++u) load_piece(0, u);
-  load_b(0, bq[0]);
-  if constexpr (BD == 3) load_b(1, bq[1]);
-#pragma unroll
-  for (int u = 0; u < PPT; ++u) store_piece(0, u);
-  wait_lgkm0();
-  __syncthreads();
-
-  // piece u of patch j+1: loaded at tap L(u) = 8u / PPT of chunk j, written at tap L(u) + 1
-  auto frag = [&](const unsigned char* P, int i, int toff, bf16x8 (&a)[3]) {
-    int pr = prow[i / 3];
-    asm volatile("" : "+v"(pr));  // keep the taps' addresses from being hoisted
-    pr = (pr >> (10 * (i % 3))) & 1023;
-    const int row = pr + toff;
-    const unsigned char* q = P + row * RB + 16 * (fq ^ ((row >> 1) & 2));  // (shift form: same time)
-#pragma unroll
-    for (int p = 0; p < 3; ++p) a[p] = *reinterpret_cast<const bf16x8*>(q + 64 * p);
-  };
-  // (MI355X_MICROARCH, two waves per SIMD: the younger half loses every VALU arbitration; one
-  // static priority for it, no per-segment flips)
-  if (g.prio && wid >= 4) __builtin_amdgcn_s_setprio(1);
-  for (int j = 0; j < nch; ++j) {
-    const unsigned char* P = smem + (j & 1) * NPR * RB;
-    bf16x8 af[2][3];
-    frag(P, 0, -(Wp + 1), af[0]);
-#pragma unroll
-    for (int t = 0; t < 9; ++t) {
-      const int s = 9 * j + t;
-      const int toff = (t / 3 - 1) * Wp + (t % 3 - 1);
-      const int toff_next = ((t + 1) / 3 - 1) * Wp + ((t + 1) % 3 - 1);
-      // taps are scheduling regions (the scheduler would sink a piece's load to its store)
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int u = 0; u < PPT; ++u)
-        if ((8 * u) / PPT == t) load_piece(j + 1, u);
-      load_b(s + BD - 1, bq[(t + BD - 1) % BD]);
-#pragma unroll
-      for (int u = 0; u < PPT; ++u)
-        if ((8 * u) / PPT + 1 == t) store_piece((j + 1) & 1, u);
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const int cur = i & 1, nxt = cur ^ 1;
-        // the next fragment (row-block i + 1 of this tap, or row-block 0 of the next tap) is
-        // read while this one's 12 MFMAs run
-        if (i + 1 < TM)
-          frag(P, i + 1, toff, af[nxt]);
-        else if (t < 8)
-          frag(P, 0, toff_next, af[nxt]);
-        const bf16x8(&b)[3][2] = bq[t % BD];
-        // the five correction products (<= 2^-7 of the main one) summed from zero in their own
-        // chain, then one add: the accumulator sees two roundings per 32-channel step instead
-        // of six (the bf16 MFMA's internal sum is not round-to-nearest at the accumulator's
-        // magnitude; tests/test_gpu_parity.py::test_x3_conv_vs_oracle).  (Summing the main
-        // product onto the corrections first and adding that once spills 3 KB: the compiler
-        // then keeps the accumulators out of MFMA operands.)
-#pragma unroll
-        for (int jb = 0; jb < 2; ++jb) {
-          f32x4 c = mfma16_bf16(af[cur][2], b[0][jb], f32x4{0.f, 0.f, 0.f, 0.f});
-          c = mfma16_bf16(af[cur][1], b[1][jb], c);
-          c = mfma16_bf16(af[cur][0], b[2][jb], c);
-          c = mfma16_bf16(af[cur][1], b[0][jb], c);
-          c = mfma16_bf16(af[cur][0], b[1][jb], c);
-          const f32x4 m = mfma16_bf16(af[cur][0], b[0][jb], acc[i][jb]);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) acc[i][jb][r] = m[r] + c[r];
-        }
-        // row-block boundaries are scheduling regions: only one block's correction chains
-        // live at a time (the other wave on the SIMD covers the adds' wait for the MFMAs)
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      // TM is odd: the tap's last fragment set lands in af[TM & 1]; re-home it for the next tap
-      if constexpr (TM & 1) {
-        if (t < 8) {
-#pragma unroll
-          for (int p = 0; p < 3; ++p) af[0][p] = af[1][p];
-        }
-      }
-    }
-    if constexpr (BD == 2) {  // the next chunk's first step was loaded into slot 1 at tap 8
-#pragma unroll
-      for (int p = 0; p < 3; ++p)
-#pragma unroll
-        for (int jb = 0; jb < 2; ++jb) bq[0][p][jb] = bq[1][p][jb];
-    }
-    if (j + 1 < nch) {  // patch j+1 written by every wave; every wave done reading patch j
-      wait_lgkm0();
-      raw_barrier();
-    }
-  }
-
-  // epilogue: the reference's fp32 epilogue, then fp32 [M][N] or the split planes of the next
-  // x3 layer's zero-bordered input; output row indices tabulated once in LDS.  (Staging each
-  // wave's 16 x 32 blocks through LDS for 128-B row stores measured slower: conv7 0.850 ->
-  // 0.895 ms, same call; the extra code costs the main loop registers.)
-  int* orow = reinterpret_cast<int*>(smem);
-  __syncthreads();  // every wave is done with the patches
-  if constexpr (POOL) {  // one entry per window: pooled pixel (or its zero-bordered row)
-    if (threadIdx.x < BM / 4) {
-      const int w = (m0 >> 2) + threadIdx.x, PHW = g.PH * g.PW;
-      const int b = w / PHW, r = w - b * PHW, py = r / g.PW, px = r - py * g.PW;
-      orow[threadIdx.x] = 4 * w >= M ? -1 : g.out_mode == 1 ? (b * (g.PH + 2) + py + 1) * (g.PW + 2) + px + 1 : w;
-    }
-    __syncthreads();
-    // (staging the pooled block through LDS for 16-B stores measured equal: conv4 0.133 ms)
-#pragma unroll
-    for (int jb = 0; jb < 2; ++jb) {
-      const int n = n0 + 16 * jb + fr;
-      const float pb = (epi.flags & EPI_BIAS) ? epi.bias[n] : 0.f;
-      const float pm = (epi.flags & (EPI_BN | EPI_BN_AB)) ? epi.mean[n] : 0.f;
-      const float ps = (epi.flags & (EPI_BN | EPI_BN_AB)) ? epi.sq[n] : 1.f;
-      const float pg = (epi.flags & EPI_BN) ? epi.gamma[n] : 1.f;
-      const int cofs = (n >> 5) * 96 + (n & 31);
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const int o = orow[4 * i + fq];
-        if (o < 0) continue;
-        const float v = pool_then_epilogue(acc[i][jb], pb, pm, ps, pg, epi.flags);
-        if (g.out_mode == 1) {
-          unsigned short s0, s1, s2;
-          split3(v, s0, s1, s2);
-          bf16_bits* d = out_split + (size_t)o * (3 * N) + cofs;
-          d[0] = s0;
-          d[32] = s1;
-          d[64] = s2;
-        } else {
-          out[(size_t)o * N + n] = v;
-        }
-      }
-    }
-    return;
-  }
-  if (threadIdx.x < BM) {
-    const int m = m0 + threadIdx.x;
-    orow[threadIdx.x] = m >= M ? -1 : (g.out_mode == 1 ? padded(m) : m);
-  }
-  __syncthreads();
-#pragma unroll
-  for (int jb = 0; jb < 2; ++jb) {
-    const int n = n0 + 16 * jb + fr;  // < N: N % 256 == 0 (launcher)
-    const float pb = (epi.flags & EPI_BIAS) ? epi.bias[n] : 0.f;
-    const float pm = (epi.flags & (EPI_BN | EPI_BN_AB)) ? epi.mean[n] : 0.f;
-    const float ps = (epi.flags & (EPI_BN | EPI_BN_AB)) ? epi.sq[n] : 1.f;
-    const float pg = (epi.flags & EPI_BN) ? epi.gamma[n] : 1.f;
-    const int cofs = (n >> 5) * 96 + (n & 31);  // bf16 offset of piece 0 inside a padded row
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int o = orow[16 * i + 4 * fq + r];
-        if (o < 0) continue;
-        if (g.out_mode == 2) {
-          out[((size_t)split * M + o) * N + n] = acc[i][jb][r];
-          continue;
-        }
-        const float v = apply_epilogue(acc[i][jb][r], pb, pm, ps, pg, epi.flags);
-        if (g.out_mode == 1) {
-          unsigned short s0, s1, s2;
-          split3(v, s0, s1, s2);
-          bf16_bits* d = out_split + (size_t)o * (3 * N) + cofs;
-          d[0] = s0;
-          d[32] = s1;
-          d[64] = s2;
-        } else {
-          out[(size_t)o * N + n] = v;
-        }
-      }
-  }
-}
+// POOL (all x3 conv kernels): a fused 2x2/s2 max pool -- GEMM rows pool-window-major (row 4 w +
+// 2 dy + dx = cell (dy, dx) of pooled pixel w; cells past an odd edge repeat cell (0, 0)), so a
+// lane's 4 accumulator registers (rows 4 q .. 4 q + 3 of its 16 x 16 block) are one window:
+// pooled before the epilogue (pool_then_epilogue, as the fp32 GEMMs' fused pools).
 
 // Narrow layers (N = 64 / 128: YOLOv2-tiny conv2 / conv3, 104x104 and 52x52 frames).  A run of
-// consecutive rows spans whole image rows plus a two-row halo, so on wide frames the kernel
-// above would stage 2.2-5x its tile's pixels (tools: its x3_span); here a workgroup owns a 2-D
+// consecutive rows spans whole image rows plus a two-row halo, so on wide frames the wide
+// kernel (gemm_x3_acc2.h) would stage 2.2-5x its tile's pixels (x3_span); here a workgroup owns a 2-D
 // tile of TH x TW output pixels and 32 WN columns, and stages its (TH + 2) x (TW + 2) patch
 // (1.56x for 4 x 52).  WM x WN waves of TM 16-row blocks x 32 columns; tile rows raster, or
 // pool-window-major (POOL: TH, TW even, so a 2x2 window never leaves its tile).  Same
@@ -662,10 +379,7 @@ conv3x3_x3_tile_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __rest
 // streaming them from L2 (73 B per MFMA at 2 waves per tile).  One chunk: no double buffer;
 // two workgroups per CU overlap each other's staging.  Same product order per step as the
 // kernels above; 32 columns (WN = 1), WM waves of TM 16-row blocks.
-// PRE: the input is already split ([B][H+2][W+2][3][16] bf16, zero-bordered: conv0's SPL output),
-// and each patch row (TW + 2 padded pixels x 96 B, contiguous) is LDS-DMA'd as is (the LDS layout
-// is the global one): no staging registers and no split VALU.
-template <int TH, int TW, int WM, int TM, bool POOL, bool A2 = true, bool PRE = false>  // A2: as the tile kernel
+template <int TH, int TW, int WM, int TM, bool POOL, bool A2 = true>  // A2: as the tile kernel
 __global__ void __launch_bounds__(64 * WM, 2)  // (waves per SIMD) two: <= 256 registers
 conv3x3_x3_c16_kernel(const float* __restrict__ in, const bf16_bits* __restrict__ Bt, float* __restrict__ out,
                       bf16_bits* __restrict__ out_split, int N, EpiParams epi, int tilesX, int tilesY, X3Geom g,
@@ -702,28 +416,7 @@ conv3x3_x3_c16_kernel(const float* __restrict__ in, const bf16_bits* __restrict_
       *reinterpret_cast<u32x4*>(smem + 16 * e) = w[u];
     }
   }
-  if constexpr (PRE) {
-    // one patch row = PW2 padded pixels x 96 B = RQ 16-B units, contiguous in global memory and
-    // in LDS: DMA instruction h of row py moves units 64 h + lane (rows past TH + 2: the last row
-    // again, same bytes to the same place)
-    constexpr int RQ = PW2 * 6, HPR = (RQ + 63) / 64, NROW = TH + 2, RPW = (NROW + WM - 1) / WM;
-    static_assert((PW2 * PB) % 16 == 0, "rows of whole units");
-    const auto rsA = __builtin_amdgcn_make_buffer_rsrc((void*)in, 0, (int)in_bytes, 0x00020000);
-    const unsigned base = (unsigned)(((b * (g.H + 2) + y0) * (g.W + 2) + x0) * 96);  // patch pixel (0, 0)
-#pragma unroll
-    for (int rr = 0; rr < RPW; ++rr) {
-      int py = wm + WM * rr;
-      py = py < NROW ? py : NROW - 1;
-#pragma unroll
-      for (int h = 0; h < HPR; ++h) {
-        if (64 * h + lane < RQ)  // (the DMA's LDS side is lane-linear: lanes past the row stay off)
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(
-              rsA, (__attribute__((address_space(3))) void*)(patch + py * PW2 * PB + 1024 * h), 16,
-              (int)(base + (unsigned)(py * (g.W + 2) * 96 + 16 * (64 * h + lane))), 0, 0, 0);
-      }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  } else {  // patch: 16-B fp32 channel quad -> three 8-B bf16 quads (pieces at 32 p + 8 q of the pixel)
+  {  // patch: 16-B fp32 channel quad -> three 8-B bf16 quads (pieces at 32 p + 8 q of the pixel)
     const auto rsA = __builtin_amdgcn_make_buffer_rsrc((void*)in, 0, (int)in_bytes, 0x00020000);
     constexpr int SB = 4;  // items in flight per thread
 #pragma unroll

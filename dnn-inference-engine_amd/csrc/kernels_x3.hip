@@ -330,16 +330,6 @@ int launch_pack_weights_x3(const float* w, bf16_bits* out, int K, int N, int Npa
 // ---- the conv
 constexpr int X3_BM = 176, X3_NPR = 320;
 
-// the narrow x3 kernels (16-channel and tile kernels) with two accumulators per output and no
-// per-step adds (gemm_x3_patch.h x3_step); DNN_HIP_X3A2=0: the round-2 form
-static bool x3_narrow_a2() {
-  static const bool on = [] {
-    const char* e = getenv("DNN_HIP_X3A2");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-
 // DNN_HIP_X3=0 keeps these layers on the fp32 MFMA (implicit GEMM)
 static bool x3_enabled() {
   const char* e = getenv("DNN_HIP_X3");
@@ -421,7 +411,7 @@ int x3_splits(int N, int K) { return (N % 256 == 0 && N > 256 && N <= 512 && (K 
 
 int launch_conv_x3(const bf16_bits* in_split, const bf16_bits* Bt, float* out, bf16_bits* out_split, long long M,
                    int N, int Npad, int K, int H, int W, int C, const EpiParams& epi, hipStream_t stream, int splits,
-                   int pool, bool c16_pre) {
+                   int pool) {
   if (M == 0 || N == 0) return 0;
   // pool: M counts GEMM rows, 4 per pooled pixel
   const int PH = pool ? (H + 1) / 2 : 0, PW = pool ? (W + 1) / 2 : 0;
@@ -447,35 +437,13 @@ int launch_conv_x3(const bf16_bits* in_split, const bf16_bits* Bt, float* out, b
     const X3Geom xg{H, W, C, out_split ? 1 : 0, 1, PH, PW};
     const float* in32p = reinterpret_cast<const float*>(in_split);
     (void)b16;
-#define X3C(POOL_, A2_)                                                                                      \
-  hipLaunchKernelGGL((conv3x3_x3_c16_kernel<16, 26, 4, 7, POOL_, A2_>), dim3((unsigned)blocks), dim3(256), 0, stream, \
-                     in32p, Bt, out, out_split, N, epi, tilesX, tilesY, xg, (unsigned)in32)
-#define X3CP(POOL_, A2_)                                                                                     \
-  hipLaunchKernelGGL((conv3x3_x3_c16_kernel<16, 26, 4, 7, POOL_, A2_, true>), dim3((unsigned)blocks), dim3(256), 0, \
-                     stream, in32p, Bt, out, out_split, N, epi, tilesX, tilesY, xg, (unsigned)in_bytes)
-    if (c16_pre) {  // the producer wrote split planes (conv0's SPL output): DMA-staged patch
-      if (in_bytes >= 0x80000000LL) {
-        set_error("conv_x3 (c16, split input): input too large");
-        return -2;
-      }
-      if (pool && x3_narrow_a2())
-        X3CP(true, true);
-      else if (pool)
-        X3CP(true, false);
-      else if (x3_narrow_a2())
-        X3CP(false, true);
-      else
-        X3CP(false, false);
-    } else if (pool && x3_narrow_a2())
-      X3C(true, true);
-    else if (pool)
-      X3C(true, false);
-    else if (x3_narrow_a2())
-      X3C(false, true);
+    // (two accumulators per output, gemm_x3_patch.h x3_step)
+    if (pool)
+      hipLaunchKernelGGL((conv3x3_x3_c16_kernel<16, 26, 4, 7, true>), dim3((unsigned)blocks), dim3(256), 0, stream,
+                         in32p, Bt, out, out_split, N, epi, tilesX, tilesY, xg, (unsigned)in32);
     else
-      X3C(false, false);
-#undef X3C
-#undef X3CP
+      hipLaunchKernelGGL((conv3x3_x3_c16_kernel<16, 26, 4, 7, false>), dim3((unsigned)blocks), dim3(256), 0, stream,
+                         in32p, Bt, out, out_split, N, epi, tilesX, tilesY, xg, (unsigned)in32);
     return check_x3("conv_x3 (c16)");
   }
   if (kind > 0) {
@@ -501,13 +469,7 @@ int launch_conv_x3(const bf16_bits* in_split, const bf16_bits* Bt, float* out, b
   hipLaunchKernelGGL((conv3x3_x3_tile_kernel<TH_, TW_, WM, WN, X3T_TM, NBUF, POOL, A2_>), dim3((unsigned)blocks),   \
                      dim3(64 * WM * WN), 0, stream, in_split, Bt, out, out_split, N, K, epi, tilesX, tilesY, tilesN, \
                      xg, (unsigned)in_bytes, (unsigned)b_bytes)
-#define X3T(TH_, TW_, WM, WN, NBUF, POOL) \
-  do {                                    \
-    if (x3_narrow_a2())                   \
-      X3T_(TH_, TW_, WM, WN, NBUF, POOL, true); \
-    else                                  \
-      X3T_(TH_, TW_, WM, WN, NBUF, POOL, false); \
-  } while (0)
+#define X3T(TH_, TW_, WM, WN, NBUF, POOL) X3T_(TH_, TW_, WM, WN, NBUF, POOL, true)
     // (kind 2 keeps the round-2 form: its 3-step weight ring and staging registers leave no
     // room for the second accumulator set)
     if (kind == 2 && pool)
@@ -531,83 +493,40 @@ int launch_conv_x3(const bf16_bits* in_split, const bf16_bits* Bt, float* out, b
     return -2;
   }
   const int tilesM = (int)((M + X3_BM - 1) / X3_BM), tilesN = N / 256;
-  // splits > 1: `out` receives the raw partials [splits][M][N] (x3_combine_kernel finishes)
-  const X3Geom xg{H, W, C, splits > 1 ? 2 : out_split ? 1 : 0, splits, PH, PW, 0};
-  // DNN_HIP_X3V: unset / 0 = the two-accumulator kernel (gemm_x3_acc2.h) with 224-B LDS rows
-  // and the next block's fragments read during this block's MFMAs (PF; measured conv7 -2 %,
-  // conv6 -1.5 % against 3, same box), 2 = the same with 192-B rows (same bits), 3 = without the
-  // fragment prefetch (another correction order), 1 = the round-2 kernel (conv3x3_x3_patch_kernel:
-  // per-step adds; another summation order)
-  static const int var = [] {
-    const char* e = getenv("DNN_HIP_X3V");
-    return e ? atoi(e) : 0;
-  }();
+  // splits > 1: `out` receives the raw partials [splits][M][N] (x3_combine_kernel finishes).
+  // Tile placement (gemm_x3_acc2.h x3_tile_of): mgroups M ranges x all N panels, so each XCD's
+  // tiles cover tilesN / (8 / mgroups) panels; DNN_HIP_X3_MG overrides (experiments: read per
+  // launch, so one process can interleave placements -- placement never changes a bit)
+  const char* mge = getenv("DNN_HIP_X3_MG");
+  const int mg_env = mge ? atoi(mge) : 0;
+  const int mg = mg_env > 0 ? mg_env : (tilesN >= 4 ? 4 : tilesN >= 2 ? 2 : 1);
+  const X3Geom xg{H, W, C, splits > 1 ? 2 : out_split ? 1 : 0, splits, PH, PW, mg < tilesM ? mg : 1};
   const dim3 grid(tilesM * tilesN * (pool ? 1 : splits));
-#define X3AF(NPR_, POOL_, LP_, PF_, FL_)                                                                          \
-  hipLaunchKernelGGL((conv3x3_x3_acc2_kernel<X3_BM, NPR_, POOL_, LP_, PF_, FL_>), grid, dim3(512), 0, stream,      \
-                     in_split, Bt, out, out_split, (int)M, N, K, epi, tilesM, xg, (unsigned)in_bytes, (unsigned)b_bytes)
-#define X3AS(FL_)                                                                                                \
-  hipLaunchKernelGGL((conv3x3_x3_acc2_kernel<X3_BM, X3_NPR, false, 224, true, FL_, true>), grid, dim3(512), 0,     \
-                     stream, in_split, Bt, out, out_split, (int)M, N, K, epi, tilesM, xg, (unsigned)in_bytes,     \
-                     (unsigned)b_bytes)
-  // DNN_HIP_X3_SKEW=1: the row-skewed patch layout (gemm_x3_acc2.h SK) where its 14 span + 4 (span /
-  // Wp + 2) units fit the buffer.  Off: it takes the modelled bank conflicts from 3.75 to 0.36
-  // extra cycles per fragment read, but its per-use image-row arithmetic (64 -> 142 VALU per tap)
-  // measured conv7 0.758 -> 0.786 ms, conv6 0.394 -> 0.408 (same box, same bits)
-  static const bool skew_on = [] {
-    const char* e = getenv("DNN_HIP_X3_SKEW");
-    return e && atoi(e) == 1;
-  }();
-  const long long span = skew_on ? x3_span(M, H, W, pool != 0) : 0;
-  const bool skew = skew_on && !pool && W + 2 <= 62 &&
-                    14 * span + 4 * (span / (W + 2) + 2) <= (long long)((X3_NPR * 224 + 8191) / 8192) * 512;
-#define X3A(NPR_, POOL_, LP_, PF_) X3AF(NPR_, POOL_, LP_, PF_, -1)
-#define X3P(NPR_, POOL_)                                                                                       \
-  hipLaunchKernelGGL((conv3x3_x3_patch_kernel<X3_BM, NPR_, POOL_>), grid, dim3(512), 0, stream, in_split, Bt, out, \
-                     out_split, (int)M, N, K, epi, tilesM, xg, (unsigned)in_bytes, (unsigned)b_bytes)
-  if (var == 1) {
+#define X3AF(NPR_, POOL_, FL_)                                                                                    \
+  hipLaunchKernelGGL((conv3x3_x3_acc2_kernel<X3_BM, NPR_, POOL_, FL_>), grid, dim3(512), 0, stream, in_split, Bt, \
+                     out, out_split, (int)M, N, K, epi, tilesM, xg, (unsigned)in_bytes, (unsigned)b_bytes)
+  if (epi.flags == (EPI_BIAS | EPI_BN | EPI_LEAKY_F64) && xg.out_mode != 2) {  // YOLO's set compiled in
     if (pool)
-      X3P(X3_NPR_POOL, true);
+      X3AF(X3_NPR_POOL, true, EPI_BIAS | EPI_BN | EPI_LEAKY_F64);
     else
-      X3P(X3_NPR, false);
-  } else if (var == 2) {
-    if (pool)
-      X3A(X3_NPR_POOL, true, 192, true);
-    else
-      X3A(X3_NPR, false, 192, true);
-  } else if (var == 3) {
-    if (pool)
-      X3A(X3_NPR_POOL, true, 224, false);
-    else
-      X3A(X3_NPR, false, 224, false);
-  } else if (skew && epi.flags == (EPI_BIAS | EPI_BN | EPI_LEAKY_F64) && xg.out_mode != 2) {
-    X3AS(EPI_BIAS | EPI_BN | EPI_LEAKY_F64);
-  } else if (skew) {
-    X3AS(-1);
-  } else if (epi.flags == (EPI_BIAS | EPI_BN | EPI_LEAKY_F64) && xg.out_mode != 2) {  // YOLO's set compiled in
-    if (pool)
-      X3AF(X3_NPR_POOL, true, 224, true, EPI_BIAS | EPI_BN | EPI_LEAKY_F64);
-    else
-      X3AF(X3_NPR, false, 224, true, EPI_BIAS | EPI_BN | EPI_LEAKY_F64);
+      X3AF(X3_NPR, false, EPI_BIAS | EPI_BN | EPI_LEAKY_F64);
   } else {
     if (pool)
-      X3A(X3_NPR_POOL, true, 224, true);
+      X3AF(X3_NPR_POOL, true, -1);
     else
-      X3A(X3_NPR, false, 224, true);
+      X3AF(X3_NPR, false, -1);
   }
-#undef X3P
-#undef X3A
 #undef X3AF
-#undef X3AS
   return check_x3("conv_x3");
 }
 
 // ---- small-M x3 conv (latency plans, gemm_x3_lat.h): 64-column tiles (NCP = 2), one or two
 // chunks per workgroup, chosen so that a frame's layer is ~256 workgroups: two chunks when the
 // one-chunk grid would be >= 512 (conv7: 16 N tiles x 32 chunks), else one (conv6: 16 x 16).
-// DNN_HIP_X3L_CPW=1|2 forces it.
+// DNN_HIP_X3L_CPW=1|2 forces it.  Read when a plan is built (x3_lat_splits fixes the layer's
+// slice count); the launch derives the chunks per workgroup from that count.
 static int x3_lat_cpw(int N, int K) {
-  const char* e = getenv("DNN_HIP_X3L_CPW");  // (read per call: plans and tests set it per plan)
+  const char* e = getenv("DNN_HIP_X3L_CPW");
   const int force = e ? atoi(e) : 0;
   const int chunks = K / 288;
   if (force == 1 || force == 2) return chunks % force == 0 ? force : 1;
@@ -640,9 +559,9 @@ int launch_conv_x3_lat(const bf16_bits* in_split, const bf16_bits* Bt, float* pa
   const long long per_img = (long long)H * W, nimg = M / per_img;
   const long long in_bytes = (long long)x3_act_bytes(nimg, H, W, C);
   const long long b_bytes = (long long)(Npad / 16) * (K / 32) * 3072;
-  const int cpw = x3_lat_cpw(N, K);
+  const int cpw = splits >= 1 && (K / 288) % splits == 0 ? (K / 288) / splits : 0;  // the plan's x3_lat_splits
   const long long span = M <= 0x7fffffffLL ? x3_span(M, H, W) : 1LL << 40;
-  if (M % per_img != 0 || K != 9 * C || C % 32 != 0 || N % 64 != 0 || Npad != N || splits != (K / 288) / cpw ||
+  if (M % per_img != 0 || K != 9 * C || C % 32 != 0 || N % 64 != 0 || Npad != N || (cpw != 1 && cpw != 2) ||
       in_bytes >= 0x80000000LL || b_bytes >= 0x80000000LL || span > X3_NPR || part == nullptr) {
     set_error("conv_x3_lat: unsupported shape M=%lld N=%d K=%d %dx%dx%d splits=%d", M, N, K, H, W, C, splits);
     return -2;
@@ -715,3 +634,16 @@ int launch_conv_x3_1x1(const bf16_bits* in_split, const bf16_bits* Bt, float* ou
 }
 
 }  // namespace dnnhip
+
+#if (X3DIAG & 16) != 0
+// diagnostic builds (tools/build_diag.sh, X3DIAG bit 16): the wide x3 kernel's per-workgroup
+// stamps [t0, r0, t1, r1] of its last launch (s_memtime / s_memrealtime at the main loop's
+// start and end) copied to host[0 .. 4n)
+extern "C" __attribute__((visibility("default"))) int dnn_x3_diag_stamps(unsigned long long* host, int n) {
+  if (n < 0 || n > dnnhip::X3_DIAG_WGS) return -2;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(dnnhip::x3_diag_stamps), (size_t)n * 4 * sizeof(unsigned long long), 0,
+                             hipMemcpyDeviceToHost) == hipSuccess
+             ? 0
+             : -1;
+}
+#endif

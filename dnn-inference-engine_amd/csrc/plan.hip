@@ -105,7 +105,6 @@ struct PlanLayer {
   int splits = 1;  // split-K partial count (> 1: GEMM writes partials, a reduce kernel finishes)
   bool pool = false;  // a 2x2/stride-2 max pool fused into this conv
   bool x3lat = false;  // MODE_X3 on the small-M kernel (latency plans: launch_conv_x3_lat)
-  bool x3pre = false;  // MODE_X3 with C = 16 reading its producer's split planes (conv0's SPL output)
   bool out_padded = false;  // output written zero-bordered (the next layer is MODE_PATCH16 / MODE_X3;
                             // fp32 plans: as x3 split planes)
   size_t pad_off = 0;       // its zero-bordered output region: float offset inside the pad area
@@ -467,18 +466,8 @@ int dnn_plan_add_conv(dnn_plan* p, int kh, int kw, int od, int stride_h, int str
     // implicit GEMM without split-K (its epilogue splits, EPI_OUT_X3) or the pool-fused patch
     // conv (conv1)
     PlanLayer& prev = p->layers.back();
-    if (L.C == 16) {  // the 16-channel x3 kernel reads the producer's fp32 output (conv1) ...
+    if (L.C == 16) {  // the 16-channel x3 kernel reads the producer's fp32 output (conv1)
       L.mode = MODE_X3;
-      // ... or (DNN_HIP_X3_C16PRE=1), after conv0's packed kernel, the split planes conv0's
-      // epilogue writes (the same pieces, DMA-staged: no split in conv1's staging; same bits).
-      // Off by default: measured conv1 0.179 -> 0.164 ms but conv0 0.148 -> 0.171 ms (three 8-B
-      // piece stores per lane and 1.5x the bytes), net +8 us at batch 64
-      const char* pre = getenv("DNN_HIP_X3_C16PRE");
-      if (pre && atoi(pre) == 1 && prev.type == 0 && prev.mode == MODE_DIRECT && prev.pool && prev.C == 3 &&
-          prev.OC == 16 && prev.OH % 2 == 0 && prev.OW % 2 == 0 && !getenv_flag_off("DNN_HIP_CONV0_PACKED")) {
-        L.x3pre = true;
-        prev.out_padded = true;
-      }
     } else if ((prev.type == 1 && prev.C % 32 == 0) || (prev.type == 0 && prev.mode == MODE_X3) ||
         (prev.type == 0 && prev.mode == MODE_IMPLICIT && prev.pool && prev.splits == 1) ||
         (prev.type == 0 && prev.mode == MODE_PATCH && prev.pool)) {
@@ -863,7 +852,7 @@ int dnn_plan_run(dnn_plan* p, int n, const float* d_in, float* d_out, void* stre
         case MODE_DIRECT: {
           DirectGeom g{n, L.H, L.W, L.OH, L.OW, L.PH, L.PW, L.pt, L.pl};
           rc = conv0_mfma_supported(L.C, L.OC, L.kh, L.kw, L.sh, L.sw)
-                   ? launch_conv0_mfma(cur, wt, dst, g, L.C, zero, epi, s, dsplit)
+                   ? launch_conv0_mfma(cur, wt, dst, g, L.C, zero, epi, s)
                    : launch_conv3x3_pool2_direct(cur, wt, dst, g, L.C, L.OC, epi, s);
           break;
         }
@@ -894,7 +883,7 @@ int dnn_plan_run(dnn_plan* p, int n, const float* d_in, float* d_out, void* stre
             rc = launch_conv_x3(reinterpret_cast<const unsigned short*>(cur),
                                 reinterpret_cast<const unsigned short*>(wt), dsplit ? nullptr : dst, dsplit,
                                 L.pool ? 4LL * n * L.PH * L.PW : Mc, L.OC, L.Npad, L.K, L.H, L.W, L.C, epi, s, 1,
-                                L.pool ? 1 : 0, L.x3pre);
+                                L.pool ? 1 : 0);
           }
           break;
         default:

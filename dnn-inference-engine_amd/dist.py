@@ -298,7 +298,7 @@ class ShardedRunner(object):
     """
 
     def __init__(self, compute, global_batch, in_shape, out_shape, device, dtype=torch.float32, timing=True,
-                 slots=None, gather_mode="sized"):
+                 slots=None, gather_mode="deferred"):
         self.timing = bool(timing)  # per-step HIP timing events for stats()
         if gather_mode not in DetectionGather.MODES:
             raise ValueError(f"gather_mode {gather_mode!r}")
@@ -363,7 +363,9 @@ class ShardedRunner(object):
         cur = torch.cuda.current_stream(dev)
         if self._freed[slot] is not None:
             cur.wait_event(self._freed[slot])
-        ev = [torch.cuda.Event(enable_timing=self.timing) for _ in range(5)]
+        # ev: 0/1 forward, 2 pack done, 3 gather enqueued (deferred: the size exchange), 4 gather
+        # done, 5 payload gather start (deferred mode; the same point as 3 otherwise)
+        ev = [torch.cuda.Event(enable_timing=self.timing) for _ in range(6)]
         out = self._outs[slot]
         ev[0].record(cur)
         self.compute(local_in, out, self.count)
@@ -393,17 +395,22 @@ class ShardedRunner(object):
                                            slots=self.slots, mode=self.gather_mode)
         t0 = time.perf_counter()
         if self.gather_mode == "deferred":
+            # the previous step's payload gather first (its sizes were exchanged a step ago), so
+            # it does not queue on the side stream behind this step's size exchange, which
+            # waits for this step's pack; then this step's size exchange
+            prev, self._deferred = self._deferred, None
+            r = self._complete(prev) if prev is not None else None
             with torch.cuda.stream(self._side):
                 self._side.wait_event(ev[2])
                 ev[3].record(self._side)
                 ha = self._gather.launch_meta(slot, packed, total, counts, self.count)
-            prev, self._deferred = self._deferred, (ha, ev, slot)
-            r = self._complete(prev) if prev is not None else None
+            self._deferred = (ha, ev, slot)
             self._host_blocked += time.perf_counter() - t0
             return r
         with torch.cuda.stream(self._side):
             self._side.wait_event(ev[2])
             ev[3].record(self._side)
+            ev[5].record(self._side)
             gh = self._gather.launch(slot, packed, total, counts, self.count)
             ev[4].record(self._side)
         self._freed[slot] = ev[4]
@@ -417,6 +424,7 @@ class ShardedRunner(object):
         finish earlier, then (rank 0) its detections."""
         ha, ev, slot = deferred
         with torch.cuda.stream(self._side):
+            ev[5].record(self._side)
             gh = self._gather.launch_payload(ha)
             ev[4].record(self._side)
         self._freed[slot] = ev[4]
@@ -450,24 +458,29 @@ class ShardedRunner(object):
                     e[4].synchronize()
                 self._sums[0] += e[0].elapsed_time(e[1])
                 self._sums[1] += e[1].elapsed_time(e[2])
-                self._sums[2] += e[3].elapsed_time(e[4])
+                self._sums[2] += e[5].elapsed_time(e[4])
+                self._sums[3] += e[3].elapsed_time(e[4])
 
     def reset_stats(self):
-        self._evq, self._nsteps, self._sums, self._host_blocked = [], 0, [0.0, 0.0, 0.0], 0.0
+        self._evq, self._nsteps, self._sums, self._host_blocked = [], 0, [0.0, 0.0, 0.0, 0.0], 0.0
         self._deferred = getattr(self, "_deferred", None)
 
     def stats(self):
         """Per-step means (ms) over the steps finished since reset_stats(): forward (run
-        stream), post (postprocess + pack), gather (side stream, from the step's size exchange
-        to its payload gather), host_blocked (host time inside finish_detections /
-        flush_detections).  Call after synchronising."""
+        stream), post (postprocess + pack), gather (side stream: the gather of the detections
+        themselves -- in "deferred" mode the payload gather alone), gather_span (side stream,
+        from the step's first gather operation to its last: in "deferred" mode from the size
+        exchange to the payload gather a step later, so it spans the next step's forward),
+        host_blocked (host time inside finish_detections / flush_detections).  Call after
+        synchronising."""
         self._account(force=True)
         n = self._nsteps
         if n == 0 or not self.timing:
             return {"host_blocked_ms": round(self._host_blocked * 1e3 / max(n, 1), 4), "steps": n}
-        f, p, g = (v / n for v in self._sums)
+        f, p, g, gs = (v / n for v in self._sums)
         return {"forward_ms": round(f, 4), "post_ms": round(p, 4), "gather_ms": round(g, 4),
-                "host_blocked_ms": round(self._host_blocked * 1e3 / n, 4), "steps": n}
+                "gather_span_ms": round(gs, 4), "host_blocked_ms": round(self._host_blocked * 1e3 / n, 4),
+                "steps": n}
 
     def step_detections(self, local_in, post, mode="sized"):
         """One batch ending in detections: local compute, then `post(out, n)` -> (packed

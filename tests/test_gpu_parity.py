@@ -1494,7 +1494,7 @@ def test_x3_tile_kernel_vs_oracle(monkeypatch, case):
     assert errs["1"] <= 1.25 * errs["0"], errs
 
 
-C16PRE_CASES = [
+CHAIN01_CASES = [
     # B, H, W: conv 3->16 + pool 2x2 s2 (conv0's packed kernel) -> 16->32 + pool (the 16-channel
     # x3 kernel) -> 32->64 (tile kernel)
     (2, 96, 104),  # whole 16 x 26 tiles of the 16-channel kernel after the pool (48 x 52)
@@ -1502,12 +1502,12 @@ C16PRE_CASES = [
 ]
 
 
-@pytest.mark.parametrize("case", C16PRE_CASES)
-def test_conv0_split_planes_feed_c16(monkeypatch, case):
-    """conv0's packed kernel storing exact split planes (SPL) and conv1's 16-channel x3 kernel
-    DMA-staging them (PRE): the same pieces as conv1 splitting conv0's fp32 output while staging,
-    so DNN_HIP_X3_C16PRE=1 (off by default) is bit-identical to the default; within the fp32 tolerance of
-    the float64 oracle; batch rows bit-equal to batch-1 runs; negative-gamma channels."""
+@pytest.mark.parametrize("case", CHAIN01_CASES)
+def test_conv0_conv1_chain(case):
+    """conv0's packed kernel (pool fused) -> conv1's 16-channel x3 kernel (splits conv0's fp32
+    output while staging; pool fused) -> a 32-channel x3 tile conv: within the fp32 tolerance of
+    the float64 oracle; batch rows bit-equal to batch-1 runs and repeat runs; negative-gamma
+    channels; whole and ragged 16 x 26 tiles."""
     B, H, W = case
     rng = np.random.default_rng(B * 13 + H + W)
     x = rng.uniform(0.0, 1.0, (B, H, W, 3)).astype(np.float32)
@@ -1540,42 +1540,31 @@ def test_conv0_split_planes_feed_c16(monkeypatch, case):
         ref = R.leaky_relu(R.batch_norm(R.bias_add(R.conv2d(ref, k), b), *n, 1e-5))
         if pool:
             ref = R.max_pool2d(ref, [1, 2, 2, 1], [1, 2, 2, 1], "SAME")
+    eng = dnn_hip.DnnInferenceEngine(graph(x.shape), False)
+    conv = [ln for ln in eng.plan().describe().splitlines() if ln.startswith("conv")]
+    assert "mode=direct" in conv[0] and "mode=patch_x3" in conv[1] and "mode=patch_x3" in conv[2], conv
+    y = eng.run(x)
+    y0 = dnn_hip.DnnInferenceEngine(graph((1,) + x.shape[1:]), False).run(x[:1])
+    assert np.array_equal(y0, y[:1])
+    assert np.array_equal(eng.run(x), y)
+    assert R.normwise_err(y, ref) < 3 * LAYER_TOL
+
+
+def test_x3_tile_placement_same_bits(monkeypatch, golden_frames):
+    """The wide x3 kernel's tile placement (gemm_x3_acc2.h x3_tile_of: mgroups M ranges x all N
+    panels per XCD range; DNN_HIP_X3_MG, read per launch) moves tiles between XCDs only: the whole
+    net at batch 3 (conv4-conv7 on that kernel, conv5 in 2 K slices) gives the same bits for
+    mgroups 1, 2, 3 (ragged groups), 4 (the default for 4 panels) and 8."""
+    x = synth.frames([0, 1, 2])
+    g, _ = yolo_graph.build_graph(dnn_hip.DnnGraphBuilder, synth.yolo_weights(), in_shape=x.shape)
+    eng = dnn_hip.DnnInferenceEngine(g, False)
     outs = {}
-    for pre in ("1", "0"):
-        monkeypatch.setenv("DNN_HIP_X3_C16PRE", pre)
-        eng = dnn_hip.DnnInferenceEngine(graph(x.shape), False)
-        conv = [ln for ln in eng.plan().describe().splitlines() if ln.startswith("conv")]
-        assert "mode=direct" in conv[0] and "mode=patch_x3" in conv[1] and "mode=patch_x3" in conv[2], conv
-        outs[pre] = eng.run(x)
-        if pre == "1":
-            y0 = dnn_hip.DnnInferenceEngine(graph((1,) + x.shape[1:]), False).run(x[:1])
-            assert np.array_equal(y0, outs[pre][:1])
-            assert np.array_equal(eng.run(x), outs[pre])
-    assert np.array_equal(outs["1"], outs["0"])
-    assert R.normwise_err(outs["1"], ref) < 3 * LAYER_TOL
-
-
-def test_x3_patch_variants(tmp_path):
-    """The wide-layer x3 kernels (DNN_HIP_X3V, read once per process: each arm in its own process)
-    on the whole net at batch 2 (conv4-conv7): the two-accumulator kernel with 224-B and with
-    192-B LDS rows (gemm_x3_acc2.h; same products in the same order) give the same bits; the
-    round-2 kernel (per-step adds: another summation order) and the variant without the
-    fragment prefetch (another correction order) agree within the net tolerance."""
-    import subprocess
-    import sys
-
-    tool = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "x3v_out.py")
-    outs = {}
-    for v in ("0", "2", "1", "3"):
-        f = str(tmp_path / ("out%s.npy" % v))
-        env = dict(os.environ, DNN_HIP_X3V=v)
-        subprocess.run([sys.executable, tool, f, "2"], env=env, check=True, timeout=110)
-        outs[v] = np.load(f)
-    assert outs["0"].shape == (2, 13, 13, 125)
-    assert np.isfinite(outs["0"]).all()
-    assert np.array_equal(outs["0"], outs["2"])
-    assert R.normwise_err(outs["1"], outs["0"]) < NET_TOL
-    assert R.normwise_err(outs["3"], outs["0"]) < NET_TOL
+    for mg in ("1", "2", "3", "4", "8"):
+        monkeypatch.setenv("DNN_HIP_X3_MG", mg)
+        outs[mg] = eng.run(x)
+    for mg in outs:
+        assert np.array_equal(outs[mg], outs["4"]), mg
+    assert R.normwise_err(outs["4"][:1], golden_frames[0]) < NET_TOL
 
 
 @pytest.mark.parametrize("kind", ["huge", "tiny"])

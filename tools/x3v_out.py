@@ -1,6 +1,6 @@
 """Write the YOLOv2-tiny output (batch argv[2], default 16; precision argv[3], default fp32) of
-the default plan to argv[1] (.npy), for tests/test_gpu_parity.py::test_x3_patch_variants and
-::test_patch16_variants (one process per DNN_HIP_X3V / DNN_HIP_P16V arm: read once per process)."""
+the default plan to argv[1] (.npy), for
+variant A/B runs (one process per arm of a switch read once per process)."""
 import os
 import sys
 
