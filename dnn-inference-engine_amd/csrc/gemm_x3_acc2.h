@@ -49,9 +49,10 @@ __device__ __forceinline__ void vm_wait() {
 // Tile placement.  L = the XCD-contiguous tile index (xcd_tile: the ~T/8 consecutive values of
 // L run on one XCD).  The M tiles are cut into mg groups of sm = ceil(tilesM / mg), and inside
 // a group the tiles run N-panel-major: with mg = 1 an XCD's range is ~31 M tiles of one N panel
-// (every M row's patch fetched from beyond L2 by the 4 XCDs of its 4 panels); with mg = 4 (the
-// default for 4-panel layers) it is 2 panels x ~16 M tiles: each patch is read by 2 XCDs and each
-// XCD streams 2 panels' weights (tools: per XCD and chunk 1.9 MB from beyond L2 against 2.3).
+// (every M row's patch fetched from beyond L2 by the 4 XCDs of its 4 panels); with mg = 4 it is
+// 2 panels x ~16 M tiles: each patch is read by 2 XCDs and each XCD streams 2 panels' weights
+// (per XCD and chunk 1.9 MB from beyond L2 against 2.3).  Measured (round 4, tools/x3_ab.py,
+// interleaved in one process): mg = 1, 2, 4 within 0.5 % on conv4-conv7, so the default stays 1.
 // Placement only: any mg gives the same products in the same order.
 __device__ __forceinline__ void x3_tile_of(int L, int tilesM, int mg, int& tm, int& tn, int tilesN) {
   const int sm = (tilesM + mg - 1) / mg, gsz = sm * tilesN;

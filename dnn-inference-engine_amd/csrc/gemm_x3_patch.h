@@ -593,4 +593,293 @@ conv3x3_x3_c16_kernel(const float* __restrict__ in, const bf16_bits* __restrict_
   }
 }
 
+
+// 16-channel layers, persistent (conv1): the 16-channel kernel's tile (TH x TW = 16 x 26 output
+// pixels, 4 waves of 7 row blocks, 32 columns, pool-window-major rows) and fragments, but each
+// workgroup (two per CU) loops over tiles t, t + G, ...: the 30 KB of weights are copied into LDS
+// once per workgroup instead of once per tile, and the next tile's fp32 patch (8 x 16 B per
+// thread) is loaded into registers right after this tile's split is written, so its latency runs
+// under this tile's MFMAs; the other workgroup on the CU computes while this one splits and
+// stores.  Per tile: split -> barrier -> MFMAs -> barrier -> epilogue (its stage in the patch
+// area) -> barrier.  HALF: the last K step (tap 8 alone: k 128-143) on v_mfma_f32_16x16x16_bf16
+// instead of a 16x16x32 step whose upper half is a zero tap -- 27 instead of 30 16x16x32-sized
+// MFMAs per block and column block, if the K = 16 form issues in half the cycles.  Summation
+// order: as the 16-channel kernel (two accumulators; steps 0-4), the order depending on (N, K)
+// only.  LDS: 30 KB weights + 48 KB split patch + 1.7 KB row table = 79 KB (two per CU).
+template <bool POOL, bool HALF>
+__global__ void __launch_bounds__(256, 2)
+conv3x3_x3_c16p_kernel(const float* __restrict__ in, const bf16_bits* __restrict__ Bt, float* __restrict__ out,
+                       bf16_bits* __restrict__ out_split, int N, EpiParams epi, int tilesX, int tilesY, int ntiles,
+                       X3Geom g, unsigned in_bytes) {
+  constexpr int TH = 16, TW = 26, WM = 4, TM = 7;
+  constexpr int NT = 64 * WM, PB = 96, PW2 = TW + 2, PR = (TH + 2) * PW2, T = TH * TW, NS = 5;
+  constexpr int ITEMS = PR * 4, PPT = (ITEMS + NT - 1) / NT;  // item = (patch pixel, channel quad)
+  constexpr int BB = 2 * NS * 3 * 1024, BPT = (BB / 16 + NT - 1) / NT;
+  constexpr int NO = POOL ? T / 4 : T;
+  constexpr int PATCH = PR * PB;
+  static_assert(WM * TM * 16 >= T && (WM * TM - 3) * 16 < T && PPT == 8, "shape");
+  static_assert(WM * TM * 4 * X3_STG_ROW * 4 <= PATCH, "epilogue stage inside the patch area");
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[BB + PATCH + NO * 4];
+  unsigned char* const patch = smem + BB;
+  int* const orow = reinterpret_cast<int*>(smem + BB + PATCH);
+
+  const int lane = threadIdx.x & 63;
+  const int wm = wave_uniform(threadIdx.x >> 6);
+  const int fr = lane & 15, fq = lane >> 4, th = fq >> 1;
+  const int Wp = g.W + 2;
+
+  // weights once: the packed [n/16][step][piece][lane][8] block of columns 0-31 is contiguous
+  {
+    u32x4 w[BPT];
+#pragma unroll
+    for (int u = 0; u < BPT; ++u) {
+      int e = threadIdx.x + u * NT;
+      e = e < BB / 16 ? e : BB / 16 - 1;
+      w[u] = *reinterpret_cast<const u32x4*>(reinterpret_cast<const unsigned char*>(Bt) + 16 * e);
+    }
+#pragma unroll
+    for (int u = 0; u < BPT; ++u) {
+      int e = threadIdx.x + u * NT;
+      e = e < BB / 16 ? e : BB / 16 - 1;
+      *reinterpret_cast<u32x4*>(smem + 16 * e) = w[u];
+    }
+  }
+
+  // per-lane patch items (fixed per thread): pixel pr, channel quad q; dst in the split patch
+  const auto rsA = __builtin_amdgcn_make_buffer_rsrc((void*)in, 0, (int)in_bytes, 0x00020000);
+  auto tile_xy = [&](int t, int& b, int& y0, int& x0) {
+    const int tx = t % tilesX, tt = t / tilesX, ty = tt % tilesY;
+    b = tt / tilesY;
+    y0 = ty * TH;
+    x0 = tx * TW;
+  };
+  f32x4 stg[PPT];
+  auto load_tile = [&](int t) {
+    int b, y0, x0;
+    tile_xy(t, b, y0, x0);
+#pragma unroll
+    for (int d = 0; d < PPT; ++d) {
+      int e = threadIdx.x + d * NT;
+      e = e < ITEMS ? e : ITEMS - 1;
+      const int pr = e >> 2, q = e & 3, py = pr / PW2, px = pr - py * PW2;
+      const int iy = y0 - 1 + py, ix = x0 - 1 + px;
+      const bool ok = (unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W;
+      const unsigned vo = ok ? (unsigned)((((b * g.H + iy) * g.W + ix) * 16 + 4 * q) * 4) : OOB_OFF;
+      stg[d] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsA, vo, 0, 0));
+    }
+  };
+  auto split_tile = [&]() {  // 16-B fp32 channel quad -> three 8-B bf16 quads (pieces at 32 p + 8 q)
+    bool ok = true;
+#pragma unroll
+    for (int d = 0; d < PPT; ++d)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) ok = ok && x3_split_ok(stg[d][c]);
+    const bool fast = __builtin_amdgcn_ballot_w64(!ok) == 0;  // (pairs of one v_cvt_pk per piece)
+#pragma unroll
+    for (int d = 0; d < PPT; ++d) {
+      int e = threadIdx.x + d * NT;
+      e = e < ITEMS ? e : ITEMS - 1;
+      const int dst = (e >> 2) * PB + 8 * (e & 3);
+      uint2 w[3];
+      split3_pack2(fast, stg[d][0], stg[d][1], w[0].x, w[1].x, w[2].x);
+      split3_pack2(fast, stg[d][2], stg[d][3], w[0].y, w[1].y, w[2].y);
+#pragma unroll
+      for (int p = 0; p < 3; ++p) *reinterpret_cast<uint2*>(patch + dst + 32 * p) = w[p];
+    }
+  };
+
+  // fragment rows (fixed per lane): the pixel of tap (1, 1) of row (wm TM + i) 16 + fr
+  // (packed two per register: byte offsets < PR PB < 2^16; the other offsets are uniform or per lane)
+  constexpr int NPP = (TM + 1) / 2;
+  static_assert(PR * PB < 65536, "16-bit patch offsets");
+  unsigned prow2[NPP];
+#pragma unroll
+  for (int k = 0; k < NPP; ++k) prow2[k] = 0;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    int r = (wm * TM + i) * 16 + fr;
+    r = r < T ? r : T - 1;
+    int ly, lx;
+    if constexpr (POOL) {
+      const int w = r >> 2, q = r & 3;
+      ly = 2 * (w / (TW / 2)) + (q >> 1);
+      lx = 2 * (w % (TW / 2)) + (q & 1);
+    } else {
+      ly = r / TW;
+      lx = r % TW;
+    }
+    prow2[i / 2] |= (unsigned)(((ly + 1) * PW2 + lx + 1) * PB) << (16 * (i % 2));
+  }
+  auto prow = [&](int i) {
+    unsigned w = prow2[i / 2];
+    asm volatile("" : "+v"(w));
+    return (int)((w >> (16 * (i % 2))) & 0xffffu);
+  };
+  const int fqo = 16 * (fq & 1);
+  auto toff = [&](int s) {  // this lane's tap offset (bytes) in full step s
+    const int ta = 2 * s, tb = 2 * s + 1 < 9 ? 2 * s + 1 : 8;
+    const int oa = ((ta / 3 - 1) * PW2 + (ta % 3 - 1)) * PB, ob = ((tb / 3 - 1) * PW2 + (tb % 3 - 1)) * PB;
+    return th ? ob : oa;
+  };
+  auto frag = [&](int i, int off, bf16x8 (&a)[3]) {
+    const unsigned char* q = patch + prow(i) + fqo + off;
+#pragma unroll
+    for (int p = 0; p < 3; ++p) a[p] = *reinterpret_cast<const bf16x8*>(q + 32 * p);
+  };
+  auto bfrag = [&](int s, bf16x8 (&bb)[3][2]) {
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        bb[p][j] = *reinterpret_cast<const bf16x8*>(smem + (j * NS * 3 + s * 3 + p) * 1024 + lane * 16);
+  };
+  // HALF: the K = 16 step (tap 8, channels 4 fq .. 4 fq + 3): A 8 B at the lane's pixel + tap 8,
+  // B 8 B of the packed step 4 (lane fr + 16 (fq >> 1), element 4 (fq & 1))
+  typedef short s16x4 __attribute__((ext_vector_type(4)));
+  const int hoff = (PW2 + 1) * PB + 8 * fq;  // tap (2, 2) relative to (1, 1), 8 fq in the pixel
+  const int hb = (fr + 16 * (fq >> 1)) * 16 + 8 * (fq & 1);
+
+  const int G = gridDim.x;
+  int t = blockIdx.x;
+  if (t < ntiles) load_tile(t);
+  while (t < ntiles) {
+    int b, y0, x0;
+    tile_xy(t, b, y0, x0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    split_tile();
+    for (int r = threadIdx.x; r < NO; r += NT) {
+      int o;
+      if constexpr (POOL) {
+        const int py = (y0 >> 1) + r / (TW / 2), px = (x0 >> 1) + r % (TW / 2);
+        o = (py >= g.PH || px >= g.PW) ? -1
+            : g.out_mode == 1         ? (b * (g.PH + 2) + py + 1) * (g.PW + 2) + px + 1
+                                      : (b * g.PH + py) * g.PW + px;
+      } else {
+        const int oy = y0 + r / TW, ox = x0 + r % TW;
+        o = (oy >= g.H || ox >= g.W) ? -1 : g.out_mode == 1 ? (b * (g.H + 2) + oy + 1) * Wp + ox + 1 : (b * g.H + oy) * g.W + ox;
+      }
+      orow[r] = o;
+    }
+    const int tn = t + G;
+    if (tn < ntiles) load_tile(tn);  // in flight during this tile's MFMAs
+    __syncthreads();                 // the patch, the row table (and, first time, the weights) written
+
+    f32x4 acc[TM][2], accc[TM][2];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = accc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    constexpr int NSF = HALF ? NS - 1 : NS;  // full 16x16x32 steps
+    // B fragments single-buffered (read at each step's start; the other workgroup's waves cover
+    // the latency): the staging registers of the next tile take the second buffer's room
+    bf16x8 af[2][3], bq[3][2];
+    frag(0, toff(0), af[0]);
+#pragma unroll
+    for (int s = 0; s < NSF; ++s) {
+      const int off = toff(s), off_next = toff(s + 1 < NSF ? s + 1 : s);
+      bfrag(s, bq);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int cur = (s * TM + i) & 1, nxt = cur ^ 1;
+        if (i + 1 < TM)
+          frag(i + 1, off, af[nxt]);
+        else if (s + 1 < NSF)
+          frag(0, off_next, af[nxt]);
+        const bf16x8(&bb)[3][2] = bq;
+#pragma unroll
+        for (int jb = 0; jb < 2; ++jb) x3_step<true>(acc[i][jb], accc[i][jb], af[cur], bb, jb);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    if constexpr (HALF) {
+      s16x4 hbq[3][2];
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          hbq[p][j] = *reinterpret_cast<const s16x4*>(smem + (j * NS * 3 + 4 * 3 + p) * 1024 + hb);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int pr = prow(i);
+        s16x4 a[3];
+#pragma unroll
+        for (int p = 0; p < 3; ++p) a[p] = *reinterpret_cast<const s16x4*>(patch + pr + hoff + 32 * p);
+#pragma unroll
+        for (int jb = 0; jb < 2; ++jb) {
+          f32x4 c = accc[i][jb];
+          c = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a[2], hbq[0][jb], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a[1], hbq[1][jb], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a[0], hbq[2][jb], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a[1], hbq[0][jb], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a[0], hbq[1][jb], c, 0, 0, 0);
+          accc[i][jb] = c;
+          acc[i][jb] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a[0], hbq[0][jb], acc[i][jb], 0, 0, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    x3_fold(acc, accc);
+    __syncthreads();  // every wave is done with the patch: the epilogue stages reuse it
+
+    if constexpr (POOL) {
+      if (g.out_mode == 1) {  // staged 16-B split-plane stores (x3_pool_split_store)
+        float* stgp = reinterpret_cast<float*>(patch) + wm * (TM * 4 * X3_STG_ROW);
+#pragma unroll
+        for (int jb = 0; jb < 2; ++jb) {
+          const int n = 16 * jb + fr;
+          const float pb = (epi.flags & EPI_BIAS) ? epi.bias[n] : 0.f;
+          const float pm = (epi.flags & (EPI_BN | EPI_BN_AB)) ? epi.mean[n] : 0.f;
+          const float ps = (epi.flags & (EPI_BN | EPI_BN_AB)) ? epi.sq[n] : 1.f;
+          const float pg = (epi.flags & EPI_BN) ? epi.gamma[n] : 1.f;
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+            stgp[(4 * i + fq) * X3_STG_ROW + 16 * jb + fr] = pool_then_epilogue(acc[i][jb], pb, pm, ps, pg, epi.flags);
+        }
+        x3_pool_split_store<TM>(stgp, orow, NO, 4 * wm * TM, out_split, 96, 0, lane);
+        __syncthreads();  // stages read before the next tile's split overwrites the patch area
+        t = tn;
+        continue;
+      }
+    }
+#pragma unroll
+    for (int jb = 0; jb < 2; ++jb) {
+      const int n = 16 * jb + fr;
+      const float pb = (epi.flags & EPI_BIAS) ? epi.bias[n] : 0.f;
+      const float pm = (epi.flags & (EPI_BN | EPI_BN_AB)) ? epi.mean[n] : 0.f;
+      const float ps = (epi.flags & (EPI_BN | EPI_BN_AB)) ? epi.sq[n] : 1.f;
+      const float pg = (epi.flags & EPI_BN) ? epi.gamma[n] : 1.f;
+      auto put = [&](int o, float v) {
+        if (g.out_mode == 1) {
+          unsigned short s0, s1, s2;
+          split3(v, s0, s1, s2);
+          bf16_bits* d = out_split + (size_t)o * 96 + n;
+          d[0] = s0;
+          d[32] = s1;
+          d[64] = s2;
+        } else {
+          out[(size_t)o * N + n] = v;
+        }
+      };
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int rb = 16 * (wm * TM + i);
+        if constexpr (POOL) {
+          const int w = rb / 4 + fq;
+          const int o = w < NO ? orow[w] : -1;
+          if (o >= 0) put(o, pool_then_epilogue(acc[i][jb], pb, pm, ps, pg, epi.flags));
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = rb + 4 * fq + r;
+            const int o = row < NO ? orow[row] : -1;
+            if (o >= 0) put(o, apply_epilogue(acc[i][jb][r], pb, pm, ps, pg, epi.flags));
+          }
+        }
+      }
+    }
+    __syncthreads();  // the row table is rewritten by the next tile
+    t = tn;
+  }
+}
+
 }  // namespace dnnhip

@@ -437,13 +437,30 @@ int launch_conv_x3(const bf16_bits* in_split, const bf16_bits* Bt, float* out, b
     const X3Geom xg{H, W, C, out_split ? 1 : 0, 1, PH, PW};
     const float* in32p = reinterpret_cast<const float*>(in_split);
     (void)b16;
-    // (two accumulators per output, gemm_x3_patch.h x3_step)
-    if (pool)
-      hipLaunchKernelGGL((conv3x3_x3_c16_kernel<16, 26, 4, 7, true>), dim3((unsigned)blocks), dim3(256), 0, stream,
-                         in32p, Bt, out, out_split, N, epi, tilesX, tilesY, xg, (unsigned)in32);
-    else
-      hipLaunchKernelGGL((conv3x3_x3_c16_kernel<16, 26, 4, 7, false>), dim3((unsigned)blocks), dim3(256), 0, stream,
-                         in32p, Bt, out, out_split, N, epi, tilesX, tilesY, xg, (unsigned)in32);
+    // (two accumulators per output, gemm_x3_patch.h x3_step).  DNN_HIP_X3_C16P (read per launch,
+    // experiments): 0 = one tile per workgroup (conv3x3_x3_c16_kernel), 1 = persistent
+    // (conv3x3_x3_c16p_kernel: same bits), 2 = persistent with the last K step on 16x16x16
+    const char* pe = getenv("DNN_HIP_X3_C16P");
+    const int pv = pe ? atoi(pe) : 2;  // (measured at batch 64: 0 -> 2 conv1 0.164 -> 0.152 ms, forward -14 us)
+    if (pv == 0 || !pool) {  // (the persistent kernel is instantiated for the pooled form: conv1)
+      if (pool)
+        hipLaunchKernelGGL((conv3x3_x3_c16_kernel<16, 26, 4, 7, true>), dim3((unsigned)blocks), dim3(256), 0, stream,
+                           in32p, Bt, out, out_split, N, epi, tilesX, tilesY, xg, (unsigned)in32);
+      else
+        hipLaunchKernelGGL((conv3x3_x3_c16_kernel<16, 26, 4, 7, false>), dim3((unsigned)blocks), dim3(256), 0, stream,
+                           in32p, Bt, out, out_split, N, epi, tilesX, tilesY, xg, (unsigned)in32);
+    } else {
+      const long long slots = 2LL * device_cu_count();
+      const dim3 pgrid((unsigned)(blocks < slots ? blocks : slots));
+#define C16P(POOL_, HALF_)                                                                                     \
+  hipLaunchKernelGGL((conv3x3_x3_c16p_kernel<POOL_, HALF_>), pgrid, dim3(256), 0, stream, in32p, Bt, out, out_split, \
+                     N, epi, tilesX, tilesY, (int)blocks, xg, (unsigned)in32)
+      if (pv == 2)
+        C16P(true, true);
+      else
+        C16P(true, false);
+#undef C16P
+    }
     return check_x3("conv_x3 (c16)");
   }
   if (kind > 0) {
@@ -499,7 +516,7 @@ int launch_conv_x3(const bf16_bits* in_split, const bf16_bits* Bt, float* out, b
   // launch, so one process can interleave placements -- placement never changes a bit)
   const char* mge = getenv("DNN_HIP_X3_MG");
   const int mg_env = mge ? atoi(mge) : 0;
-  const int mg = mg_env > 0 ? mg_env : (tilesN >= 4 ? 4 : tilesN >= 2 ? 2 : 1);
+  const int mg = mg_env > 0 ? mg_env : 1;  // (measured: 1, 2 and 4 equal within 0.5 %, round 4)
   const X3Geom xg{H, W, C, splits > 1 ? 2 : out_split ? 1 : 0, splits, PH, PW, mg < tilesM ? mg : 1};
   const dim3 grid(tilesM * tilesN * (pool ? 1 : splits));
 #define X3AF(NPR_, POOL_, FL_)                                                                                    \

@@ -36,17 +36,35 @@ def clock_stamps(lib, nwg):
     buf = (ctypes.c_ulonglong * (4 * nwg))()
     if fn(buf, nwg) != 0:
         return None
-    ghz, loop_us = [], []
+    ghz, loop_us, cyc, rows = [], [], [], []
     for w in range(nwg):
         t0, r0, t1, r1 = buf[4 * w:4 * w + 4]
         if r1 > r0 and t1 > t0:
             ghz.append((t1 - t0) / (r1 - r0) * 0.1)  # s_memrealtime ticks at 100 MHz
             loop_us.append((r1 - r0) / 100.0)
+            cyc.append(t1 - t0)
+            rows.append((w, r0, r1, t1 - t0))
     if not ghz:
         return None
+    r0min = min(r[1] for r in rows)
+    # per XCD (blocks b and b + 8 share one: b % 8): clock, loop time, loop start and end
+    # relative to the earliest loop start (us)
+    xcd = {}
+    for x in range(8):
+        sel = [r for r in rows if r[0] % 8 == x]
+        if not sel:
+            continue
+        xcd[x] = {"ghz": round(statistics.median(r[3] / (r[2] - r[1]) * 0.1 for r in sel), 4),
+                  "loop_us": round(statistics.median((r[2] - r[1]) / 100 for r in sel), 2),
+                  "start_us_max": round(max((r[1] - r0min) / 100 for r in sel), 2),
+                  "end_us_max": round(max((r[2] - r0min) / 100 for r in sel), 2),
+                  "mcycles": round(statistics.median(r[3] for r in sel) / 1e6, 4)}
     return {"median_ghz": round(statistics.median(ghz), 4), "min_ghz": round(min(ghz), 4),
             "max_ghz": round(max(ghz), 4), "median_loop_us": round(statistics.median(loop_us), 2),
-            "max_loop_us": round(max(loop_us), 2), "workgroups": len(ghz)}
+            "max_loop_us": round(max(loop_us), 2), "workgroups": len(ghz),
+            "mcycles_median": round(statistics.median(cyc) / 1e6, 4), "mcycles_min": round(min(cyc) / 1e6, 4),
+            "mcycles_max": round(max(cyc) / 1e6, 4),
+            "span_us": round((max(r[2] for r in rows) - r0min) / 100, 2), "per_xcd": xcd}
 
 
 def main():
@@ -56,7 +74,7 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--preheat", type=float, default=3.0)
     ap.add_argument("--batch", type=int, default=64)
-    ap.add_argument("--kernels", default="conv4,conv5,conv6,conv7")
+    ap.add_argument("--kernels", default="conv0,conv1,conv2,conv3,conv4,conv5,conv6,conv7,conv8")
     a = ap.parse_args()
     arms = [{}]
     for spec in a.env:
@@ -96,7 +114,12 @@ def main():
         stream.synchronize()
     res = {json.dumps(x): {"fwd_ms": [], "k": {n: [] for n in names}, "clock": []} for x in arms}
     for r in range(a.rounds):
-        for arm in arms:
+        # arm order rotated and reversed round by round (no arm always follows the same one:
+        # the clock a kernel runs at depends on the power drawn just before it)
+        order = arms[r % len(arms):] + arms[:r % len(arms)]
+        if r % 2:
+            order = order[::-1]
+        for arm in order:
             set_arm(arm)
             fwd(2)
             plan.timing_begin(a.iters)
