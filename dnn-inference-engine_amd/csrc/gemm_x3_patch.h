@@ -125,249 +125,6 @@ __device__ __forceinline__ void x3_pool_split_store(const float* stg, const int*
 // lane's 4 accumulator registers (rows 4 q .. 4 q + 3 of its 16 x 16 block) are one window:
 // pooled before the epilogue (pool_then_epilogue, as the fp32 GEMMs' fused pools).
 
-// Narrow layers (N = 64 / 128: YOLOv2-tiny conv2 / conv3, 104x104 and 52x52 frames).  A run of
-// consecutive rows spans whole image rows plus a two-row halo, so on wide frames the wide
-// kernel (gemm_x3_acc2.h) would stage 2.2-5x its tile's pixels (x3_span); here a workgroup owns a 2-D
-// tile of TH x TW output pixels and 32 WN columns, and stages its (TH + 2) x (TW + 2) patch
-// (1.56x for 4 x 52).  WM x WN waves of TM 16-row blocks x 32 columns; tile rows raster, or
-// pool-window-major (POOL: TH, TW even, so a 2x2 window never leaves its tile).  Same
-// fragments, weight stream, per-step MFMA sequence and accumulation order as the kernel above
-// (the order depends on (N, K) only).  NBUF = 1: one 32-channel chunk (K = 288), the patch is
-// staged once; NBUF = 2: chunk j + 1 staged during chunk j's taps.  Rows past the tile
-// (WM TM 16 > TH TW) and pixels past the frame compute on clamped rows and are not stored.
-// A2: two accumulators per output over all of K and no per-step adds (gemm_x3_acc2.h's
-// arithmetic and product order); false: the correction chain from zero + one add per step.
-template <int TH, int TW, int WM, int WN, int TM, int NBUF, bool POOL, bool A2 = true>
-__global__ void __launch_bounds__(64 * WM * WN, 512 / (64 * WM * WN))
-conv3x3_x3_tile_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __restrict__ Bt, float* __restrict__ out,
-                       bf16_bits* __restrict__ out_split, int N, int K, EpiParams epi, int tilesX, int tilesY,
-                       int tilesN, X3Geom g, unsigned in_bytes, unsigned b_bytes) {
-  constexpr int NT = 64 * WM * WN, RB = 192, PW2 = TW + 2, PR = (TH + 2) * PW2, T = TH * TW;
-  constexpr int ITEMS = PR * 12, PPT = (ITEMS + NT - 1) / NT;  // 16-B patch pieces per thread
-  static_assert(TH % 2 == 0 && TW % 2 == 0 && WM * TM * 16 >= T && (WM * TM - 2) * 16 < T && PPT <= 16 &&
-                    (NBUF == 1 || NBUF == 2),
-                "shape");
-  __shared__ __attribute__((aligned(1024))) unsigned char smem[NBUF * PR * RB];
-
-  const int lane = threadIdx.x & 63;
-  const int wid = wave_uniform(threadIdx.x >> 6);
-  const int wn = wid % WN, wm = wid / WN;
-  // tiles: N panel fastest, then x, y, image (neighbouring tiles share halo rows in their L2)
-  int t = xcd_tile(blockIdx.x, gridDim.x);
-  const int tn = t % tilesN;
-  t /= tilesN;
-  const int tx = t % tilesX;
-  t /= tilesX;
-  const int ty = t % tilesY;
-  const int b = t / tilesY;
-  const int y0 = ty * TH, x0 = tx * TW;  // tile's first output pixel; patch row py = padded row y0 + py
-  const int n0 = tn * (32 * WN) + wn * 32;
-  const int Wp = g.W + 2;
-
-  const int fr = lane & 15, fq = lane >> 4;
-  int prow[TM];  // patch row of the lane's output pixel in row-block i (tap (1, 1))
-#pragma unroll
-  for (int i = 0; i < TM; ++i) {
-    int r = (wm * TM + i) * 16 + fr;
-    r = r < T ? r : T - 1;
-    int ly, lx;
-    if constexpr (POOL) {
-      const int w = r >> 2, q = r & 3;
-      ly = 2 * (w / (TW / 2)) + (q >> 1);
-      lx = 2 * (w % (TW / 2)) + (q & 1);
-    } else {
-      ly = r / TW;
-      lx = r % TW;
-    }
-    prow[i] = (ly + 1) * PW2 + lx + 1;
-  }
-
-  // patch staging: item e = (patch row e / 12, 16-B slot e % 12); the last thread's surplus
-  // items repeat item ITEMS - 1 (same bytes to the same address).  Patch pixels past the frame
-  // read the next padded row / image or the descriptor's zeros: only dropped outputs use them
-  const int nk = K / 32, nch = nk / 9;
-  const int rowB = 6 * g.C;
-  const auto rsA = __builtin_amdgcn_make_buffer_rsrc((void*)in, 0, (int)in_bytes, 0x00020000);
-  unsigned pvo[PPT];
-  int pdst[PPT];
-#pragma unroll
-  for (int u = 0; u < PPT; ++u) {
-    int e = threadIdx.x + u * NT;
-    e = e < ITEMS ? e : ITEMS - 1;
-    const int pr = e / 12, ss = e - pr * 12, py = pr / PW2, px = pr - py * PW2;
-    pvo[u] = (unsigned)(((b * (g.H + 2) + y0 + py) * Wp + x0 + px) * rowB + ss * 16);
-    pdst[u] = pr * RB + (ss >> 2) * 64 + 16 * ((ss & 3) ^ ((pr >> 1) & 2));
-  }
-  u32x4 pst[PPT];
-  auto load_piece = [&](int chunk, int u) { pst[u] = __builtin_amdgcn_raw_buffer_load_b128(rsA, pvo[u], chunk * RB, 0); };
-  auto store_piece = [&](int buf, int u) {
-    *reinterpret_cast<u32x4*>(smem + buf * PR * RB + pdst[u]) = pst[u];
-  };
-
-  const unsigned bvo = (unsigned)((n0 / 16) * nk * 3072 + lane * 16);
-  const int bjs = nk * 3072;
-  const auto rsB = __builtin_amdgcn_make_buffer_rsrc((void*)Bt, 0, (int)b_bytes, 0x00020000);
-  bf16x8 bq[3][3][2];
-#pragma unroll
-  for (int a = 0; a < 3; ++a)
-#pragma unroll
-    for (int p = 0; p < 3; ++p)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) bq[a][p][j] = bf16x8{};
-  auto load_b = [&](int s, bf16x8 (&dst)[3][2]) {
-#pragma unroll
-    for (int p = 0; p < 3; ++p)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-        dst[p][j] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rsB, bvo, s * 3072 + p * 1024 + j * bjs, 0));
-  };
-
-  f32x4 acc[TM][2], accc[TM][2];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = accc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-#pragma unroll
-  for (int u = 0; u < PPT; ++u) load_piece(0, u);
-  load_b(0, bq[0]);
-  load_b(1, bq[1]);
-#pragma unroll
-  for (int u = 0; u < PPT; ++u) store_piece(0, u);
-  wait_lgkm0();
-  __syncthreads();
-
-  auto frag = [&](const unsigned char* P, int i, int toff, bf16x8 (&a)[3]) {
-    int pr = prow[i];
-    asm volatile("" : "+v"(pr));
-    const int row = pr + toff;
-    const unsigned char* q = P + row * RB + 16 * (fq ^ ((row >> 1) & 2));
-#pragma unroll
-    for (int p = 0; p < 3; ++p) a[p] = *reinterpret_cast<const bf16x8*>(q + 64 * p);
-  };
-  for (int j = 0; j < nch; ++j) {
-    const unsigned char* P = smem + (NBUF == 2 ? (j & 1) : 0) * PR * RB;
-    bf16x8 af[2][3];
-    frag(P, 0, -(PW2 + 1), af[0]);
-#pragma unroll
-    for (int tp = 0; tp < 9; ++tp) {
-      const int s = 9 * j + tp;
-      const int toff = (tp / 3 - 1) * PW2 + (tp % 3 - 1);
-      const int toff_next = ((tp + 1) / 3 - 1) * PW2 + ((tp + 1) % 3 - 1);
-      __builtin_amdgcn_sched_barrier(0);
-      if constexpr (NBUF == 2) {
-#pragma unroll
-        for (int u = 0; u < PPT; ++u)
-          if ((8 * u) / PPT == tp) load_piece(j + 1, u);
-      }
-      load_b(s + 2, bq[(tp + 2) % 3]);
-      if constexpr (NBUF == 2) {
-#pragma unroll
-        for (int u = 0; u < PPT; ++u)
-          if ((8 * u) / PPT + 1 == tp) store_piece((j + 1) & 1, u);
-      }
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const int cur = i & 1, nxt = cur ^ 1;
-        if (i + 1 < TM)
-          frag(P, i + 1, toff, af[nxt]);
-        else if (tp < 8)
-          frag(P, 0, toff_next, af[nxt]);
-        const bf16x8(&bb)[3][2] = bq[tp % 3];
-#pragma unroll
-        for (int jb = 0; jb < 2; ++jb) x3_step<A2>(acc[i][jb], accc[i][jb], af[cur], bb, jb);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      if constexpr (TM & 1) {
-        if (tp < 8) {
-#pragma unroll
-          for (int p = 0; p < 3; ++p) af[0][p] = af[1][p];
-        }
-      }
-    }
-    if (NBUF == 2 && j + 1 < nch) {
-      wait_lgkm0();
-      raw_barrier();
-    }
-  }
-
-  if constexpr (A2) x3_fold(acc, accc);
-  // epilogue: output rows (or pooled pixels) of the tile tabulated in LDS, -1 past the frame
-  int* orow = reinterpret_cast<int*>(smem);
-  __syncthreads();
-  constexpr int NO = POOL ? T / 4 : T;
-  for (int r = threadIdx.x; r < NO; r += NT) {
-    int o;
-    if constexpr (POOL) {
-      const int py = (y0 >> 1) + r / (TW / 2), px = (x0 >> 1) + r % (TW / 2);
-      o = (py >= g.PH || px >= g.PW) ? -1
-          : g.out_mode == 1         ? (b * (g.PH + 2) + py + 1) * (g.PW + 2) + px + 1
-                                    : (b * g.PH + py) * g.PW + px;
-    } else {
-      const int oy = y0 + r / TW, ox = x0 + r % TW;
-      o = (oy >= g.H || ox >= g.W) ? -1 : g.out_mode == 1 ? (b * (g.H + 2) + oy + 1) * Wp + ox + 1 : (b * g.H + oy) * g.W + ox;
-    }
-    orow[r] = o;
-  }
-  __syncthreads();
-  if constexpr (POOL) {
-    if (g.out_mode == 1) {  // staged 16-B split-plane stores (x3_pool_split_store)
-      static_assert(1024 + NT / 64 * TM * 4 * X3_STG_ROW * 4 <= NBUF * PR * RB && NO * 4 <= 1024, "stage");
-      float* stg = reinterpret_cast<float*>(smem + 1024) + wid * (TM * 4 * X3_STG_ROW);
-#pragma unroll
-      for (int jb = 0; jb < 2; ++jb) {
-        const int n = n0 + 16 * jb + fr;
-        const float pb = (epi.flags & EPI_BIAS) ? epi.bias[n] : 0.f;
-        const float pm = (epi.flags & (EPI_BN | EPI_BN_AB)) ? epi.mean[n] : 0.f;
-        const float ps = (epi.flags & (EPI_BN | EPI_BN_AB)) ? epi.sq[n] : 1.f;
-        const float pg = (epi.flags & EPI_BN) ? epi.gamma[n] : 1.f;
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-          stg[(4 * i + fq) * X3_STG_ROW + 16 * jb + fr] = pool_then_epilogue(acc[i][jb], pb, pm, ps, pg, epi.flags);
-      }
-      x3_pool_split_store<TM>(stg, orow, NO, 4 * wm * TM, out_split, 3 * (size_t)N, (n0 >> 5) * 96, lane);
-      return;
-    }
-  }
-#pragma unroll
-  for (int jb = 0; jb < 2; ++jb) {
-    const int n = n0 + 16 * jb + fr;  // < N: N % (32 WN) == 0 (launcher)
-    const float pb = (epi.flags & EPI_BIAS) ? epi.bias[n] : 0.f;
-    const float pm = (epi.flags & (EPI_BN | EPI_BN_AB)) ? epi.mean[n] : 0.f;
-    const float ps = (epi.flags & (EPI_BN | EPI_BN_AB)) ? epi.sq[n] : 1.f;
-    const float pg = (epi.flags & EPI_BN) ? epi.gamma[n] : 1.f;
-    const int cofs = (n >> 5) * 96 + (n & 31);
-    auto put = [&](int o, float v) {
-      if (g.out_mode == 1) {
-        unsigned short s0, s1, s2;
-        split3(v, s0, s1, s2);
-        bf16_bits* d = out_split + (size_t)o * (3 * N) + cofs;
-        d[0] = s0;
-        d[32] = s1;
-        d[64] = s2;
-      } else {
-        out[(size_t)o * N + n] = v;
-      }
-    };
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const int rb = 16 * (wm * TM + i);
-      if constexpr (POOL) {  // lane's 4 registers = window rb / 4 + fq
-        const int w = rb / 4 + fq;
-        const int o = w < NO ? orow[w] : -1;
-        if (o >= 0) put(o, pool_then_epilogue(acc[i][jb], pb, pm, ps, pg, epi.flags));
-      } else {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = rb + 4 * fq + r;
-          const int o = row < NO ? orow[row] : -1;
-          if (o >= 0) put(o, apply_epilogue(acc[i][jb][r], pb, pm, ps, pg, epi.flags));
-        }
-      }
-    }
-  }
-}
-
 // 16-channel layers (YOLOv2-tiny conv1, 208x208x16 -> 32): the input is the producer's plain
 // fp32 NHWC (no split planes), split into the three bf16 pieces while the patch is staged
 // (frame padding = the descriptor's zeros).  K = 144 runs as 5 steps of 32: step s feeds k
@@ -879,6 +636,240 @@ conv3x3_x3_c16p_kernel(const float* __restrict__ in, const bf16_bits* __restrict
     }
     __syncthreads();  // the row table is rewritten by the next tile
     t = tn;
+  }
+}
+
+
+// Narrow layers (N = 64 / 128: YOLOv2-tiny conv2 / conv3, 104x104 and 52x52 frames).  A run of
+// consecutive rows spans whole image rows plus a two-row halo, so on wide frames the wide kernel
+// (gemm_x3_acc2.h) would stage 2.2-5x its tile's pixels (x3_span); here a workgroup owns a 2-D
+// tile of TH x TW output pixels and 32 WN columns, and stages its (TH + 2) x (TW + 2) patch.  WM x
+// WN waves of TM 16-row blocks x 32 columns; tile rows raster, or pool-window-major (POOL: TH, TW
+// even, so a 2x2 window never leaves its tile).  Rows past the tile (WM TM 16 > TH TW) and pixels
+// past the frame compute on clamped rows and are not stored.  Weights straight from L2 to
+// registers two steps ahead (a 3-step ring).  Round 4 layout, the wide kernel's: 224-B LDS pixel rows (the 192 data
+// bytes of a 32-channel chunk + 32 never-read bytes; tools: 2.86 extra conflict cycles per
+// fragment read at these tiles, the same as the 192-B rows' XOR swizzle, with plain offsets)
+// filled by LDS-DMA (1 KiB pieces, per-lane source = its pixel row's chunk + 16 u, no staging
+// registers), so a fragment address is a per-block register + a tap offset that is an
+// instruction immediate (no per-fragment multiply, XOR or shift: the old loop spent ~6 VALU per
+// fragment, one a quarter-rate v_mul_lo).  Chunk j + 1 is DMA'd into the other buffer when chunk
+// j starts (NBUF = 2) or after it (NBUF = 1, one buffer).  Two accumulators per output (A2) for
+// every configuration.  (Rounds 2-3: register-staged 192-B rows with an XOR swizzle, per-step adds
+// for N = 128: conv3 0.127 -> 0.114 ms, conv2 0.129 -> 0.126 ms with this form; git history.)
+template <int TH, int TW, int WM, int WN, int TM, int NBUF, bool POOL>
+__global__ void __launch_bounds__(64 * WM * WN, 512 / (64 * WM * WN))
+conv3x3_x3_tile2_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __restrict__ Bt, float* __restrict__ out,
+                        bf16_bits* __restrict__ out_split, int N, int K, EpiParams epi, int tilesX, int tilesY,
+                        int tilesN, X3Geom g, unsigned in_bytes, unsigned b_bytes) {
+  constexpr int NW = WM * WN, NT = 64 * NW, LP = 224, PU = LP / 16, PW2 = TW + 2, PR = (TH + 2) * PW2, T = TH * TW;
+  constexpr int NPC = (PR * PU + 63) / 64, NPW = (NPC + NW - 1) / NW;  // 1-KiB DMA pieces per chunk / per wave
+  constexpr int BUFB = NPW * NW * 1024;
+  static_assert(TH % 2 == 0 && TW % 2 == 0 && WM * TM * 16 >= T && (WM * TM - 2) * 16 < T && (NBUF == 1 || NBUF == 2) &&
+                    NPW <= 24,
+                "shape");
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[NBUF * BUFB];
+
+  const int lane = threadIdx.x & 63;
+  const int wid = wave_uniform(threadIdx.x >> 6);
+  const int wn = wid % WN, wm = wid / WN;
+  int t = xcd_tile(blockIdx.x, gridDim.x);
+  const int tn = t % tilesN;
+  t /= tilesN;
+  const int tx = t % tilesX;
+  t /= tilesX;
+  const int ty = t % tilesY;
+  const int b = t / tilesY;
+  const int y0 = ty * TH, x0 = tx * TW;
+  const int n0 = tn * (32 * WN) + wn * 32;
+  const int Wp = g.W + 2;
+  const int fr = lane & 15, fq = lane >> 4;
+
+  // fragment rows: byte offset of the lane's tap-(0, 0) pixel row of block i (+ 16 fq)
+  int rowoff[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    int r = (wm * TM + i) * 16 + fr;
+    r = r < T ? r : T - 1;
+    int ly, lx;
+    if constexpr (POOL) {
+      const int w = r >> 2, q = r & 3;
+      ly = 2 * (w / (TW / 2)) + (q >> 1);
+      lx = 2 * (w % (TW / 2)) + (q & 1);
+    } else {
+      ly = r / TW;
+      lx = r % TW;
+    }
+    rowoff[i] = (ly * PW2 + lx) * LP + 16 * fq;
+  }
+
+  // patch DMA: piece k of this wave covers LDS units U = 64 (wid + NW k) + lane = pixel row r =
+  // U / PU (rows past the patch repeat the last), unit u = U % PU; source = the padded pixel
+  // (y0 + r / PW2, x0 + r % PW2) of image b, chunk c, + 16 u (units 12, 13: the next 32 bytes)
+  const int nk = K / 32, nch = nk / 9;
+  const unsigned rowB = 6u * (unsigned)g.C;
+  const auto rsA = __builtin_amdgcn_make_buffer_rsrc((void*)in, 0, (int)in_bytes, 0x00020000);
+  const unsigned pbase = (unsigned)((b * (g.H + 2) + y0) * Wp + x0);  // padded pixel of patch (0, 0)
+  auto issue_chunk = [&](int c, int buf) {
+#pragma unroll
+    for (int k = 0; k < NPW; ++k) {
+      const unsigned U = 64u * (unsigned)(wid + NW * k) + (unsigned)lane;
+      unsigned r = U / PU;
+      const unsigned u = U - r * PU;
+      r = r < (unsigned)PR ? r : (unsigned)PR - 1;
+      const unsigned py = r / PW2, px = r - py * PW2;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rsA, (__attribute__((address_space(3))) void*)(smem + buf * BUFB + 1024 * (wid + NW * k)), 16,
+          (int)((pbase + py * (unsigned)Wp + px) * rowB + 16u * u), (int)(c * 192), 0, 0);
+    }
+  };
+
+  const unsigned bvo = (unsigned)((n0 / 16) * nk * 3072 + lane * 16);
+  const int bjs = nk * 3072;
+  const auto rsB = __builtin_amdgcn_make_buffer_rsrc((void*)Bt, 0, (int)b_bytes, 0x00020000);
+  bf16x8 bq[3][3][2];
+  auto load_b = [&](int s, bf16x8 (&dst)[3][2]) {
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        dst[p][j] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rsB, bvo, s * 3072 + p * 1024 + j * bjs, 0));
+  };
+
+  f32x4 acc[TM][2], accc[TM][2];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = accc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  issue_chunk(0, 0);
+  load_b(0, bq[0]);
+  load_b(1, bq[1]);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  auto frag = [&](const unsigned char* P, int i, int tap, bf16x8 (&a)[3]) {
+    const int toff = ((tap / 3) * PW2 + (tap % 3)) * LP;
+    const unsigned char* q = P + rowoff[i] + toff;
+#pragma unroll
+    for (int p = 0; p < 3; ++p) a[p] = *reinterpret_cast<const bf16x8*>(q + 64 * p);
+  };
+  for (int j = 0; j < nch; ++j) {
+    const unsigned char* P = smem + (NBUF == 2 ? (j & 1) : 0) * BUFB;
+    if (NBUF == 2 && j + 1 < nch) issue_chunk(j + 1, (j + 1) & 1);  // the other buffer: read in chunk j - 1
+    bf16x8 af[2][3];
+    frag(P, 0, 0, af[0]);
+#pragma unroll
+    for (int tp = 0; tp < 9; ++tp) {
+      const int s = 9 * j + tp;
+      __builtin_amdgcn_sched_barrier(0);
+      load_b(s + 2, bq[(tp + 2) % 3]);  // (past the last step: unused, in-range or zero-filled)
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int cur = i & 1, nxt = cur ^ 1;
+        if (i + 1 < TM)
+          frag(P, i + 1, tp, af[nxt]);
+        else if (tp < 8)
+          frag(P, 0, tp + 1, af[nxt]);
+        const bf16x8(&bb)[3][2] = bq[tp % 3];
+#pragma unroll
+        for (int jb = 0; jb < 2; ++jb) x3_step<true>(acc[i][jb], accc[i][jb], af[cur], bb, jb);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if constexpr (TM & 1) {
+        if (tp < 8) {
+#pragma unroll
+          for (int p = 0; p < 3; ++p) af[0][p] = af[1][p];
+        }
+      }
+    }
+    // the ring holds steps s + 1, s + 2 in slots (tp + 1) % 3 = 0 and 1 for the next chunk (9 % 3 == 0)
+    if (j + 1 < nch) {
+      if constexpr (NBUF == 1) {
+        wait_lgkm0();
+        __syncthreads();  // every wave done with the patch
+        issue_chunk(j + 1, 0);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      wait_lgkm0();
+      __syncthreads();  // chunk j + 1 landed (every wave's pieces); chunk j read by every wave
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  x3_fold(acc, accc);
+  int* orow = reinterpret_cast<int*>(smem);
+  __syncthreads();
+  constexpr int NO = POOL ? T / 4 : T;
+  for (int r = threadIdx.x; r < NO; r += NT) {
+    int o;
+    if constexpr (POOL) {
+      const int py = (y0 >> 1) + r / (TW / 2), px = (x0 >> 1) + r % (TW / 2);
+      o = (py >= g.PH || px >= g.PW) ? -1
+          : g.out_mode == 1         ? (b * (g.PH + 2) + py + 1) * (g.PW + 2) + px + 1
+                                    : (b * g.PH + py) * g.PW + px;
+    } else {
+      const int oy = y0 + r / TW, ox = x0 + r % TW;
+      o = (oy >= g.H || ox >= g.W) ? -1 : g.out_mode == 1 ? (b * (g.H + 2) + oy + 1) * Wp + ox + 1 : (b * g.H + oy) * g.W + ox;
+    }
+    orow[r] = o;
+  }
+  __syncthreads();
+  if constexpr (POOL) {
+    if (g.out_mode == 1) {  // staged 16-B split-plane stores (x3_pool_split_store)
+      static_assert(1024 + NW * TM * 4 * X3_STG_ROW * 4 <= NBUF * BUFB && NO * 4 <= 1024, "stage");
+      float* stg = reinterpret_cast<float*>(smem + 1024) + wid * (TM * 4 * X3_STG_ROW);
+#pragma unroll
+      for (int jb = 0; jb < 2; ++jb) {
+        const int n = n0 + 16 * jb + fr;
+        const float pb = (epi.flags & EPI_BIAS) ? epi.bias[n] : 0.f;
+        const float pm = (epi.flags & (EPI_BN | EPI_BN_AB)) ? epi.mean[n] : 0.f;
+        const float ps = (epi.flags & (EPI_BN | EPI_BN_AB)) ? epi.sq[n] : 1.f;
+        const float pg = (epi.flags & EPI_BN) ? epi.gamma[n] : 1.f;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+          stg[(4 * i + fq) * X3_STG_ROW + 16 * jb + fr] = pool_then_epilogue(acc[i][jb], pb, pm, ps, pg, epi.flags);
+      }
+      x3_pool_split_store<TM>(stg, orow, NO, 4 * wm * TM, out_split, 3 * (size_t)N, (n0 >> 5) * 96, lane);
+      return;
+    }
+  }
+#pragma unroll
+  for (int jb = 0; jb < 2; ++jb) {
+    const int n = n0 + 16 * jb + fr;  // < N: N % (32 WN) == 0 (launcher)
+    const float pb = (epi.flags & EPI_BIAS) ? epi.bias[n] : 0.f;
+    const float pm = (epi.flags & (EPI_BN | EPI_BN_AB)) ? epi.mean[n] : 0.f;
+    const float ps = (epi.flags & (EPI_BN | EPI_BN_AB)) ? epi.sq[n] : 1.f;
+    const float pg = (epi.flags & EPI_BN) ? epi.gamma[n] : 1.f;
+    const int cofs = (n >> 5) * 96 + (n & 31);
+    auto put = [&](int o, float v) {
+      if (g.out_mode == 1) {
+        unsigned short s0, s1, s2;
+        split3(v, s0, s1, s2);
+        bf16_bits* d = out_split + (size_t)o * (3 * N) + cofs;
+        d[0] = s0;
+        d[32] = s1;
+        d[64] = s2;
+      } else {
+        out[(size_t)o * N + n] = v;
+      }
+    };
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int rb = 16 * (wm * TM + i);
+      if constexpr (POOL) {
+        const int w = rb / 4 + fq;
+        const int o = w < NO ? orow[w] : -1;
+        if (o >= 0) put(o, pool_then_epilogue(acc[i][jb], pb, pm, ps, pg, epi.flags));
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = rb + 4 * fq + r;
+          const int o = row < NO ? orow[row] : -1;
+          if (o >= 0) put(o, apply_epilogue(acc[i][jb][r], pb, pm, ps, pg, epi.flags));
+        }
+      }
+    }
   }
 }
 

@@ -360,7 +360,7 @@ static long long x3_span(long long M, int H, int W, bool pool = false) {
   return mx;
 }
 
-// narrow layers: the 2-D tile kernel (conv3x3_x3_tile_kernel), 8 x 26 (N = 64) or 4 x 26
+// narrow layers: the 2-D tile kernel (conv3x3_x3_tile2_kernel), 8 x 26 (N = 64) or 4 x 26
 // (N % 128 == 0) output pixels per tile: YOLOv2-tiny's 104- and 52-wide frames in whole tiles
 constexpr int X3T_TM = 7;  // row blocks of 16 per wave
 
@@ -470,7 +470,7 @@ int launch_conv_x3(const bf16_bits* in_split, const bf16_bits* Bt, float* out, b
       set_error("conv_x3 (tile): unsupported shape M=%lld N=%d K=%d %dx%dx%d", M, N, K, H, W, C);
       return -2;
     }
-    // kind 2: 4 x 26 tiles, 4 waves (1 x 4), 2 workgroups per CU (64.5 KB LDS each): at batch 64
+    // kind 2: 4 x 26 tiles, 4 waves (1 x 4), 2 workgroups per CU (80 KB LDS each): at batch 64
     // conv3 is 1,664 tiles, 6.5 per CU, where 4 x 52 tiles of 8 waves were 3.25 rounds of one per
     // CU (measured 0.157 -> 0.131 ms).  kind 1: 8 x 26 tiles (1.35x patch rows per output row;
     // 4 x 52: 1.56x, conv2 0.142 -> 0.140 ms)
@@ -482,23 +482,21 @@ int launch_conv_x3(const bf16_bits* in_split, const bf16_bits* Bt, float* out, b
       return -2;
     }
     const X3Geom xg{H, W, C, out_split ? 1 : 0, 1, PH, PW};
-#define X3T_(TH_, TW_, WM, WN, NBUF, POOL, A2_)                                                                  \
-  hipLaunchKernelGGL((conv3x3_x3_tile_kernel<TH_, TW_, WM, WN, X3T_TM, NBUF, POOL, A2_>), dim3((unsigned)blocks),   \
+    // conv3x3_x3_tile2_kernel: 224-B LDS rows by LDS-DMA, immediate tap offsets, two accumulators
+#define X3T2(TH_, TW_, WM, WN, NBUF, POOL)                                                                      \
+  hipLaunchKernelGGL((conv3x3_x3_tile2_kernel<TH_, TW_, WM, WN, X3T_TM, NBUF, POOL>), dim3((unsigned)blocks),     \
                      dim3(64 * WM * WN), 0, stream, in_split, Bt, out, out_split, N, K, epi, tilesX, tilesY, tilesN, \
                      xg, (unsigned)in_bytes, (unsigned)b_bytes)
-#define X3T(TH_, TW_, WM, WN, NBUF, POOL) X3T_(TH_, TW_, WM, WN, NBUF, POOL, true)
-    // (kind 2 keeps the round-2 form: its 3-step weight ring and staging registers leave no
-    // room for the second accumulator set)
-    if (kind == 2 && pool)
-      X3T_(4, 26, 1, 4, 2, true, false);
-    else if (kind == 2)
-      X3T_(4, 26, 1, 4, 2, false, false);
-    else if (pool)
-      X3T(8, 26, 2, 2, 1, true);
-    else
-      X3T(8, 26, 2, 2, 1, false);
-#undef X3T
-#undef X3T_
+    if (kind == 2 && pool) {
+      X3T2(4, 26, 1, 4, 2, true);
+    } else if (kind == 2) {
+      X3T2(4, 26, 1, 4, 2, false);
+    } else if (pool) {
+      X3T2(8, 26, 2, 2, 1, true);
+    } else {
+      X3T2(8, 26, 2, 2, 1, false);
+    }
+#undef X3T2
     return check_x3("conv_x3 (tile)");
   }
   if (M % per_img != 0 || K != 9 * C || C % 32 != 0 || N % 256 != 0 || Npad != N || (pool && splits != 1) ||

@@ -1420,7 +1420,7 @@ X3_TILE_CASES = [
 
 @pytest.mark.parametrize("case", X3_TILE_CASES)
 def test_x3_tile_kernel_vs_oracle(monkeypatch, case):
-    """conv3x3_x3_tile_kernel (N = 64 / 128 on 2-D 8 x 26 / 4 x 26 output tiles),
+    """conv3x3_x3_tile2_kernel (N = 64 / 128 on 2-D 8 x 26 / 4 x 26 output tiles),
     conv3x3_x3_c16_kernel (16 input channels, two taps per 32-wide K step) and the patch conv's
     split-plane epilogue: modes as planned, the chain within the fp32 tolerance of the float64
     oracle and within 1.25x of the fp32-MFMA plan's error (DNN_HIP_X3=0), negative-gamma
