@@ -6,6 +6,7 @@
 #include "dnn_common.h"
 #include "gemm_f16.h"
 #include "gemm_f16_patch.h"
+#include "gemm_f16_acc.h"
 
 namespace dnnhip {
 
@@ -249,7 +250,7 @@ __global__ void maxpool16_kernel(const half_t* __restrict__ in, half_t* __restri
 #pragma unroll
     for (int e = 0; e < 8; ++e) o[e] = (half_t)m[e];
     // opad: write into the interior of a zero-bordered [B][OH+2][OW+2][C] buffer (the input of a
-    // conv3x3_f16_patch_kernel layer)
+    // conv3x3_f16_acc_kernel layer)
     *reinterpret_cast<h8*>(out + (((size_t)b * (g.OH + 2 * opad) + oy + opad) * (g.OW + 2 * opad) + ox + opad) * g.C +
                            c) = o;
   }
@@ -265,17 +266,10 @@ int launch_maxpool16(const half_t* in, half_t* out, const PoolGeom& g, hipStream
   return check16("maxpool16");
 }
 
-// ---- conv3x3_f16_patch_kernel (gemm_f16_patch.h): conv6/conv7 of the fp16 path
-// MFMA shape of the patch kernel: 16 (v_mfma_f32_16x16x32_f16, 176-row tiles) or 32
-// (32x32x16, 192-row tiles); DNN_HIP_P16MF overrides (experiments).  The weight packing order
-// follows it (patch16_pack_order).
-constexpr int P16_NPR = 320;
-static int p16_mf() {
-  const char* e = getenv("DNN_HIP_P16MF");
-  return e && atoi(e) == 32 ? 32 : 16;
-}
-static int p16_bm() { return p16_mf() == 32 ? 192 : 176; }
-int patch16_pack_order() { return p16_mf() == 32 ? 3 : 4; }
+// ---- conv3x3_f16_acc_kernel (gemm_f16_acc.h): conv6/conv7 of the fp16 path, 176-row tiles,
+// v_mfma_f32_16x16x32_f16; weights packed in order 4 ([n/16][k/32][lane][8])
+constexpr int P16_NPR = 320, P16_BM = 176;
+int patch16_pack_order() { return 4; }
 constexpr bool P16_DEFAULT = true;  // measured: conv6 0.1415 -> 0.1286 ms, conv7 equal (batch 64)
 
 // DNN_HIP_PATCH16=0/1 overrides the default choice of the patch kernel for eligible layers
@@ -298,7 +292,7 @@ static int patch16_span(long long M, int H, int W) {
     return (b * (H + 2) + oy + 1) * Wp + ox + 1;
   };
   long long mx = 0;
-  const int bm = p16_bm();
+  const int bm = P16_BM;
   for (long long m0 = 0; m0 < M; m0 += bm) {
     const long long last = m0 + bm - 1 < M ? m0 + bm - 1 : M - 1;
     const long long v = padded(last) - padded(m0) + 2 * (Wp + 1) + 1;
@@ -317,15 +311,22 @@ int launch_conv_patch16(const half_t* in_padded, const half_t* Bt, int ldb, half
     set_error("conv_patch16: unsupported shape M=%lld N=%d K=%d %dx%dx%d", M, N, K, H, W, C);
     return -2;
   }
-  const int bm = p16_bm();
+  const int bm = P16_BM;
   const int tilesM = (int)((M + bm - 1) / bm), tilesN = N / 256;
   const Patch16Geom pg{H, W, C, out_padded};
-  if (bm == 176)
-    hipLaunchKernelGGL((conv3x3_f16_patch_kernel<176, P16_NPR, half_t, 16>), dim3(tilesM * tilesN), dim3(512), 0,
-                       stream, in_padded, Bt, ldb, out, (int)M, N, K, epi, tilesM, pg, (unsigned)in_bytes);
+  // the row-skewed patch: span * 10 + 12 * (span / Wp + 2) 16-B units in the 56-KiB buffer
+  const long long span = patch16_span(M, H, W), b_bytes = (long long)N * ldb * 2;
+  if (span * 10 + 12 * (span / (W + 2) + 2) > 7 * 8 * 64 || b_bytes >= 0x80000000LL) {
+    set_error("conv_patch16: unsupported shape M=%lld N=%d K=%d %dx%dx%d", M, N, K, H, W, C);
+    return -2;
+  }
+  constexpr int F16YOLO = EPI_BN_AB | EPI_LEAKY_F32;  // the fp16 path's folded epilogue, compiled in
+  if (epi.flags == F16YOLO)
+    hipLaunchKernelGGL((conv3x3_f16_acc_kernel<P16_BM, P16_NPR, F16YOLO>), dim3(tilesM * tilesN), dim3(512), 0, stream,
+                       in_padded, Bt, ldb, out, (int)M, N, K, epi, tilesM, pg, (unsigned)in_bytes, (unsigned)b_bytes);
   else
-    hipLaunchKernelGGL((conv3x3_f16_patch_kernel<192, P16_NPR, half_t, 32>), dim3(tilesM * tilesN), dim3(512), 0,
-                       stream, in_padded, Bt, ldb, out, (int)M, N, K, epi, tilesM, pg, (unsigned)in_bytes);
+    hipLaunchKernelGGL((conv3x3_f16_acc_kernel<P16_BM, P16_NPR, -1>), dim3(tilesM * tilesN), dim3(512), 0, stream,
+                       in_padded, Bt, ldb, out, (int)M, N, K, epi, tilesM, pg, (unsigned)in_bytes, (unsigned)b_bytes);
   return check16("conv_patch16");
 }
 

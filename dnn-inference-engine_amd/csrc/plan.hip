@@ -85,7 +85,7 @@ static size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
 using namespace dnnhip;
 
-// MODE_PATCH16: fp16 3x3 conv on a zero-bordered input (conv3x3_f16_patch_kernel; conv6/conv7)
+// MODE_PATCH16: fp16 3x3 conv on a zero-bordered input (conv3x3_f16_acc_kernel; conv6/conv7)
 // MODE_X3: fp32 3x3 conv on the bf16 MFMA with exact 3-way splits, split zero-bordered input
 // (conv3x3_x3_patch_kernel; conv6/conv7 of the fp32 path)
 // MODE_X3_1X1: fp32 1x1 conv with the same arithmetic on its producer's split planes

@@ -1101,11 +1101,11 @@ PATCH16_CASES = [
 ]
 
 
-@pytest.mark.parametrize("mf", ["16", "32"])
 @pytest.mark.parametrize("case", PATCH16_CASES)
-def test_fp16_patch_conv_vs_oracle(monkeypatch, case, mf):
-    """conv3x3_f16_patch_kernel (input staged once per 64-channel chunk for all 9 taps, weights
-    straight to registers): whole chain within the fp16 layer tolerance of the fp32 oracle,
+def test_fp16_patch_conv_vs_oracle(monkeypatch, case):
+    """conv3x3_f16_acc_kernel (input LDS-DMA'd once per 64-channel chunk for all 9 taps into
+    row-skewed 160-B rows, weights straight to registers): whole chain within the fp16 layer
+    tolerance of the fp32 oracle,
     both convs on mode patch16, and batch rows independent of the batch (row 0 alone == row 0
     of the batch, bit for bit)."""
     B, H, W, C, od1, od2 = case
@@ -1131,7 +1131,6 @@ def test_fp16_patch_conv_vs_oracle(monkeypatch, case, mf):
         return g
 
     monkeypatch.setenv("DNN_HIP_PATCH16", "1")
-    monkeypatch.setenv("DNN_HIP_P16MF", mf)  # 16x16x32 (176-row tiles, default) / 32x32x16 (192-row)
     eng = dnn_hip.DnnInferenceEngine(graph(x.shape), False, precision="fp16")
     assert eng.plan().describe().count("mode=patch16") == 2
     y = eng.run(x)

@@ -23,6 +23,9 @@ O=$R/gpurun_out/${OUT:-job}
 mkdir -p "$O"
 cd "$R" || exit 1
 FAST="--no-cpu --no-latency --no-fp16 --no-unfused --no-e2e --no-fp32-mfma"
+# counter passes serialise every dispatch: no pre-heat / sustained windows there (the kernel-trace
+# passes keep them, so their durations are the steady-state ones)
+NOHEAT="--preheat 0 --sustained 0"
 
 run_tests() {
   timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread "$@" > "$O/pytest_gpu.log" 2>&1
@@ -103,22 +106,22 @@ EOF2
     # --gather outputs: no postprocess kernels on the side stream, so no other kernel runs
     # beside a profiled dispatch (GRBM_GUI_ACTIVE and the SQ counters sample the whole GPU:
     # a concurrent postprocess inflated round 2's conv4 row 5x)
-    prof "pmc_$group" --pmc $C -- --steps 3 --warmup 1 $FAST --gather outputs "$@"
+    prof "pmc_$group" --pmc $C -- --steps 3 --warmup 1 $FAST $NOHEAT --gather outputs "$@"
     ;;
   profiles)
     P="--gather outputs"
     prof fused_trace --kernel-trace --stats -- --steps 10 --warmup 3 $FAST || exit 1
-    prof fused_fetch --pmc FETCH_SIZE -- --steps 3 --warmup 1 $FAST $P || exit 1
-    prof fused_write --pmc WRITE_SIZE -- --steps 3 --warmup 1 $FAST $P || exit 1
+    prof fused_fetch --pmc FETCH_SIZE -- --steps 3 --warmup 1 $FAST $NOHEAT $P || exit 1
+    prof fused_write --pmc WRITE_SIZE -- --steps 3 --warmup 1 $FAST $NOHEAT $P || exit 1
     for g in sqa sqb; do bash "$0" pmc $g || exit 1; done
     export DNN_HIP_FUSE=0
     prof unf_trace --kernel-trace --stats -- --steps 10 --warmup 3 $FAST || exit 1
-    prof unf_fetch --pmc FETCH_SIZE -- --steps 3 --warmup 1 $FAST $P || exit 1
-    prof unf_write --pmc WRITE_SIZE -- --steps 3 --warmup 1 $FAST $P || exit 1
+    prof unf_fetch --pmc FETCH_SIZE -- --steps 3 --warmup 1 $FAST $NOHEAT $P || exit 1
+    prof unf_write --pmc WRITE_SIZE -- --steps 3 --warmup 1 $FAST $NOHEAT $P || exit 1
     unset DNN_HIP_FUSE
     prof f16_trace --kernel-trace --stats -- --steps 10 --warmup 3 $FAST --precision fp16 || exit 1
-    prof f16_fetch --pmc FETCH_SIZE -- --steps 3 --warmup 1 $FAST $P --precision fp16 || exit 1
-    prof f16_write --pmc WRITE_SIZE -- --steps 3 --warmup 1 $FAST $P --precision fp16 || exit 1
+    prof f16_fetch --pmc FETCH_SIZE -- --steps 3 --warmup 1 $FAST $NOHEAT $P --precision fp16 || exit 1
+    prof f16_write --pmc WRITE_SIZE -- --steps 3 --warmup 1 $FAST $NOHEAT $P --precision fp16 || exit 1
     echo PROFILESOK
     ;;
   full)

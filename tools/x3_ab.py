@@ -74,6 +74,7 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--preheat", type=float, default=3.0)
     ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--precision", default="fp32")
     ap.add_argument("--kernels", default="conv0,conv1,conv2,conv3,conv4,conv5,conv6,conv7,conv8")
     a = ap.parse_args()
     arms = [{}]
@@ -84,7 +85,7 @@ def main():
     B = a.batch
     ws = synth.yolo_weights()
     g, _ = yolo_graph.build_graph(dnn_hip.DnnGraphBuilder, ws, in_shape=(B, 416, 416, 3))
-    plan = dnn_hip.Plan.from_graph(g, device=0)
+    plan = dnn_hip.Plan.from_graph(g, device=0, precision=a.precision)
     frames = torch.rand((B, 416, 416, 3), generator=torch.Generator(device=dev).manual_seed(7), device=dev)
     out = torch.empty((B,) + plan.out_shape, device=dev)
     stream = torch.cuda.Stream(dev)
