@@ -304,7 +304,7 @@ int launch_conv3x3_patch_pool(const float* in, const float* Bt, int ldb, float* 
     return -2;
   }
   const size_t out_bytes = out_split ? (size_t)g.B * (g.PH + 2) * (g.PW + 2) * N * 6 : (size_t)g.B * g.PH * g.PW * N * 4;
-  if (C == 16 && N == 32 && out_bytes < OOB_OFF && !getenv_flag_off("DNN_HIP_PATCH_PERSIST")) {
+  if (C == 16 && N == 32 && out_bytes < OOB_OFF) {
     // persistent: as many workgroups as fit resident (3 per CU by LDS), each looping over tiles
     const long long slots = (long long)device_cu_count() * PP_WG_PER_CU;
     const unsigned grid = (unsigned)(blocks < slots ? blocks : slots);

@@ -367,7 +367,7 @@ static int launch_conv0(const float* in, const float* w, OutT* out, const Direct
 
 int launch_conv0_mfma(const float* in, const float* w, float* out, const DirectGeom& g, int cin, const float* zero,
                       const EpiParams& epi, hipStream_t s) {
-  if (cin != 3 || !zero || getenv_flag_off("DNN_HIP_CONV0_PACKED"))
+  if (cin != 3 || !zero)
     return launch_conv0<false, float>(in, w, out, g, cin, epi, s);
   if (g.B == 0) return 0;
   const int tilesX = (g.OW + SC_T - 1) / SC_T, tilesY = (g.OH + SC_T - 1) / SC_T;
@@ -392,9 +392,8 @@ int launch_conv0_mfma(const float* in, const float* w, float* out, const DirectG
   // allows (7 per CU at 72 registers: 28 per CU, ~6 tiles each), so the dispatcher refills CUs
   // that finish early.  Measured at batch 64 (workgroups per CU: ms): one resident round 7:
   // 0.185, 8 (the 8th as a lone second round): 0.168, 14: 0.153, 28: 0.1485, 56: 0.153, one tile
-  // per workgroup (169): 0.184.  DNN_HIP_CONV0_WGS overrides the per-CU count (experiments)
-  // (cached per instantiation and device: the occupancy query and DNN_HIP_CONV0_WGS are read on a
-  // device's first launch, so the grid is fixed per process and device)
+  // per workgroup (169): 0.184.
+  // (cached per instantiation and device: the occupancy query runs on a device's first launch)
   auto slots_of = [](const void* kern, long long (&cache)[64]) {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
@@ -402,7 +401,6 @@ int launch_conv0_mfma(const float* in, const float* w, float* out, const DirectG
     int v = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, kern, 256, 0) != hipSuccess || v < 1) v = 1;
     v = 4 * (v < 8 ? v : 8);
-    if (const char* e = getenv("DNN_HIP_CONV0_WGS")) v = atoi(e) > 0 ? atoi(e) : v;
     return cache[dev] = (long long)v * device_cu_count();
   };
 #define C0P(FL_, EV_)                                                                                           \

@@ -46,22 +46,6 @@ __device__ __forceinline__ void vm_wait() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-// Tile placement.  L = the XCD-contiguous tile index (xcd_tile: the ~T/8 consecutive values of
-// L run on one XCD).  The M tiles are cut into mg groups of sm = ceil(tilesM / mg), and inside
-// a group the tiles run N-panel-major: with mg = 1 an XCD's range is ~31 M tiles of one N panel
-// (every M row's patch fetched from beyond L2 by the 4 XCDs of its 4 panels); with mg = 4 it is
-// 2 panels x ~16 M tiles: each patch is read by 2 XCDs and each XCD streams 2 panels' weights
-// (per XCD and chunk 1.9 MB from beyond L2 against 2.3).  Measured (round 4, tools/x3_ab.py,
-// interleaved in one process): mg = 1, 2, 4 within 0.5 % on conv4-conv7, so the default stays 1.
-// Placement only: any mg gives the same products in the same order.
-__device__ __forceinline__ void x3_tile_of(int L, int tilesM, int mg, int& tm, int& tn, int tilesN) {
-  const int sm = (tilesM + mg - 1) / mg, gsz = sm * tilesN;
-  const int gi = L / gsz, r = L - gi * gsz;
-  const int gm = tilesM - gi * sm < sm ? tilesM - gi * sm : sm;  // >= 1: L < tilesM tilesN
-  tn = r / gm;
-  tm = gi * sm + (r - tn * gm);
-}
-
 // Structure: BM x 256 tiles, 8 waves of BM x 32 (two per SIMD, 256 registers each: the two
 // accumulator sets take 176), the weights of the next tap loaded while this one runs (48), the
 // patch of one 32-channel chunk staged by LDS-DMA into a double buffer (no staging registers),
@@ -97,9 +81,12 @@ conv3x3_x3_acc2_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __rest
   const int lane = threadIdx.x & 63;
   const int wid = wave_uniform(threadIdx.x >> 6);
   const int tile_s = xcd_tile(blockIdx.x, gridDim.x), ntiles = gridDim.x / g.splits;
-  const int split = tile_s / ntiles;
-  int tm, tn;
-  x3_tile_of(tile_s - split * ntiles, tilesM, g.mgroups, tm, tn, N / BN);
+  const int split = tile_s / ntiles, tile = tile_s - split * ntiles;
+  // tiles N-major inside each XCD's contiguous range (~31 M tiles of one N panel per XCD).
+  // (Round 4: 2 panels x ~16 M tiles per XCD, so each patch is fetched from beyond L2 by 2 XCDs
+  // instead of 4, measured within 0.5 % on conv4-conv7: the patch DMA's beyond-L2 bytes are not
+  // what costs -- tools/x3_ab.py, git history)
+  const int tn = tile / tilesM, tm = tile - tn * tilesM;
   const int m0 = tm * BM, n0 = tn * BN + wid * 32;  // this wave's 32 columns
   const int Wp = g.W + 2, HWo = g.H * g.W;
   auto padded = [&](int m) {

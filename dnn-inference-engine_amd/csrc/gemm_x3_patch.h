@@ -39,7 +39,6 @@ struct X3Geom {
                    // s at out + s*M*N (no epilogue; x3_combine_kernel finishes)
   int splits;      // K split into this many contiguous chunk ranges (grid = tiles x splits)
   int PH, PW;      // POOL kernels: the 2x2/s2 pooled output (rows are pool-window-major)
-  int mgroups = 1; // wide kernel: tiles placed as mgroups M ranges x all N panels (x3_tile_of)
 };
 
 __device__ __forceinline__ f32x4 mfma16_bf16(bf16x8 a, bf16x8 b, f32x4 c) {

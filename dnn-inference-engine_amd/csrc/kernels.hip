@@ -194,13 +194,8 @@ int launch_im2col(const float* in, float* col, const ConvGeom& g, hipStream_t st
   }
   const int kch = g.Kpad < IM2COL_KCH ? g.Kpad : IM2COL_KCH;
   // floats moved per block: 4 K for K-chunks of <= 1024 columns' worth of short rows (conv1-3:
-  // 5.4 -> 6.1 TB/s), 8 K for the long-K layers (conv4-7 lose with 4 K); DNN_HIP_IM2COL_FLOATS
-  // overrides (experiments)
-  static const int blk_env = [] {
-    const char* e = getenv("DNN_HIP_IM2COL_FLOATS");
-    return e && atoi(e) >= 1024 ? atoi(e) : 0;
-  }();
-  const int blk_floats = blk_env ? blk_env : (g.Kpad < IM2COL_KCH ? 4096 : IM2COL_BLOCK_FLOATS);
+  // 5.4 -> 6.1 TB/s), 8 K for the long-K layers (conv4-7 lose with 4 K)
+  const int blk_floats = g.Kpad < IM2COL_KCH ? 4096 : IM2COL_BLOCK_FLOATS;
   int rows = blk_floats / kch;
   rows = rows < 1 ? 1 : (rows > IM2COL_MAX_ROWS ? IM2COL_MAX_ROWS : rows);
   dim3 grid(ceil_div_i(M, rows), ceil_div_i(g.Kpad, IM2COL_KCH));
@@ -337,11 +332,11 @@ int choose_splitk(int N, int K, bool combine) {
   return 1;
 }
 
-// Latency plans.  When the batch rule's (cfg, splits) leaves the chip under 90 % occupied
-// (DNN_HIP_LAT_UNITS work units, default 256 = one per CU), every candidate tile config --
-// the batch rule's, 32x64 for N <= 128, and (DNN_HIP_LAT_CAND bit 2) 192x64 when M <= 192 --
-// is tried with every split S <= 32 that divides its K-steps into parts of at least
-// DNN_HIP_LAT_MINSTEPS (default 6); the pick maximises the balance
+// Latency plans.  When the batch rule's (cfg, splits) leaves the chip under 90 % occupied (256
+// work units = one per CU), every candidate tile config -- the batch rule's and 32x64 for N <=
+// 128 (192x64 when M <= 192 measured slower at batch 1: conv7 0.060 vs 0.051 ms) -- is tried
+// with every split S <= 32 that divides its K-steps into parts of at least 6; the pick
+// maximises the balance
 // units / (256 * ceil(units / 256)), then prefers fewer splits (less partial traffic in the
 // combine), then fewer units.  Batch 1 of YOLOv2-tiny: conv6/conv7 -> 32x128 x 16 splits (768
 // units), conv5 -> x 9, conv4 -> x 4, conv3 -> x 3, conv8 -> 32x64 x 4 (tools/lat_cfg_sweep_job.sh:
@@ -349,18 +344,10 @@ int choose_splitk(int N, int K, bool combine) {
 // memory round trips costs ~5 us per layer).
 void choose_latency_plan(long long M, int N, int K, int* cfg, int* splits, bool pool) {
   if (*cfg < GEMM_128x128_K32) return;
-  const char* e = getenv("DNN_HIP_LAT_UNITS");
-  const long long target = e && atoi(e) > 0 ? atoi(e) : 256;
-  const char* ms = getenv("DNN_HIP_LAT_MINSTEPS");
-  const int minsteps = ms && atoi(ms) > 0 ? atoi(ms) : 6;
+  const long long target = 256;
+  const int minsteps = 6;
   if (splitk_tiles(*cfg, M, N) * *splits * 10 >= target * 9) return;
-  // DNN_HIP_LAT_CAND (experiments): bit mask of the candidates tried; default 5 = the batch
-  // rule's config and 32x64 (192x64 measured slower at batch 1: conv7 0.060 vs 0.051 ms)
-  const char* ce = getenv("DNN_HIP_LAT_CAND");
-  const int cmask = ce && atoi(ce) > 0 ? atoi(ce) : 5;
-  int cand[3] = {(cmask & 1) ? *cfg : -1, -1, -1};
-  if ((cmask & 2) && M <= 192 && N % 64 == 0) cand[1] = GEMM_G192x64_W4;
-  if ((cmask & 4) && N <= 128) cand[2] = GEMM_G32x64_NS4;
+  int cand[2] = {*cfg, N <= 128 ? GEMM_G32x64_NS4 : -1};
   double best_eff = -1.0;
   long long best_units = 0;
   int best_cfg = *cfg, best_s = *splits;
@@ -456,11 +443,11 @@ static bool fits_buf(long long bytes) { return bytes > 0 && bytes < 0x80000000LL
 // DNN_HIP_GEMM_BUF=0: flat 64-bit DMA addresses (experiments and the equivalence tests)
 static bool abuf_enabled() { return !getenv_flag_off("DNN_HIP_GEMM_BUF"); }
 
-// N-major tile order (DNN_HIP_NMAJOR=1, experiment): tiles of one weight panel on one XCD
+// N-major tile order (round 1 experiment, measured without gain): off
 int nmajor_order(int N, int tilesN) {
-  const char* e = getenv("DNN_HIP_NMAJOR");
   (void)N;
-  return (e && e[0] == '1' && tilesN > 1) ? 1 : 0;
+  (void)tilesN;
+  return 0;
 }
 
 // configs whose waves hold <= 32 accumulator registers: the only ones with the any-split /
@@ -612,11 +599,7 @@ static int launch_persist_t(const float* Bt, int ldb, float* C, int ldc, int M, 
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, kern, WM * WN * 64, 0) != hipSuccess) v = 0;
     per_cu = v;
   }
-  int wgs = per_cu;
-  if (const char* e = getenv("DNN_HIP_PERSIST_WGS")) {  // experiments: workgroups per CU
-    const int v = atoi(e);
-    if (v > 0 && v < wgs) wgs = v;
-  }
+  const int wgs = per_cu;
   long long grid = (long long)device_cus() * wgs;
   // fewer than two tiles per workgroup: the tail of the ones holding two costs more than the
   // pipelining gains (conv4 at batch 64: 452 tiles on 448 slots, 0.224 -> 0.317 ms)

@@ -239,9 +239,8 @@ int launch_x3_combine(const float* part, int splits, long long slab, const EpiPa
     return -2;
   }
   const int win = g.kh == 2 && g.kw == 2 ? 2 : g.kh == 1 && g.kw == 1 ? 1 : 0;
-  // many slices (> 2: latency plans): 4 channels per thread (DNN_HIP_X3C_CPT=8: 8)
-  const char* ce = getenv("DNN_HIP_X3C_CPT");
-  const int cpt = splits > 2 && win > 0 && !(ce && atoi(ce) == 8) ? 4 : 8;
+  // many slices (> 2: latency plans): 4 channels per thread (8 measured slower there)
+  const int cpt = splits > 2 && win > 0 ? 4 : 8;
   const long long total = (long long)g.B * g.OH * g.OW * (g.C / cpt);
   if ((total + 255) / 256 > 0x7fffffffLL) {
     set_error("x3_combine: %lld outputs", total);
@@ -509,13 +508,7 @@ int launch_conv_x3(const bf16_bits* in_split, const bf16_bits* Bt, float* out, b
   }
   const int tilesM = (int)((M + X3_BM - 1) / X3_BM), tilesN = N / 256;
   // splits > 1: `out` receives the raw partials [splits][M][N] (x3_combine_kernel finishes).
-  // Tile placement (gemm_x3_acc2.h x3_tile_of): mgroups M ranges x all N panels, so each XCD's
-  // tiles cover tilesN / (8 / mgroups) panels; DNN_HIP_X3_MG overrides (experiments: read per
-  // launch, so one process can interleave placements -- placement never changes a bit)
-  const char* mge = getenv("DNN_HIP_X3_MG");
-  const int mg_env = mge ? atoi(mge) : 0;
-  const int mg = mg_env > 0 ? mg_env : 1;  // (measured: 1, 2 and 4 equal within 0.5 %, round 4)
-  const X3Geom xg{H, W, C, splits > 1 ? 2 : out_split ? 1 : 0, splits, PH, PW, mg < tilesM ? mg : 1};
+  const X3Geom xg{H, W, C, splits > 1 ? 2 : out_split ? 1 : 0, splits, PH, PW};
   const dim3 grid(tilesM * tilesN * (pool ? 1 : splits));
 #define X3AF(NPR_, POOL_, FL_)                                                                                    \
   hipLaunchKernelGGL((conv3x3_x3_acc2_kernel<X3_BM, NPR_, POOL_, FL_>), grid, dim3(512), 0, stream, in_split, Bt, \
@@ -555,7 +548,7 @@ constexpr int X3L_NPR_SMALL = 240;  // one 13x13 frame's tile spans 225 padded r
 bool conv_x3_lat_supported(long long batch, int C, int OC, int H, int W, int OH, int OW, int kh, int kw, int sh,
                            int sw, int pt, int pl) {
   if (!(kh == 3 && kw == 3 && sh == 1 && sw == 1 && pt == 1 && pl == 1 && OH == H && OW == W && C % 32 == 0 &&
-        OC % 64 == 0 && x3_enabled() && !getenv_flag_off("DNN_HIP_X3_LAT")))
+        OC % 64 == 0 && x3_enabled()))
     return false;
   const long long M = batch * H * W;
   // only where one-chunk slices fill half the chip (conv6 / conv7 of a frame: 256 / 512): with
@@ -587,7 +580,7 @@ int launch_conv_x3_lat(const bf16_bits* in_split, const bf16_bits* Bt, float* pa
     set_error("conv_x3_lat: grid too large");
     return -2;
   }
-  const X3Geom xg{H, W, C, 2, splits, 0, 0, 0};
+  const X3Geom xg{H, W, C, 2, splits, 0, 0};
 #define X3L(CPW_, NPR_)                                                                                       \
   hipLaunchKernelGGL((conv3x3_x3_lat_kernel<2, CPW_, NPR_>), dim3((unsigned)blocks), dim3(512), 0, stream, in_split, \
                      Bt, part, (int)M, N, K, tilesM, xg, (unsigned)in_bytes, (unsigned)b_bytes)
@@ -623,24 +616,19 @@ int launch_conv_x3_1x1(const bf16_bits* in_split, const bf16_bits* Bt, float* ou
     set_error("conv_x3_1x1: unsupported shape M=%lld N=%d K=%d %dx%dx%d", M, N, K, H, W, C);
     return -2;
   }
-  // 16 TMW-row tiles: 2 (32 rows, 338 workgroups at batch 64) or 4 (DNN_HIP_X3_1X1_TM=4: 64 rows)
-  static const int tmw = [] {
-    const char* e = getenv("DNN_HIP_X3_1X1_TM");
-    return e && atoi(e) == 4 ? 4 : 2;
-  }();
+  // 32-row tiles (338 workgroups at batch 64; 64-row tiles measured 0.039 vs 0.0355 ms)
+  constexpr int tmw = 2;
   const long long tilesM = (M + 16 * tmw - 1) / (16 * tmw), blocks = tilesM * (Npad / X3_1X1_BN);
   if (blocks > 0x7fffffffLL) {
     set_error("conv_x3_1x1: grid too large");
     return -2;
   }
-  const X3Geom xg{H, W, C, 0, 1, 0, 0, 0};
+  const X3Geom xg{H, W, C, 0, 1, 0, 0};
   constexpr int BIAS = EPI_BIAS;
 #define X1(FL_, TM_)                                                                                             \
   hipLaunchKernelGGL((conv1x1_x3_kernel<FL_, TM_>), dim3((unsigned)blocks), dim3(256), 0, stream, in_split, Bt, \
                      out, (int)M, N, K, epi, (int)tilesM, xg, (unsigned)in_bytes, (unsigned)b_bytes)
-  if (epi.flags == BIAS && tmw == 4)  // YOLO's detection layer: bias, linear
-    X1(BIAS, 4);
-  else if (epi.flags == BIAS)
+  if (epi.flags == BIAS)  // YOLO's detection layer: bias, linear
     X1(BIAS, 2);
   else
     X1(-1, 2);

@@ -323,15 +323,6 @@ static void set_cfg(dnn_plan* p, PlanLayer& L) {
   }
   if (p->fp16) {  // fp16 MFMA configs: BK = 64 halves, split rule on (N, K) only
     L.cfg = choose_gemm16_cfg(M, L.OC, L.K);
-    if (const char* e = getenv("DNN_HIP_CFG16")) {  // tuning experiments: "K:cfg,K:cfg,..."
-      for (const char* q = e; *q;) {
-        int k = 0, c = 0, n = 0;
-        if (sscanf(q, "%d:%d%n", &k, &c, &n) != 2) break;
-        if (k == L.K && c >= 0 && c < GEMM16_NUM_CFGS) L.cfg = c;
-        q += n;
-        if (*q == ',') ++q;
-      }
-    }
     L.Kpad = (int)align_up(L.K, 64);
     L.Npad = (int)align_up(L.OC, gemm16_cfg_bn(L.cfg));
     L.splits = (L.Kpad == L.K) ? choose_splitk16(L.OC, L.K) : 1;
@@ -558,8 +549,7 @@ int dnn_plan_add_max_pool(dnn_plan* p, int kh, int kw, int stride_h, int stride_
                                                                       prev.sw)) {
         prev.mode = MODE_DIRECT;
         ok = true;
-      } else if (prev.mode == MODE_X3 && !p->fp16 && conv_x3_pool_supported(prev.OC, prev.C, prev.H, prev.W) &&
-                 !getenv_flag_off("DNN_HIP_X3_POOL")) {
+      } else if (prev.mode == MODE_X3 && !p->fp16 && conv_x3_pool_supported(prev.OC, prev.C, prev.H, prev.W)) {
         ok = true;  // pool-window-major rows, pooled before the epilogue in the x3 kernel
       }
       if (ok) {

@@ -1557,23 +1557,6 @@ def test_conv0_conv1_chain(monkeypatch, case):
     assert R.normwise_err(outs["2"], ref) <= 1.25 * max(R.normwise_err(outs["1"], ref), 1e-7)
 
 
-def test_x3_tile_placement_same_bits(monkeypatch, golden_frames):
-    """The wide x3 kernel's tile placement (gemm_x3_acc2.h x3_tile_of: mgroups M ranges x all N
-    panels per XCD range; DNN_HIP_X3_MG, read per launch) moves tiles between XCDs only: the whole
-    net at batch 3 (conv4-conv7 on that kernel, conv5 in 2 K slices) gives the same bits for
-    mgroups 1, 2, 3 (ragged groups), 4 (the default for 4 panels) and 8."""
-    x = synth.frames([0, 1, 2])
-    g, _ = yolo_graph.build_graph(dnn_hip.DnnGraphBuilder, synth.yolo_weights(), in_shape=x.shape)
-    eng = dnn_hip.DnnInferenceEngine(g, False)
-    outs = {}
-    for mg in ("1", "2", "3", "4", "8"):
-        monkeypatch.setenv("DNN_HIP_X3_MG", mg)
-        outs[mg] = eng.run(x)
-    for mg in outs:
-        assert np.array_equal(outs[mg], outs["4"]), mg
-    assert R.normwise_err(outs["4"][:1], golden_frames[0]) < NET_TOL
-
-
 @pytest.mark.parametrize("kind", ["huge", "tiny"])
 def test_x3_split_total_over_finite_fp32(monkeypatch, kind):
     """split3 (gemm_f32.h) is total over finite fp32: an operand above the largest bf16

@@ -2,9 +2,9 @@
 §5.4 rule 24: variants interleaved in one process, after a >= 2 s pre-heat at the clock the
 chip holds under load).
 
-  python tools/x3_ab.py --env DNN_HIP_X3_MG=1,4 [--rounds 6] [--iters 20] [--preheat 3]
+  python tools/x3_ab.py --env DNN_HIP_X3_C16P=0,2 [--env DNN_AB_DUMMY=a,b] [--rounds 6] [--iters 20] [--preheat 3]
 
-Only switches read per launch take effect between arms (DNN_HIP_X3_MG).  Prints, per arm, the
+Only switches read per launch take effect between arms (DNN_HIP_X3_C16P; a switch no code reads, e.g. DNN_AB_DUMMY, gives null arms: the noise floor).  Prints, per arm, the
 median over rounds of each kernel's mean HIP-event time and of the forward.  With a library
 built with X3DIAG bit 16 (tools/build_diag.sh 16, DNN_HIP_LIB=diag/libdnn_hip_d16.so) it also
 reads the wide x3 kernel's per-workgroup s_memtime / s_memrealtime stamps of the last conv7
