@@ -195,6 +195,11 @@ conv0_mfma_pool_kernel(const float* __restrict__ in, const float* __restrict__ w
 // step s reads k = 4s + p at a per-lane LDS offset koff[s] (dy*RS + dx*CIN + c) from its
 // pixel, the M-tile offset being an immediate.  (RS = 56: every ds_read_b32 is exactly
 // 2-way; no row stride makes the two pixel rows of an M-tile conflict-free.)
+// C0DIAG (diagnostic builds only, wrong results): bit 1 drops the loop's patch DMA, 2 the pool and
+// epilogue arithmetic, 4 the MFMAs (a VALU multiply-add on the same LDS reads instead)
+#ifndef C0DIAG
+#define C0DIAG 0
+#endif
 constexpr int C0_RS = 56;  // patch row stride (floats) >= 18 * CIN
 constexpr int C0_ROWS_PER_WAVE = 5;  // 20 row DMAs per tile over 4 waves (rows 18, 19 dummies)
 
@@ -291,7 +296,7 @@ conv0_packed_pool_kernel(const float* __restrict__ in, const float* __restrict__
     // tile t+2 into the buffer tile t-1 used (dummy past the end: the count stays fixed)
     const int t2 = t + 2 * G;
     const Tile nn = coords(t2 < ntiles ? t2 : 0);
-    issue(nn, t2 < ntiles, buf == 0 ? 2 : buf - 1);
+    if (!(C0DIAG & 1)) issue(nn, t2 < ntiles, buf == 0 ? 2 : buf - 1);
     const float* P = patch[buf];
 
     f32x4 acc[4];
@@ -301,8 +306,12 @@ conv0_packed_pool_kernel(const float* __restrict__ in, const float* __restrict__
     for (int s = 0; s < KS; ++s) {
       const float* a = P + pix0 + koff[s];
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
-        acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[2 * (i >> 1) * RS + 8 * (i & 1) * CIN], wv[s], acc[i], 0, 0, 0);
+      for (int i = 0; i < 4; ++i) {
+        if constexpr ((C0DIAG & 4) != 0)
+          acc[i][s & 3] += a[2 * (i >> 1) * RS + 8 * (i & 1) * CIN] * wv[s];
+        else
+          acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[2 * (i >> 1) * RS + 8 * (i & 1) * CIN], wv[s], acc[i], 0, 0, 0);
+      }
     }
 
     const int b = cur.b, y0 = cur.ty * SC_T, x0 = cur.tx * SC_T;
@@ -317,7 +326,10 @@ conv0_packed_pool_kernel(const float* __restrict__ in, const float* __restrict__
         const bool x1 = 2 * wx + 1 < g.OW, y1 = 2 * wy + 1 < g.OH;
         v = f32x4{acc[i][0], x1 ? acc[i][1] : acc[i][0], y1 ? acc[i][2] : acc[i][0], x1 && y1 ? acc[i][3] : acc[i][0]};
       }
-      stage[wid][i >> 1][4 * (i & 1) + fp][n] = pool_then_epilogue_t<FL>(v, pb_, pm, ps, pg, epi.flags);
+      if constexpr ((C0DIAG & 2) != 0)
+        stage[wid][i >> 1][4 * (i & 1) + fp][n] = v[0] + v[1] + v[2] + v[3];
+      else
+        stage[wid][i >> 1][4 * (i & 1) + fp][n] = pool_then_epilogue_t<FL>(v, pb_, pm, ps, pg, epi.flags);
     }
     wait_lgkm0();  // the stage is wave-private
     {  // one 16-B store per lane (2 window rows x 8 windows x 16 channels per wave)
