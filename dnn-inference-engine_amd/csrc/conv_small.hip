@@ -203,6 +203,13 @@ conv0_mfma_pool_kernel(const float* __restrict__ in, const float* __restrict__ w
 constexpr int C0_RS = 56;  // patch row stride (floats) >= 18 * CIN
 constexpr int C0_ROWS_PER_WAVE = 5;  // 20 row DMAs per tile over 4 waves (rows 18, 19 dummies)
 
+// Round 4 diagnostics (same box): without the loop's patch DMA 0.124 -> 0.104 ms, without the
+// pool/epilogue arithmetic 0.110, without the MFMAs (a VALU FMA on the same LDS reads) 0.083.
+// An x3 conv0 (K = 9 taps x (3 channels + 0) on 3 steps of v_mfma_f32_16x16x16_bf16 from a split
+// patch [piece][pixel][4], 144 instead of 224 MFMA cycles per 16 pixels, register-staged frame
+// loads split on the way into LDS) measured 0.149 vs 0.138 ms in one process: the split staging,
+// the 2.6x LDS read bytes and 5 instead of 7 waves per SIMD cost more than the MFMA cycles saved
+// (git history).
 // FL: the epilogue flag set at compile time (-1: runtime `epi.flags`); EVEN: OH and OW even, so
 // no pool window is ragged (YOLO's 416 x 416: the per-window edge selects drop out).  (Round 3's
 // SPL form stored conv1's split planes here: conv1 -15 us, conv0 +23 us; removed, git history.)
