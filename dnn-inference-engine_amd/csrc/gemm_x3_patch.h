@@ -28,7 +28,18 @@
 #pragma once
 #include "gemm_f16.h"
 
+// X3DIAG (diagnostic builds only, tools/build_diag.sh; see also gemm_x3_acc2.h): bit 32 records
+// conv3x3_x3_c16p_kernel's per-workgroup phase cycles (results unchanged), bit 64 drops its pool /
+// epilogue math, bit 128 replaces its input split by a 2-instruction truncation (wrong results)
+#ifndef X3DIAG
+#define X3DIAG 0
+#endif
 namespace dnnhip {
+
+#if (X3DIAG & 32) != 0  // conv3x3_x3_c16p_kernel phase cycles (gemm_x3_patch.h)
+constexpr int C16_DIAG_WGS = 1024;
+__device__ unsigned long long c16_diag_stamps[C16_DIAG_WGS * 4];  // [workgroup][split, mfma, epilogue, tiles]
+#endif
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
@@ -362,7 +373,7 @@ conv3x3_x3_c16_kernel(const float* __restrict__ in, const bf16_bits* __restrict_
 // MFMAs per block and column block, if the K = 16 form issues in half the cycles.  Summation
 // order: as the 16-channel kernel (two accumulators; steps 0-4), the order depending on (N, K)
 // only.  LDS: 30 KB weights + 48 KB split patch + 1.7 KB row table = 79 KB (two per CU).
-template <bool POOL, bool HALF>
+template <bool POOL, bool HALF, int FL = -1>
 __global__ void __launch_bounds__(256, 2)
 conv3x3_x3_c16p_kernel(const float* __restrict__ in, const bf16_bits* __restrict__ Bt, float* __restrict__ out,
                        bf16_bits* __restrict__ out_split, int N, EpiParams epi, int tilesX, int tilesY, int ntiles,
@@ -380,6 +391,7 @@ conv3x3_x3_c16p_kernel(const float* __restrict__ in, const bf16_bits* __restrict
   int* const orow = reinterpret_cast<int*>(smem + BB + PATCH);
 
   const int lane = threadIdx.x & 63;
+  const int eflags = FL < 0 ? epi.flags : FL;  // FL: the epilogue flag set compiled in (-1: runtime)
   const int wm = wave_uniform(threadIdx.x >> 6);
   const int fr = lane & 15, fq = lane >> 4, th = fq >> 1;
   const int Wp = g.W + 2;
@@ -437,8 +449,17 @@ conv3x3_x3_c16p_kernel(const float* __restrict__ in, const bf16_bits* __restrict
       e = e < ITEMS ? e : ITEMS - 1;
       const int dst = (e >> 2) * PB + 8 * (e & 3);
       uint2 w[3];
-      split3_pack2(fast, stg[d][0], stg[d][1], w[0].x, w[1].x, w[2].x);
-      split3_pack2(fast, stg[d][2], stg[d][3], w[0].y, w[1].y, w[2].y);
+      if constexpr ((X3DIAG & 128) != 0) {  // (diagnostic: truncating 2-piece "split", 2 v_perm per pair)
+        const unsigned a0 = __builtin_bit_cast(unsigned, stg[d][0]), a1 = __builtin_bit_cast(unsigned, stg[d][1]);
+        const unsigned a2 = __builtin_bit_cast(unsigned, stg[d][2]), a3 = __builtin_bit_cast(unsigned, stg[d][3]);
+        w[0] = uint2{__builtin_amdgcn_perm(a1, a0, 0x07060302u), __builtin_amdgcn_perm(a3, a2, 0x07060302u)};
+        w[1] = uint2{__builtin_amdgcn_perm(a1, a0, 0x05040100u), __builtin_amdgcn_perm(a3, a2, 0x05040100u)};
+        w[2] = uint2{0u, 0u};
+        (void)fast;
+      } else {
+        split3_pack2(fast, stg[d][0], stg[d][1], w[0].x, w[1].x, w[2].x);
+        split3_pack2(fast, stg[d][2], stg[d][3], w[0].y, w[1].y, w[2].y);
+      }
 #pragma unroll
       for (int p = 0; p < 3; ++p) *reinterpret_cast<uint2*>(patch + dst + 32 * p) = w[p];
     }
@@ -497,8 +518,24 @@ conv3x3_x3_c16p_kernel(const float* __restrict__ in, const bf16_bits* __restrict
 
   const int G = gridDim.x;
   int t = blockIdx.x;
+#if (X3DIAG & 32) != 0  // per-phase s_memtime sums: tile top -> split barrier -> MFMA barrier -> tile end
+  unsigned long long dg_a = 0, dg_b = 0, dg_c = 0, dg_n = 0, dg_t0 = 0, dg_t1 = 0;
+#define C16_STAMP(acc)                                       \
+  {                                                          \
+    const unsigned long long now = __builtin_amdgcn_s_memtime(); \
+    acc += now - dg_t1;                                      \
+    dg_t1 = now;                                             \
+  }
+#else
+#define C16_STAMP(acc)
+#endif
   if (t < ntiles) load_tile(t);
   while (t < ntiles) {
+#if (X3DIAG & 32) != 0
+    dg_t0 = dg_t1 = __builtin_amdgcn_s_memtime();
+    (void)dg_t0;
+    ++dg_n;
+#endif
     int b, y0, x0;
     tile_xy(t, b, y0, x0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -519,6 +556,7 @@ conv3x3_x3_c16p_kernel(const float* __restrict__ in, const bf16_bits* __restrict
     const int tn = t + G;
     if (tn < ntiles) load_tile(tn);  // in flight during this tile's MFMAs
     __syncthreads();                 // the patch, the row table (and, first time, the weights) written
+    C16_STAMP(dg_a)
 
     f32x4 acc[TM][2], accc[TM][2];
 #pragma unroll
@@ -576,6 +614,7 @@ conv3x3_x3_c16p_kernel(const float* __restrict__ in, const bf16_bits* __restrict
     }
     x3_fold(acc, accc);
     __syncthreads();  // every wave is done with the patch: the epilogue stages reuse it
+    C16_STAMP(dg_b)
 
     if constexpr (POOL) {
       if (g.out_mode == 1) {  // staged 16-B split-plane stores (x3_pool_split_store)
@@ -583,16 +622,19 @@ conv3x3_x3_c16p_kernel(const float* __restrict__ in, const bf16_bits* __restrict
 #pragma unroll
         for (int jb = 0; jb < 2; ++jb) {
           const int n = 16 * jb + fr;
-          const float pb = (epi.flags & EPI_BIAS) ? epi.bias[n] : 0.f;
-          const float pm = (epi.flags & (EPI_BN | EPI_BN_AB)) ? epi.mean[n] : 0.f;
-          const float ps = (epi.flags & (EPI_BN | EPI_BN_AB)) ? epi.sq[n] : 1.f;
-          const float pg = (epi.flags & EPI_BN) ? epi.gamma[n] : 1.f;
+          const float pb = (eflags & EPI_BIAS) ? epi.bias[n] : 0.f;
+          const float pm = (eflags & (EPI_BN | EPI_BN_AB)) ? epi.mean[n] : 0.f;
+          const float ps = (eflags & (EPI_BN | EPI_BN_AB)) ? epi.sq[n] : 1.f;
+          const float pg = (eflags & EPI_BN) ? epi.gamma[n] : 1.f;
 #pragma unroll
           for (int i = 0; i < TM; ++i)
-            stgp[(4 * i + fq) * X3_STG_ROW + 16 * jb + fr] = pool_then_epilogue(acc[i][jb], pb, pm, ps, pg, epi.flags);
+            stgp[(4 * i + fq) * X3_STG_ROW + 16 * jb + fr] =
+                (X3DIAG & 64) != 0 ? acc[i][jb][0] + pb  // (diagnostic: no pool / epilogue math)
+                                   : pool_then_epilogue_t<FL>(acc[i][jb], pb, pm, ps, pg, epi.flags);
         }
         x3_pool_split_store<TM>(stgp, orow, NO, 4 * wm * TM, out_split, 96, 0, lane);
         __syncthreads();  // stages read before the next tile's split overwrites the patch area
+        C16_STAMP(dg_c)
         t = tn;
         continue;
       }
@@ -600,10 +642,10 @@ conv3x3_x3_c16p_kernel(const float* __restrict__ in, const bf16_bits* __restrict
 #pragma unroll
     for (int jb = 0; jb < 2; ++jb) {
       const int n = 16 * jb + fr;
-      const float pb = (epi.flags & EPI_BIAS) ? epi.bias[n] : 0.f;
-      const float pm = (epi.flags & (EPI_BN | EPI_BN_AB)) ? epi.mean[n] : 0.f;
-      const float ps = (epi.flags & (EPI_BN | EPI_BN_AB)) ? epi.sq[n] : 1.f;
-      const float pg = (epi.flags & EPI_BN) ? epi.gamma[n] : 1.f;
+      const float pb = (eflags & EPI_BIAS) ? epi.bias[n] : 0.f;
+      const float pm = (eflags & (EPI_BN | EPI_BN_AB)) ? epi.mean[n] : 0.f;
+      const float ps = (eflags & (EPI_BN | EPI_BN_AB)) ? epi.sq[n] : 1.f;
+      const float pg = (eflags & EPI_BN) ? epi.gamma[n] : 1.f;
       auto put = [&](int o, float v) {
         if (g.out_mode == 1) {
           unsigned short s0, s1, s2;
@@ -622,13 +664,13 @@ conv3x3_x3_c16p_kernel(const float* __restrict__ in, const bf16_bits* __restrict
         if constexpr (POOL) {
           const int w = rb / 4 + fq;
           const int o = w < NO ? orow[w] : -1;
-          if (o >= 0) put(o, pool_then_epilogue(acc[i][jb], pb, pm, ps, pg, epi.flags));
+          if (o >= 0) put(o, pool_then_epilogue_t<FL>(acc[i][jb], pb, pm, ps, pg, epi.flags));
         } else {
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int row = rb + 4 * fq + r;
             const int o = row < NO ? orow[row] : -1;
-            if (o >= 0) put(o, apply_epilogue(acc[i][jb][r], pb, pm, ps, pg, epi.flags));
+            if (o >= 0) put(o, apply_epilogue_t<FL>(acc[i][jb][r], pb, pm, ps, pg, epi.flags));
           }
         }
       }
@@ -636,6 +678,16 @@ conv3x3_x3_c16p_kernel(const float* __restrict__ in, const bf16_bits* __restrict
     __syncthreads();  // the row table is rewritten by the next tile
     t = tn;
   }
+#if (X3DIAG & 32) != 0
+  if (threadIdx.x == 0 && blockIdx.x < C16_DIAG_WGS) {  // (vector stores from lane 0)
+    unsigned long long* d = c16_diag_stamps + 4 * blockIdx.x;
+    d[0] = dg_a;
+    d[1] = dg_b;
+    d[2] = dg_c;
+    d[3] = dg_n;
+  }
+#endif
+#undef C16_STAMP
 }
 
 
@@ -656,7 +708,7 @@ conv3x3_x3_c16p_kernel(const float* __restrict__ in, const bf16_bits* __restrict
 // j starts (NBUF = 2) or after it (NBUF = 1, one buffer).  Two accumulators per output (A2) for
 // every configuration.  (Rounds 2-3: register-staged 192-B rows with an XOR swizzle, per-step adds
 // for N = 128: conv3 0.127 -> 0.114 ms, conv2 0.129 -> 0.126 ms with this form; git history.)
-template <int TH, int TW, int WM, int WN, int TM, int NBUF, bool POOL>
+template <int TH, int TW, int WM, int WN, int TM, int NBUF, bool POOL, int FL = -1>
 __global__ void __launch_bounds__(64 * WM * WN, 512 / (64 * WM * WN))
 conv3x3_x3_tile2_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __restrict__ Bt, float* __restrict__ out,
                         bf16_bits* __restrict__ out_split, int N, int K, EpiParams epi, int tilesX, int tilesY,
@@ -670,6 +722,7 @@ conv3x3_x3_tile2_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __res
   __shared__ __attribute__((aligned(1024))) unsigned char smem[NBUF * BUFB];
 
   const int lane = threadIdx.x & 63;
+  const int eflags = FL < 0 ? epi.flags : FL;  // FL: the epilogue flag set compiled in (-1: runtime)
   const int wid = wave_uniform(threadIdx.x >> 6);
   const int wn = wid % WN, wm = wid / WN;
   int t = xcd_tile(blockIdx.x, gridDim.x);
@@ -821,13 +874,13 @@ conv3x3_x3_tile2_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __res
 #pragma unroll
       for (int jb = 0; jb < 2; ++jb) {
         const int n = n0 + 16 * jb + fr;
-        const float pb = (epi.flags & EPI_BIAS) ? epi.bias[n] : 0.f;
-        const float pm = (epi.flags & (EPI_BN | EPI_BN_AB)) ? epi.mean[n] : 0.f;
-        const float ps = (epi.flags & (EPI_BN | EPI_BN_AB)) ? epi.sq[n] : 1.f;
-        const float pg = (epi.flags & EPI_BN) ? epi.gamma[n] : 1.f;
+        const float pb = (eflags & EPI_BIAS) ? epi.bias[n] : 0.f;
+        const float pm = (eflags & (EPI_BN | EPI_BN_AB)) ? epi.mean[n] : 0.f;
+        const float ps = (eflags & (EPI_BN | EPI_BN_AB)) ? epi.sq[n] : 1.f;
+        const float pg = (eflags & EPI_BN) ? epi.gamma[n] : 1.f;
 #pragma unroll
         for (int i = 0; i < TM; ++i)
-          stg[(4 * i + fq) * X3_STG_ROW + 16 * jb + fr] = pool_then_epilogue(acc[i][jb], pb, pm, ps, pg, epi.flags);
+          stg[(4 * i + fq) * X3_STG_ROW + 16 * jb + fr] = pool_then_epilogue_t<FL>(acc[i][jb], pb, pm, ps, pg, epi.flags);
       }
       x3_pool_split_store<TM>(stg, orow, NO, 4 * wm * TM, out_split, 3 * (size_t)N, (n0 >> 5) * 96, lane);
       return;
@@ -836,10 +889,10 @@ conv3x3_x3_tile2_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __res
 #pragma unroll
   for (int jb = 0; jb < 2; ++jb) {
     const int n = n0 + 16 * jb + fr;  // < N: N % (32 WN) == 0 (launcher)
-    const float pb = (epi.flags & EPI_BIAS) ? epi.bias[n] : 0.f;
-    const float pm = (epi.flags & (EPI_BN | EPI_BN_AB)) ? epi.mean[n] : 0.f;
-    const float ps = (epi.flags & (EPI_BN | EPI_BN_AB)) ? epi.sq[n] : 1.f;
-    const float pg = (epi.flags & EPI_BN) ? epi.gamma[n] : 1.f;
+    const float pb = (eflags & EPI_BIAS) ? epi.bias[n] : 0.f;
+    const float pm = (eflags & (EPI_BN | EPI_BN_AB)) ? epi.mean[n] : 0.f;
+    const float ps = (eflags & (EPI_BN | EPI_BN_AB)) ? epi.sq[n] : 1.f;
+    const float pg = (eflags & EPI_BN) ? epi.gamma[n] : 1.f;
     const int cofs = (n >> 5) * 96 + (n & 31);
     auto put = [&](int o, float v) {
       if (g.out_mode == 1) {
@@ -859,13 +912,13 @@ conv3x3_x3_tile2_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __res
       if constexpr (POOL) {
         const int w = rb / 4 + fq;
         const int o = w < NO ? orow[w] : -1;
-        if (o >= 0) put(o, pool_then_epilogue(acc[i][jb], pb, pm, ps, pg, epi.flags));
+        if (o >= 0) put(o, pool_then_epilogue_t<FL>(acc[i][jb], pb, pm, ps, pg, epi.flags));
       } else {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int row = rb + 4 * fq + r;
           const int o = row < NO ? orow[row] : -1;
-          if (o >= 0) put(o, apply_epilogue(acc[i][jb][r], pb, pm, ps, pg, epi.flags));
+          if (o >= 0) put(o, apply_epilogue_t<FL>(acc[i][jb][r], pb, pm, ps, pg, epi.flags));
         }
       }
     }

@@ -12,6 +12,8 @@
 
 namespace dnnhip {
 
+constexpr int X3_YOLO_FL = EPI_BIAS | EPI_BN | EPI_LEAKY_F64;  // YOLO's epilogue set (compiled-in forms)
+
 static int check_x3(const char* what) {
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
@@ -452,12 +454,24 @@ int launch_conv_x3(const bf16_bits* in_split, const bf16_bits* Bt, float* out, b
       const long long slots = 2LL * device_cu_count();
       const dim3 pgrid((unsigned)(blocks < slots ? blocks : slots));
 #define C16P(POOL_, HALF_)                                                                                     \
-  hipLaunchKernelGGL((conv3x3_x3_c16p_kernel<POOL_, HALF_>), pgrid, dim3(256), 0, stream, in32p, Bt, out, out_split, \
+  hipLaunchKernelGGL((conv3x3_x3_c16p_kernel<POOL_, HALF_, C16P_FL>), pgrid, dim3(256), 0, stream, in32p, Bt, out, out_split, \
                      N, epi, tilesX, tilesY, (int)blocks, xg, (unsigned)in32)
-      if (pv == 2)
-        C16P(true, true);
-      else
-        C16P(true, false);
+      // YOLO's epilogue set compiled in (bias + BatchNorm + double-rounded leaky; same arithmetic)
+      if (epi.flags == X3_YOLO_FL) {
+#define C16P_FL X3_YOLO_FL
+        if (pv == 2)
+          C16P(true, true);
+        else
+          C16P(true, false);
+#undef C16P_FL
+      } else {
+#define C16P_FL -1
+        if (pv == 2)
+          C16P(true, true);
+        else
+          C16P(true, false);
+#undef C16P_FL
+      }
 #undef C16P
     }
     return check_x3("conv_x3 (c16)");
@@ -482,18 +496,23 @@ int launch_conv_x3(const bf16_bits* in_split, const bf16_bits* Bt, float* out, b
     }
     const X3Geom xg{H, W, C, out_split ? 1 : 0, 1, PH, PW};
     // conv3x3_x3_tile2_kernel: 224-B LDS rows by LDS-DMA, immediate tap offsets, two accumulators
-#define X3T2(TH_, TW_, WM, WN, NBUF, POOL)                                                                      \
-  hipLaunchKernelGGL((conv3x3_x3_tile2_kernel<TH_, TW_, WM, WN, X3T_TM, NBUF, POOL>), dim3((unsigned)blocks),     \
+#define X3T2(TH_, TW_, WM, WN, NBUF, POOL, FL_)                                                                 \
+  hipLaunchKernelGGL((conv3x3_x3_tile2_kernel<TH_, TW_, WM, WN, X3T_TM, NBUF, POOL, FL_>), dim3((unsigned)blocks),     \
                      dim3(64 * WM * WN), 0, stream, in_split, Bt, out, out_split, N, K, epi, tilesX, tilesY, tilesN, \
                      xg, (unsigned)in_bytes, (unsigned)b_bytes)
-    if (kind == 2 && pool) {
-      X3T2(4, 26, 1, 4, 2, true);
+    const bool yolo = epi.flags == X3_YOLO_FL;  // YOLO's epilogue set compiled in for the pooled forms
+    if (kind == 2 && pool && yolo) {
+      X3T2(4, 26, 1, 4, 2, true, X3_YOLO_FL);
+    } else if (kind == 2 && pool) {
+      X3T2(4, 26, 1, 4, 2, true, -1);
     } else if (kind == 2) {
-      X3T2(4, 26, 1, 4, 2, false);
+      X3T2(4, 26, 1, 4, 2, false, -1);
+    } else if (pool && yolo) {
+      X3T2(8, 26, 2, 2, 1, true, X3_YOLO_FL);
     } else if (pool) {
-      X3T2(8, 26, 2, 2, 1, true);
+      X3T2(8, 26, 2, 2, 1, true, -1);
     } else {
-      X3T2(8, 26, 2, 2, 1, false);
+      X3T2(8, 26, 2, 2, 1, false, -1);
     }
 #undef X3T2
     return check_x3("conv_x3 (tile)");
@@ -513,11 +532,11 @@ int launch_conv_x3(const bf16_bits* in_split, const bf16_bits* Bt, float* out, b
 #define X3AF(NPR_, POOL_, FL_)                                                                                    \
   hipLaunchKernelGGL((conv3x3_x3_acc2_kernel<X3_BM, NPR_, POOL_, FL_>), grid, dim3(512), 0, stream, in_split, Bt, \
                      out, out_split, (int)M, N, K, epi, tilesM, xg, (unsigned)in_bytes, (unsigned)b_bytes)
-  if (epi.flags == (EPI_BIAS | EPI_BN | EPI_LEAKY_F64) && xg.out_mode != 2) {  // YOLO's set compiled in
+  if (epi.flags == X3_YOLO_FL && xg.out_mode != 2) {  // YOLO's set compiled in
     if (pool)
-      X3AF(X3_NPR_POOL, true, EPI_BIAS | EPI_BN | EPI_LEAKY_F64);
+      X3AF(X3_NPR_POOL, true, X3_YOLO_FL);
     else
-      X3AF(X3_NPR, false, EPI_BIAS | EPI_BN | EPI_LEAKY_F64);
+      X3AF(X3_NPR, false, X3_YOLO_FL);
   } else {
     if (pool)
       X3AF(X3_NPR_POOL, true, -1);
@@ -645,6 +664,18 @@ int launch_conv_x3_1x1(const bf16_bits* in_split, const bf16_bits* Bt, float* ou
 extern "C" __attribute__((visibility("default"))) int dnn_x3_diag_stamps(unsigned long long* host, int n) {
   if (n < 0 || n > dnnhip::X3_DIAG_WGS) return -2;
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(dnnhip::x3_diag_stamps), (size_t)n * 4 * sizeof(unsigned long long), 0,
+                             hipMemcpyDeviceToHost) == hipSuccess
+             ? 0
+             : -1;
+}
+#endif
+
+#if (X3DIAG & 32) != 0
+// diagnostic builds (X3DIAG bit 32): conv3x3_x3_c16p_kernel's per-workgroup cycle sums of its
+// last launch [split phase, MFMA phase, epilogue phase, tiles] copied to host[0 .. 4n)
+extern "C" __attribute__((visibility("default"))) int dnn_c16_diag_stamps(unsigned long long* host, int n) {
+  if (n < 0 || n > dnnhip::C16_DIAG_WGS) return -2;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(dnnhip::c16_diag_stamps), (size_t)n * 4 * sizeof(unsigned long long), 0,
                              hipMemcpyDeviceToHost) == hipSuccess
              ? 0
              : -1;

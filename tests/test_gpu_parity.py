@@ -155,7 +155,9 @@ def test_avx_abi(avx, oc):
     assert R.normwise_err(out, ref) < LAYER_TOL
     kr = np.ascontiguousarray(k.transpose(2, 0, 1, 3).reshape(-1, od))
     out2 = np.zeros_like(out)
-    avx.conv2d_cuda_pthread(_p(xp), _p(out2), _p(kr), _p(out2), B, args.ctypes.data_as(ctypes.POINTER(ctypes.c_int)))
+    # the col scratch (B * oh * ow rows of 3*3*C, the reference's im2col buffer) apart from the result
+    col = np.full((B * oh * ow, 9 * C), np.nan, np.float32)
+    avx.conv2d_cuda_pthread(_p(xp), _p(col), _p(kr), _p(out2), B, args.ctypes.data_as(ctypes.POINTER(ctypes.c_int)))
     assert R.normwise_err(out2, ref) < LAYER_TOL
 
     y = ref

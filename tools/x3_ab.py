@@ -67,6 +67,29 @@ def clock_stamps(lib, nwg):
             "span_us": round((max(r[2] for r in rows) - r0min) / 100, 2), "per_xcd": xcd}
 
 
+def c16_phases(lib, nwg=512):
+    """X3DIAG bit 32 builds: conv1's persistent x3 kernel, per-workgroup s_memtime sums of its
+    split / MFMA / epilogue phases (last launch); medians over workgroups, per tile."""
+    fn = getattr(lib, "dnn_c16_diag_stamps", None)
+    if fn is None:
+        return None
+    fn.restype = ctypes.c_int
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    buf = (ctypes.c_ulonglong * (4 * nwg))()
+    if fn(buf, nwg) != 0:
+        return None
+    rows = [buf[4 * w:4 * w + 4] for w in range(nwg) if buf[4 * w + 3] > 0]
+    if not rows:
+        return None
+    per = lambda k: statistics.median(r[k] / r[3] for r in rows)  # noqa: E731
+    tot = [r[0] + r[1] + r[2] for r in rows]
+    return {"workgroups": len(rows), "tiles_median": statistics.median(r[3] for r in rows),
+            "split_cycles_per_tile": round(per(0)), "mfma_cycles_per_tile": round(per(1)),
+            "epilogue_cycles_per_tile": round(per(2)),
+            "total_mcycles_median": round(statistics.median(tot) / 1e6, 4),
+            "total_mcycles_max": round(max(tot) / 1e6, 4)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--env", action="append", default=[], help="VAR=v1,v2,... (arms)")
@@ -137,12 +160,17 @@ def main():
             c = clock_stamps(plan.lib, 4096)
             if c:
                 d["clock"].append(c)
+            c = c16_phases(plan.lib)
+            if c:
+                d.setdefault("c16", []).append(c)
     want = [n for n in names if n.split(".")[0] in a.kernels.split(",")]
     summary = {"cold_clock": cold, "arms": {}}
     for key, d in res.items():
         s = {"fwd_ms_median": round(statistics.median(d["fwd_ms"]), 4), "fwd_ms_min": round(min(d["fwd_ms"]), 4),
              "kernels_ms_median": {n: round(statistics.median(d["k"][n]), 4) for n in want},
              "kernels_ms_min": {n: round(min(d["k"][n]), 4) for n in want}}
+        if d.get("c16"):
+            s["c16_phases_last_round"] = d["c16"][-1]
         if d["clock"]:
             s["clock_last_round"] = d["clock"][-1]
             s["clock_median_ghz_over_rounds"] = round(statistics.median(c["median_ghz"] for c in d["clock"]), 4)
