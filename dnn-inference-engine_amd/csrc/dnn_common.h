@@ -229,6 +229,8 @@ bool conv_patch16_supported(int C, int OC, int H, int W, int OH, int OW, int kh,
 // fp32 path "x3" conv (kernels_x3.hip, gemm_x3_patch.h): fp32 operands split exactly into three
 // bf16 pieces, six bf16 MFMA products, fp32 accumulation; activations in split planes
 // [B][H+2][W+2][C/32][3][32] bf16 (zero-bordered), weights packed by launch_pack_weights_x3
+// which x3 kernel family runs a layer (kernels_x3.hip x3_kind): 0 wide rows, 1 / 2 2-D tiles, 3 16-channel; -1 none
+int conv_x3_kind(int OC, int C);
 bool conv_x3_supported(int C, int OC, int H, int W, int OH, int OW, int kh, int kw, int sh, int sw, int pt, int pl);
 size_t x3_act_bytes(long long nimg, int H, int W, int C);
 int launch_maxpool_x3(const float* in, unsigned short* out, const PoolGeom& g, hipStream_t s);

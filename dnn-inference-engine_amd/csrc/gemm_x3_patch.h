@@ -38,7 +38,11 @@ namespace dnnhip {
 
 #if (X3DIAG & 32) != 0  // conv3x3_x3_c16p_kernel phase cycles (gemm_x3_patch.h)
 constexpr int C16_DIAG_WGS = 1024;
-__device__ unsigned long long c16_diag_stamps[C16_DIAG_WGS * 4];  // [workgroup][split, mfma, epilogue, tiles]
+constexpr int C16_DIAG_SLOTS = 10;
+// [workgroup][slot]: wave 0's s_memtime sums over its tiles -- 0 the loop-top drain, 1 split + row
+// table + next loads, 2 barrier, 3 MFMAs, 4 barrier, 5 epilogue math + stage, 6 split-plane
+// stores, 7 barrier; 8 tiles
+__device__ unsigned long long c16_diag_stamps[C16_DIAG_WGS * C16_DIAG_SLOTS];
 #endif
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -127,6 +131,52 @@ __device__ __forceinline__ void x3_pool_split_store(const float* stg, const int*
     bf16_bits* d = out_split + (size_t)o * n3 + col0 + c8;
 #pragma unroll
     for (int pc = 0; pc < 3; ++pc) *reinterpret_cast<u32x4*>(d + 32 * pc) = q[pc];
+  }
+}
+
+// The same store with a fixed count of vector-memory instructions per wave: every lane runs
+// ceil(16 TM / 64) tasks (tasks past the wave's 16 TM and windows past the frame take a clamped
+// stage read and a buffer store at an offset past the descriptor, which the hardware drops), no
+// branch around a store.  A persistent kernel that has its next tile's loads in flight across
+// this epilogue can then wait for those loads alone: vmcnt counts loads and stores together, in
+// issue order, so a fixed number of younger stores is a fixed count to leave outstanding (a
+// variable count makes the compiler's wait drain the stores too).
+template <int TM>
+constexpr int x3_fixed_store_count() {
+  return 3 * ((16 * TM + 63) / 64);
+}
+template <int TM>
+__device__ __forceinline__ void x3_pool_split_store_fixed(const float* stg, const int* orow, int no, int wbase,
+                                                          __amdgpu_buffer_rsrc_t rs, int n3, int col0, int lane) {
+  wait_lgkm0();  // the stage is wave-private
+  asm volatile("" : "+v"(lane));  // (per-lane task addresses recomputed here, not held across a persistent loop)
+#pragma unroll
+  for (int it = 0; it < (16 * TM + 63) / 64; ++it) {
+    const int task = lane + 64 * it;
+    const bool tv = task < 16 * TM;
+    const int tc = tv ? task : 16 * TM - 1;
+    const int wl = tc >> 2, c8 = 8 * (tc & 3), w = wbase + wl;
+    const int o = orow[w < no ? w : no - 1];
+    const bool st = tv && w < no && o >= 0;
+    const f32x4 lo = *reinterpret_cast<const f32x4*>(stg + wl * X3_STG_ROW + c8);
+    const f32x4 hi = *reinterpret_cast<const f32x4*>(stg + wl * X3_STG_ROW + c8 + 4);
+    bool ok = true;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) ok = ok && x3_split_ok(lo[e]) && x3_split_ok(hi[e]);
+    const bool fast = __builtin_amdgcn_ballot_w64(!ok) == 0;
+    u32x4 q[3];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      unsigned w0, w1, w2;
+      split3_pack2(fast, e < 2 ? lo[2 * e] : hi[2 * e - 4], e < 2 ? lo[2 * e + 1] : hi[2 * e - 3], w0, w1, w2);
+      q[0][e] = w0;
+      q[1][e] = w1;
+      q[2][e] = w2;
+    }
+    const unsigned off = st ? (unsigned)(o * n3 + col0 + c8) * 2u : OOB_OFF;
+#pragma unroll
+    for (int pc = 0; pc < 3; ++pc) __builtin_amdgcn_raw_buffer_store_b128(q[pc], rs, off + 64 * pc, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);  // (one task's registers at a time)
   }
 }
 
@@ -373,7 +423,7 @@ conv3x3_x3_c16_kernel(const float* __restrict__ in, const bf16_bits* __restrict_
 // MFMAs per block and column block, if the K = 16 form issues in half the cycles.  Summation
 // order: as the 16-channel kernel (two accumulators; steps 0-4), the order depending on (N, K)
 // only.  LDS: 30 KB weights + 48 KB split patch + 1.7 KB row table = 79 KB (two per CU).
-template <bool POOL, bool HALF, int FL = -1>
+template <bool POOL, bool HALF, int FL = -1, bool SPL = false>
 __global__ void __launch_bounds__(256, 2)
 conv3x3_x3_c16p_kernel(const float* __restrict__ in, const bf16_bits* __restrict__ Bt, float* __restrict__ out,
                        bf16_bits* __restrict__ out_split, int N, EpiParams epi, int tilesX, int tilesY, int ntiles,
@@ -518,27 +568,38 @@ conv3x3_x3_c16p_kernel(const float* __restrict__ in, const bf16_bits* __restrict
 
   const int G = gridDim.x;
   int t = blockIdx.x;
-#if (X3DIAG & 32) != 0  // per-phase s_memtime sums: tile top -> split barrier -> MFMA barrier -> tile end
-  unsigned long long dg_a = 0, dg_b = 0, dg_c = 0, dg_n = 0, dg_t0 = 0, dg_t1 = 0;
-#define C16_STAMP(acc)                                       \
-  {                                                          \
+#if (X3DIAG & 32) != 0  // per-phase s_memtime sums (c16_diag_stamps)
+  unsigned long long dg[C16_DIAG_SLOTS] = {}, dg_t1 = 0;
+#define C16_STAMP(k)                                             \
+  {                                                              \
     const unsigned long long now = __builtin_amdgcn_s_memtime(); \
-    acc += now - dg_t1;                                      \
-    dg_t1 = now;                                             \
+    dg[k] += now - dg_t1;                                        \
+    dg_t1 = now;                                                 \
   }
 #else
-#define C16_STAMP(acc)
+#define C16_STAMP(k)
 #endif
+  // SPL (pooled split-plane output): the epilogue's stores are x3_pool_split_store_fixed's fixed
+  // count per wave, and the first tile's loads are followed by as many dropped stores (offset past
+  // the descriptor), so on both paths into the loop top the staged loads are the only older
+  // operations the compiler's vmcnt waits cover: the previous tile's stores stay in flight (a
+  // drain there cost conv1 ~5k cycles per tile, X3DIAG 32)
+  const auto rsO = __builtin_amdgcn_make_buffer_rsrc((void*)out_split, 0, 0x7fffffff, 0x00020000);
   if (t < ntiles) load_tile(t);
+  if constexpr (SPL) {
+#pragma unroll
+    for (int k = 0; k < x3_fixed_store_count<TM>(); ++k)
+      __builtin_amdgcn_raw_buffer_store_b128(u32x4{0u, 0u, 0u, 0u}, rsO, OOB_OFF + 16 * k, 0, 0);  // (distinct: not merged)
+  }
   while (t < ntiles) {
 #if (X3DIAG & 32) != 0
-    dg_t0 = dg_t1 = __builtin_amdgcn_s_memtime();
-    (void)dg_t0;
-    ++dg_n;
+    dg_t1 = __builtin_amdgcn_s_memtime();
+    ++dg[8];
 #endif
     int b, y0, x0;
     tile_xy(t, b, y0, x0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if constexpr (!SPL) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (variable store counts: drain)
+    C16_STAMP(0)
     split_tile();
     for (int r = threadIdx.x; r < NO; r += NT) {
       int o;
@@ -555,8 +616,9 @@ conv3x3_x3_c16p_kernel(const float* __restrict__ in, const bf16_bits* __restrict
     }
     const int tn = t + G;
     if (tn < ntiles) load_tile(tn);  // in flight during this tile's MFMAs
+    C16_STAMP(1)
     __syncthreads();                 // the patch, the row table (and, first time, the weights) written
-    C16_STAMP(dg_a)
+    C16_STAMP(2)
 
     f32x4 acc[TM][2], accc[TM][2];
 #pragma unroll
@@ -613,11 +675,12 @@ conv3x3_x3_c16p_kernel(const float* __restrict__ in, const bf16_bits* __restrict
       }
     }
     x3_fold(acc, accc);
+    C16_STAMP(3)
     __syncthreads();  // every wave is done with the patch: the epilogue stages reuse it
-    C16_STAMP(dg_b)
+    C16_STAMP(4)
 
     if constexpr (POOL) {
-      if (g.out_mode == 1) {  // staged 16-B split-plane stores (x3_pool_split_store)
+      if (SPL || g.out_mode == 1) {  // staged 16-B split-plane stores (x3_pool_split_store)
         float* stgp = reinterpret_cast<float*>(patch) + wm * (TM * 4 * X3_STG_ROW);
 #pragma unroll
         for (int jb = 0; jb < 2; ++jb) {
@@ -632,9 +695,14 @@ conv3x3_x3_c16p_kernel(const float* __restrict__ in, const bf16_bits* __restrict
                 (X3DIAG & 64) != 0 ? acc[i][jb][0] + pb  // (diagnostic: no pool / epilogue math)
                                    : pool_then_epilogue_t<FL>(acc[i][jb], pb, pm, ps, pg, epi.flags);
         }
-        x3_pool_split_store<TM>(stgp, orow, NO, 4 * wm * TM, out_split, 96, 0, lane);
+        C16_STAMP(5)
+        if constexpr (SPL)
+          x3_pool_split_store_fixed<TM>(stgp, orow, NO, 4 * wm * TM, rsO, 96, 0, lane);
+        else
+          x3_pool_split_store<TM>(stgp, orow, NO, 4 * wm * TM, out_split, 96, 0, lane);
+        C16_STAMP(6)
         __syncthreads();  // stages read before the next tile's split overwrites the patch area
-        C16_STAMP(dg_c)
+        C16_STAMP(7)
         t = tn;
         continue;
       }
@@ -680,11 +748,9 @@ conv3x3_x3_c16p_kernel(const float* __restrict__ in, const bf16_bits* __restrict
   }
 #if (X3DIAG & 32) != 0
   if (threadIdx.x == 0 && blockIdx.x < C16_DIAG_WGS) {  // (vector stores from lane 0)
-    unsigned long long* d = c16_diag_stamps + 4 * blockIdx.x;
-    d[0] = dg_a;
-    d[1] = dg_b;
-    d[2] = dg_c;
-    d[3] = dg_n;
+    unsigned long long* d = c16_diag_stamps + C16_DIAG_SLOTS * blockIdx.x;
+#pragma unroll
+    for (int k = 0; k < C16_DIAG_SLOTS; ++k) d[k] = dg[k];
   }
 #endif
 #undef C16_STAMP

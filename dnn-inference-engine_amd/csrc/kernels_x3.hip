@@ -376,6 +376,8 @@ static int x3_kind(int N, int C) {
   return -1;
 }
 
+int conv_x3_kind(int OC, int C) { return x3_kind(OC, C); }
+
 bool conv_x3_supported(int C, int OC, int H, int W, int OH, int OW, int kh, int kw, int sh, int sw, int pt, int pl) {
   if (!(kh == 3 && kw == 3 && sh == 1 && sw == 1 && pt == 1 && pl == 1 && OH == H && OW == W &&
         (C % 32 == 0 || C == 16) && x3_enabled()))
@@ -439,10 +441,11 @@ int launch_conv_x3(const bf16_bits* in_split, const bf16_bits* Bt, float* out, b
     const float* in32p = reinterpret_cast<const float*>(in_split);
     (void)b16;
     // (two accumulators per output, gemm_x3_patch.h x3_step).  DNN_HIP_X3_C16P (read per launch,
-    // experiments): 0 = one tile per workgroup (conv3x3_x3_c16_kernel), 1 = persistent
-    // (conv3x3_x3_c16p_kernel: same bits), 2 = persistent with the last K step on 16x16x16
+    // experiments): 0 = one tile per workgroup (conv3x3_x3_c16_kernel); default (1): persistent
+    // (conv3x3_x3_c16p_kernel, the last K step on 16x16x16; measured at batch 64: conv1 0.164 ->
+    // 0.152 ms, forward -14 us), same bits up to the K = 16 step's summation
     const char* pe = getenv("DNN_HIP_X3_C16P");
-    const int pv = pe ? atoi(pe) : 2;  // (measured at batch 64: 0 -> 2 conv1 0.164 -> 0.152 ms, forward -14 us)
+    const int pv = pe ? atoi(pe) : 1;
     if (pv == 0 || !pool) {  // (the persistent kernel is instantiated for the pooled form: conv1)
       if (pool)
         hipLaunchKernelGGL((conv3x3_x3_c16_kernel<16, 26, 4, 7, true>), dim3((unsigned)blocks), dim3(256), 0, stream,
@@ -453,25 +456,17 @@ int launch_conv_x3(const bf16_bits* in_split, const bf16_bits* Bt, float* out, b
     } else {
       const long long slots = 2LL * device_cu_count();
       const dim3 pgrid((unsigned)(blocks < slots ? blocks : slots));
-#define C16P(POOL_, HALF_)                                                                                     \
-  hipLaunchKernelGGL((conv3x3_x3_c16p_kernel<POOL_, HALF_, C16P_FL>), pgrid, dim3(256), 0, stream, in32p, Bt, out, out_split, \
-                     N, epi, tilesX, tilesY, (int)blocks, xg, (unsigned)in32)
-      // YOLO's epilogue set compiled in (bias + BatchNorm + double-rounded leaky; same arithmetic)
-      if (epi.flags == X3_YOLO_FL) {
-#define C16P_FL X3_YOLO_FL
-        if (pv == 2)
-          C16P(true, true);
-        else
-          C16P(true, false);
-#undef C16P_FL
-      } else {
-#define C16P_FL -1
-        if (pv == 2)
-          C16P(true, true);
-        else
-          C16P(true, false);
-#undef C16P_FL
-      }
+      // split-plane output: the fixed-count store form (SPL); YOLO's epilogue set compiled in
+#define C16P(FL_, SPL_)                                                                                         \
+  hipLaunchKernelGGL((conv3x3_x3_c16p_kernel<true, true, FL_, SPL_>), pgrid, dim3(256), 0, stream, in32p, Bt, out, \
+                     out_split, N, epi, tilesX, tilesY, (int)blocks, xg, (unsigned)in32)
+      const bool yolo = epi.flags == X3_YOLO_FL;
+      if (out_split && yolo && pv == 2)  // (2: fixed-count stores left in flight; measured slower, A/B)
+        C16P(X3_YOLO_FL, true);
+      else if (out_split && yolo)
+        C16P(X3_YOLO_FL, false);
+      else
+        C16P(-1, false);
 #undef C16P
     }
     return check_x3("conv_x3 (c16)");
@@ -487,8 +482,15 @@ int launch_conv_x3(const bf16_bits* in_split, const bf16_bits* Bt, float* out, b
     // conv3 is 1,664 tiles, 6.5 per CU, where 4 x 52 tiles of 8 waves were 3.25 rounds of one per
     // CU (measured 0.157 -> 0.131 ms).  kind 1: 8 x 26 tiles (1.35x patch rows per output row;
     // 4 x 52: 1.56x, conv2 0.142 -> 0.140 ms)
-    const int TH = kind == 1 ? 8 : 4, TW = 26;
-    const int tilesX = (W + TW - 1) / TW, tilesY = (H + TH - 1) / TH, tilesN = N / (kind == 1 ? 64 : 128);
+    // small batches (the single-frame latency plans: conv2 52 tiles, conv3 26 at one frame, a
+    // quarter of the chip or less): 2 x 26 tiles, 2 x 2 waves of 2 row blocks x 32 columns (each
+    // wave's MFMA chain 2 / 7 of the batch form's), 64 columns per workgroup.  The summation order
+    // depends on (N, K) only: the same bits as the batch tiles
+    const long long big = nimg * ((H + (kind == 1 ? 7 : 3)) / (kind == 1 ? 8 : 4)) * ((W + 25) / 26) *
+                          (N / (kind == 1 ? 64 : 128));
+    const bool small = big < 2LL * device_cu_count();
+    const int TH = small ? 2 : kind == 1 ? 8 : 4, TW = 26;
+    const int tilesX = (W + TW - 1) / TW, tilesY = (H + TH - 1) / TH, tilesN = N / (small || kind == 1 ? 64 : 128);
     const long long blocks = nimg * tilesX * tilesY * tilesN;
     if (blocks > 0x7fffffffLL) {
       set_error("conv_x3 (tile): grid too large");
@@ -496,12 +498,26 @@ int launch_conv_x3(const bf16_bits* in_split, const bf16_bits* Bt, float* out, b
     }
     const X3Geom xg{H, W, C, out_split ? 1 : 0, 1, PH, PW};
     // conv3x3_x3_tile2_kernel: 224-B LDS rows by LDS-DMA, immediate tap offsets, two accumulators
-#define X3T2(TH_, TW_, WM, WN, NBUF, POOL, FL_)                                                                 \
-  hipLaunchKernelGGL((conv3x3_x3_tile2_kernel<TH_, TW_, WM, WN, X3T_TM, NBUF, POOL, FL_>), dim3((unsigned)blocks),     \
+#define X3T2M(TH_, TW_, WM, WN, TM_, NBUF, POOL, FL_)                                                         \
+  hipLaunchKernelGGL((conv3x3_x3_tile2_kernel<TH_, TW_, WM, WN, TM_, NBUF, POOL, FL_>), dim3((unsigned)blocks),  \
                      dim3(64 * WM * WN), 0, stream, in_split, Bt, out, out_split, N, K, epi, tilesX, tilesY, tilesN, \
                      xg, (unsigned)in_bytes, (unsigned)b_bytes)
+#define X3T2(TH_, TW_, WM, WN, NBUF, POOL, FL_) X3T2M(TH_, TW_, WM, WN, X3T_TM, NBUF, POOL, FL_)
     const bool yolo = epi.flags == X3_YOLO_FL;  // YOLO's epilogue set compiled in for the pooled forms
-    if (kind == 2 && pool && yolo) {
+    if (small) {
+      if (pool && yolo && kind == 2)
+        X3T2M(2, 26, 2, 2, 2, 2, true, X3_YOLO_FL);
+      else if (pool && yolo)
+        X3T2M(2, 26, 2, 2, 2, 1, true, X3_YOLO_FL);
+      else if (pool && kind == 2)
+        X3T2M(2, 26, 2, 2, 2, 2, true, -1);
+      else if (pool)
+        X3T2M(2, 26, 2, 2, 2, 1, true, -1);
+      else if (kind == 2)
+        X3T2M(2, 26, 2, 2, 2, 2, false, -1);
+      else
+        X3T2M(2, 26, 2, 2, 2, 1, false, -1);
+    } else if (kind == 2 && pool && yolo) {
       X3T2(4, 26, 1, 4, 2, true, X3_YOLO_FL);
     } else if (kind == 2 && pool) {
       X3T2(4, 26, 1, 4, 2, true, -1);
@@ -515,6 +531,7 @@ int launch_conv_x3(const bf16_bits* in_split, const bf16_bits* Bt, float* out, b
       X3T2(8, 26, 2, 2, 1, false, -1);
     }
 #undef X3T2
+#undef X3T2M
     return check_x3("conv_x3 (tile)");
   }
   if (M % per_img != 0 || K != 9 * C || C % 32 != 0 || N % 256 != 0 || Npad != N || (pool && splits != 1) ||
@@ -672,10 +689,10 @@ extern "C" __attribute__((visibility("default"))) int dnn_x3_diag_stamps(unsigne
 
 #if (X3DIAG & 32) != 0
 // diagnostic builds (X3DIAG bit 32): conv3x3_x3_c16p_kernel's per-workgroup cycle sums of its
-// last launch [split phase, MFMA phase, epilogue phase, tiles] copied to host[0 .. 4n)
+// last launch (C16_DIAG_SLOTS per workgroup, gemm_x3_patch.h) copied to host[0 .. slots n)
 extern "C" __attribute__((visibility("default"))) int dnn_c16_diag_stamps(unsigned long long* host, int n) {
   if (n < 0 || n > dnnhip::C16_DIAG_WGS) return -2;
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(dnnhip::c16_diag_stamps), (size_t)n * 4 * sizeof(unsigned long long), 0,
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(dnnhip::c16_diag_stamps), (size_t)n * dnnhip::C16_DIAG_SLOTS * sizeof(unsigned long long), 0,
                              hipMemcpyDeviceToHost) == hipSuccess
              ? 0
              : -1;

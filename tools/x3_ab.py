@@ -67,27 +67,30 @@ def clock_stamps(lib, nwg):
             "span_us": round((max(r[2] for r in rows) - r0min) / 100, 2), "per_xcd": xcd}
 
 
+C16_SLOTS = ["drain", "split", "bar1", "mfma", "bar2", "epi_math", "stores", "bar3"]
+
+
 def c16_phases(lib, nwg=512):
-    """X3DIAG bit 32 builds: conv1's persistent x3 kernel, per-workgroup s_memtime sums of its
-    split / MFMA / epilogue phases (last launch); medians over workgroups, per tile."""
+    """X3DIAG bit 32 builds: conv1's persistent x3 kernel, wave 0's s_memtime sums per phase
+    (c16_diag_stamps, last launch); medians over workgroups of cycles per tile."""
     fn = getattr(lib, "dnn_c16_diag_stamps", None)
     if fn is None:
         return None
     fn.restype = ctypes.c_int
     fn.argtypes = [ctypes.c_void_p, ctypes.c_int]
-    buf = (ctypes.c_ulonglong * (4 * nwg))()
+    ns = 10
+    buf = (ctypes.c_ulonglong * (ns * nwg))()
     if fn(buf, nwg) != 0:
         return None
-    rows = [buf[4 * w:4 * w + 4] for w in range(nwg) if buf[4 * w + 3] > 0]
+    rows = [buf[ns * w:ns * w + ns] for w in range(nwg) if buf[ns * w + 8] > 0]
     if not rows:
         return None
-    per = lambda k: statistics.median(r[k] / r[3] for r in rows)  # noqa: E731
-    tot = [r[0] + r[1] + r[2] for r in rows]
-    return {"workgroups": len(rows), "tiles_median": statistics.median(r[3] for r in rows),
-            "split_cycles_per_tile": round(per(0)), "mfma_cycles_per_tile": round(per(1)),
-            "epilogue_cycles_per_tile": round(per(2)),
-            "total_mcycles_median": round(statistics.median(tot) / 1e6, 4),
-            "total_mcycles_max": round(max(tot) / 1e6, 4)}
+    out = {"workgroups": len(rows), "tiles_median": statistics.median(r[8] for r in rows)}
+    for k, name in enumerate(C16_SLOTS):
+        out[name] = round(statistics.median(r[k] / r[8] for r in rows))
+    tot = [sum(r[:8]) for r in rows]
+    out["total_mcycles_median"] = round(statistics.median(tot) / 1e6, 4)
+    return out
 
 
 def main():
