@@ -134,52 +134,6 @@ __device__ __forceinline__ void x3_pool_split_store(const float* stg, const int*
   }
 }
 
-// The same store with a fixed count of vector-memory instructions per wave: every lane runs
-// ceil(16 TM / 64) tasks (tasks past the wave's 16 TM and windows past the frame take a clamped
-// stage read and a buffer store at an offset past the descriptor, which the hardware drops), no
-// branch around a store.  A persistent kernel that has its next tile's loads in flight across
-// this epilogue can then wait for those loads alone: vmcnt counts loads and stores together, in
-// issue order, so a fixed number of younger stores is a fixed count to leave outstanding (a
-// variable count makes the compiler's wait drain the stores too).
-template <int TM>
-constexpr int x3_fixed_store_count() {
-  return 3 * ((16 * TM + 63) / 64);
-}
-template <int TM>
-__device__ __forceinline__ void x3_pool_split_store_fixed(const float* stg, const int* orow, int no, int wbase,
-                                                          __amdgpu_buffer_rsrc_t rs, int n3, int col0, int lane) {
-  wait_lgkm0();  // the stage is wave-private
-  asm volatile("" : "+v"(lane));  // (per-lane task addresses recomputed here, not held across a persistent loop)
-#pragma unroll
-  for (int it = 0; it < (16 * TM + 63) / 64; ++it) {
-    const int task = lane + 64 * it;
-    const bool tv = task < 16 * TM;
-    const int tc = tv ? task : 16 * TM - 1;
-    const int wl = tc >> 2, c8 = 8 * (tc & 3), w = wbase + wl;
-    const int o = orow[w < no ? w : no - 1];
-    const bool st = tv && w < no && o >= 0;
-    const f32x4 lo = *reinterpret_cast<const f32x4*>(stg + wl * X3_STG_ROW + c8);
-    const f32x4 hi = *reinterpret_cast<const f32x4*>(stg + wl * X3_STG_ROW + c8 + 4);
-    bool ok = true;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) ok = ok && x3_split_ok(lo[e]) && x3_split_ok(hi[e]);
-    const bool fast = __builtin_amdgcn_ballot_w64(!ok) == 0;
-    u32x4 q[3];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      unsigned w0, w1, w2;
-      split3_pack2(fast, e < 2 ? lo[2 * e] : hi[2 * e - 4], e < 2 ? lo[2 * e + 1] : hi[2 * e - 3], w0, w1, w2);
-      q[0][e] = w0;
-      q[1][e] = w1;
-      q[2][e] = w2;
-    }
-    const unsigned off = st ? (unsigned)(o * n3 + col0 + c8) * 2u : OOB_OFF;
-#pragma unroll
-    for (int pc = 0; pc < 3; ++pc) __builtin_amdgcn_raw_buffer_store_b128(q[pc], rs, off + 64 * pc, 0, 0);
-    __builtin_amdgcn_sched_barrier(0);  // (one task's registers at a time)
-  }
-}
-
 // POOL (all x3 conv kernels): a fused 2x2/s2 max pool -- GEMM rows pool-window-major (row 4 w +
 // 2 dy + dx = cell (dy, dx) of pooled pixel w; cells past an odd edge repeat cell (0, 0)), so a
 // lane's 4 accumulator registers (rows 4 q .. 4 q + 3 of its 16 x 16 block) are one window:
@@ -423,7 +377,7 @@ conv3x3_x3_c16_kernel(const float* __restrict__ in, const bf16_bits* __restrict_
 // MFMAs per block and column block, if the K = 16 form issues in half the cycles.  Summation
 // order: as the 16-channel kernel (two accumulators; steps 0-4), the order depending on (N, K)
 // only.  LDS: 30 KB weights + 48 KB split patch + 1.7 KB row table = 79 KB (two per CU).
-template <bool POOL, bool HALF, int FL = -1, bool SPL = false>
+template <bool POOL, bool HALF, int FL = -1>
 __global__ void __launch_bounds__(256, 2)
 conv3x3_x3_c16p_kernel(const float* __restrict__ in, const bf16_bits* __restrict__ Bt, float* __restrict__ out,
                        bf16_bits* __restrict__ out_split, int N, EpiParams epi, int tilesX, int tilesY, int ntiles,
@@ -579,18 +533,7 @@ conv3x3_x3_c16p_kernel(const float* __restrict__ in, const bf16_bits* __restrict
 #else
 #define C16_STAMP(k)
 #endif
-  // SPL (pooled split-plane output): the epilogue's stores are x3_pool_split_store_fixed's fixed
-  // count per wave, and the first tile's loads are followed by as many dropped stores (offset past
-  // the descriptor), so on both paths into the loop top the staged loads are the only older
-  // operations the compiler's vmcnt waits cover: the previous tile's stores stay in flight (a
-  // drain there cost conv1 ~5k cycles per tile, X3DIAG 32)
-  const auto rsO = __builtin_amdgcn_make_buffer_rsrc((void*)out_split, 0, 0x7fffffff, 0x00020000);
   if (t < ntiles) load_tile(t);
-  if constexpr (SPL) {
-#pragma unroll
-    for (int k = 0; k < x3_fixed_store_count<TM>(); ++k)
-      __builtin_amdgcn_raw_buffer_store_b128(u32x4{0u, 0u, 0u, 0u}, rsO, OOB_OFF + 16 * k, 0, 0);  // (distinct: not merged)
-  }
   while (t < ntiles) {
 #if (X3DIAG & 32) != 0
     dg_t1 = __builtin_amdgcn_s_memtime();
@@ -598,7 +541,12 @@ conv3x3_x3_c16p_kernel(const float* __restrict__ in, const bf16_bits* __restrict
 #endif
     int b, y0, x0;
     tile_xy(t, b, y0, x0);
-    if constexpr (!SPL) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (variable store counts: drain)
+    // all of this wave's memory operations retired: the staged loads, and the previous tile's
+    // stores (X3DIAG 32: ~80 cycles, they are done by now).  (Round 4, measured: leaving those
+    // stores in flight -- a fixed store count per wave, so that the wait could leave them
+    // outstanding -- made the next tile's patch loads, issued behind them, ~10k cycles slower
+    // per tile: conv1 0.152 -> 0.19 ms.)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     C16_STAMP(0)
     split_tile();
     for (int r = threadIdx.x; r < NO; r += NT) {
@@ -680,7 +628,7 @@ conv3x3_x3_c16p_kernel(const float* __restrict__ in, const bf16_bits* __restrict
     C16_STAMP(4)
 
     if constexpr (POOL) {
-      if (SPL || g.out_mode == 1) {  // staged 16-B split-plane stores (x3_pool_split_store)
+      if (g.out_mode == 1) {  // staged 16-B split-plane stores (x3_pool_split_store)
         float* stgp = reinterpret_cast<float*>(patch) + wm * (TM * 4 * X3_STG_ROW);
 #pragma unroll
         for (int jb = 0; jb < 2; ++jb) {
@@ -696,10 +644,7 @@ conv3x3_x3_c16p_kernel(const float* __restrict__ in, const bf16_bits* __restrict
                                    : pool_then_epilogue_t<FL>(acc[i][jb], pb, pm, ps, pg, epi.flags);
         }
         C16_STAMP(5)
-        if constexpr (SPL)
-          x3_pool_split_store_fixed<TM>(stgp, orow, NO, 4 * wm * TM, rsO, 96, 0, lane);
-        else
-          x3_pool_split_store<TM>(stgp, orow, NO, 4 * wm * TM, out_split, 96, 0, lane);
+        x3_pool_split_store<TM>(stgp, orow, NO, 4 * wm * TM, out_split, 96, 0, lane);
         C16_STAMP(6)
         __syncthreads();  // stages read before the next tile's split overwrites the patch area
         C16_STAMP(7)

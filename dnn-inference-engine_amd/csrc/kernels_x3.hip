@@ -440,13 +440,11 @@ int launch_conv_x3(const bf16_bits* in_split, const bf16_bits* Bt, float* out, b
     const X3Geom xg{H, W, C, out_split ? 1 : 0, 1, PH, PW};
     const float* in32p = reinterpret_cast<const float*>(in_split);
     (void)b16;
-    // (two accumulators per output, gemm_x3_patch.h x3_step).  DNN_HIP_X3_C16P (read per launch,
-    // experiments): 0 = one tile per workgroup (conv3x3_x3_c16_kernel); default (1): persistent
+    // (two accumulators per output, gemm_x3_patch.h x3_step).  DNN_HIP_X3_C16P=0 (read per
+    // launch, experiments): one tile per workgroup (conv3x3_x3_c16_kernel); default: persistent
     // (conv3x3_x3_c16p_kernel, the last K step on 16x16x16; measured at batch 64: conv1 0.164 ->
     // 0.152 ms, forward -14 us), same bits up to the K = 16 step's summation
-    const char* pe = getenv("DNN_HIP_X3_C16P");
-    const int pv = pe ? atoi(pe) : 1;
-    if (pv == 0 || !pool) {  // (the persistent kernel is instantiated for the pooled form: conv1)
+    if (getenv_flag_off("DNN_HIP_X3_C16P") || !pool) {  // (the persistent kernel: the pooled form, conv1)
       if (pool)
         hipLaunchKernelGGL((conv3x3_x3_c16_kernel<16, 26, 4, 7, true>), dim3((unsigned)blocks), dim3(256), 0, stream,
                            in32p, Bt, out, out_split, N, epi, tilesX, tilesY, xg, (unsigned)in32);
@@ -456,17 +454,13 @@ int launch_conv_x3(const bf16_bits* in_split, const bf16_bits* Bt, float* out, b
     } else {
       const long long slots = 2LL * device_cu_count();
       const dim3 pgrid((unsigned)(blocks < slots ? blocks : slots));
-      // split-plane output: the fixed-count store form (SPL); YOLO's epilogue set compiled in
-#define C16P(FL_, SPL_)                                                                                         \
-  hipLaunchKernelGGL((conv3x3_x3_c16p_kernel<true, true, FL_, SPL_>), pgrid, dim3(256), 0, stream, in32p, Bt, out, \
+#define C16P(FL_)                                                                                              \
+  hipLaunchKernelGGL((conv3x3_x3_c16p_kernel<true, true, FL_>), pgrid, dim3(256), 0, stream, in32p, Bt, out,  \
                      out_split, N, epi, tilesX, tilesY, (int)blocks, xg, (unsigned)in32)
-      const bool yolo = epi.flags == X3_YOLO_FL;
-      if (out_split && yolo && pv == 2)  // (2: fixed-count stores left in flight; measured slower, A/B)
-        C16P(X3_YOLO_FL, true);
-      else if (out_split && yolo)
-        C16P(X3_YOLO_FL, false);
+      if (epi.flags == X3_YOLO_FL)  // YOLO's epilogue set compiled in
+        C16P(X3_YOLO_FL);
       else
-        C16P(-1, false);
+        C16P(-1);
 #undef C16P
     }
     return check_x3("conv_x3 (c16)");

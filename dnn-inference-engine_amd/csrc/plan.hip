@@ -431,9 +431,12 @@ int dnn_plan_add_conv(dnn_plan* p, int kh, int kw, int od, int stride_h, int str
   bool x3_cand = false, x3_lat = false;
   if (!p->fp16 && L.mode == MODE_IMPLICIT && !p->layers.empty()) {
     const bool batch_ok = conv_x3_supported(L.C, od, L.H, L.W, L.OH, L.OW, kh, kw, stride_h, stride_w, L.pt, L.pl);
-    // (the narrow layers' tile kernels take small tiles at small batches: batch_ok is enough)
+    // (the N = 64 / 128 tile kernels take small tiles at small batches: batch_ok is enough; the
+    // 16-channel kernel's 16 x 26 tiles are 104 at one frame: 11.7 us against the fp32 patch
+    // conv's 10.0, which writes conv2's split planes as well)
+    const int xk = conv_x3_kind(od, L.C);
     if (p->latency && fused_splitk(p) &&
-        !(batch_ok && (conv_x3_kind(od, L.C) > 0 || x3_tiles(p->batch, L.OH, L.OW, od, L.C, L.K) >= 128))) {
+        !(batch_ok && (xk == 1 || xk == 2 || x3_tiles(p->batch, L.OH, L.OW, od, L.C, L.K) >= 128))) {
       x3_lat = conv_x3_lat_supported(p->batch, L.C, od, L.H, L.W, L.OH, L.OW, kh, kw, stride_h, stride_w, L.pt,
                                      L.pl) &&
                x3_lat_splits(od, L.K) >= 2;
