@@ -244,6 +244,13 @@ bool conv_x3_pool_supported(int OC, int C, int H, int W);  // an x3 conv of this
 long long x3_tiles(long long batch, int OH, int OW, int OC, int C, int K);
 // small-M x3 conv of the latency plans (gemm_x3_lat.h): raw partials [splits][M][N] of
 // x3_lat_splits(N, K) K slices into `part`, summed with the epilogue by launch_x3_combine
+// latency plans' mid layers: x3 with the K split inside the workgroup (gemm_x3_ktile.h), one
+// launch, no partials; deterministic, tolerance against the batch plans
+bool conv_x3_ktile_supported(long long batch, int C, int OC, int H, int W, int OH, int OW, int kh, int kw, int sh,
+                             int sw, int pt, int pl, bool pool);
+int launch_conv_x3_ktile(const unsigned short* in_split, const unsigned short* Bt, float* out,
+                         unsigned short* out_split, long long M, int N, int Npad, int K, int H, int W, int C,
+                         const EpiParams& epi, hipStream_t stream, int pool);
 bool conv_x3_lat_supported(long long batch, int C, int OC, int H, int W, int OH, int OW, int kh, int kw, int sh,
                            int sw, int pt, int pl);
 int x3_lat_splits(int N, int K);

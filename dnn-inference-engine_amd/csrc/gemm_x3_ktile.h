@@ -1,0 +1,264 @@
+// x3 3x3 conv for the single-frame latency plans' mid layers (YOLOv2-tiny conv4: 26x26x128 ->
+// 256 + 2x2 pool, conv5: 13x13x256 -> 512), device code only.
+//
+// At one frame these layers are 13-26 output rows of 26 or 13 pixels: the batch kernel's
+// 176 x 256 tiles are 4 per layer, and the fp32 MFMA's split-K GEMM (its K slices combined by the
+// last-arriving workgroup) took 14.4 / 17.5 us, most of it serial MFMA chains (a 32 x 32 wave
+// tile over 256-288 of K on the 64-cycle 32x32x2 fp32 MFMA) and the combine's memory round trip.
+// Here a workgroup owns a TH x TW tile (one or two image rows) and 32 WN columns, and splits K INSIDE the
+// workgroup: KW groups of WM x WN waves, group k taking chunks k CPK .. k CPK + CPK - 1; every
+// chunk of the tile's patch is staged by LDS-DMA at once, so no wave waits on another until the
+// end, where groups 1 .. KW - 1 hand their folded sums to group 0 through LDS and group 0 adds
+// them in group order, then runs the epilogue (fused 2x2 pool, split-plane or fp32 stores) as
+// the tile kernel does.  Per output: each group's x3 steps (two accumulators, gemm_x3_patch.h
+// x3_step, chunk-major tap-minor), folded, then the groups summed 0, 1, ..., KW - 1: the order
+// depends on (N, K, KW) only, deterministic, not the batch kernels' (latency plans are held to
+// the fp32 tolerance, as their fp32 split-K GEMMs).
+#pragma once
+#include "gemm_x3_patch.h"
+
+namespace dnnhip {
+
+#if (X3DIAG & 256) != 0  // diagnostic builds: per workgroup s_memrealtime at start, patch landed, MFMAs done,
+                         // end; 26-wide shape at workgroups 0-511, 13-wide at 512-1023
+constexpr int KT_DIAG_WGS = 1024;
+__device__ unsigned long long ktile_diag_stamps[KT_DIAG_WGS * 4];
+#define KT_STAMP(k)                                                       \
+  if (threadIdx.x == 0 && blockIdx.x < KT_DIAG_WGS / 2)                   \
+    ktile_diag_stamps[4 * (blockIdx.x + (TW == 26 ? 0 : KT_DIAG_WGS / 2)) + (k)] = __builtin_amdgcn_s_memrealtime();
+#else
+#define KT_STAMP(k)
+#endif
+
+template <int TH, int TW, int WM, int WN, int TM, int KW, int CPK, bool POOL, int FL = -1, int NB = 3>
+__global__ void __launch_bounds__(64 * WM * WN * KW, 1)
+conv3x3_x3_ktile_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __restrict__ Bt, float* __restrict__ out,
+                        bf16_bits* __restrict__ out_split, int N, int K, EpiParams epi, int tilesX, int tilesY,
+                        int tilesN, X3Geom g, unsigned in_bytes, unsigned b_bytes) {
+  constexpr int NG = WM * WN, NW = NG * KW, NT = 64 * NW, LP = 224, PU = LP / 16, PW2 = TW + 2;
+  constexpr int PR = (TH + 2) * PW2, T = TH * TW, NCH = KW * CPK;
+  constexpr int NPC = (PR * PU + 63) / 64;           // 1-KiB DMA pieces per chunk
+  constexpr int BUFB = NPC * 1024;                   // one chunk's patch
+  constexpr int NPW = (NCH * NPC + NW - 1) / NW;     // pieces per wave, all chunks
+  constexpr int RED = (KW - 1) * NG * TM * 2 * 1024;  // groups 1 .. KW - 1: f32x4 per lane, block, column block
+  constexpr int NO = POOL ? T / 4 : T;
+  constexpr int PATCH = NCH * BUFB;
+  constexpr int SM = (PATCH > RED ? PATCH : RED);
+  static_assert((!POOL || (TH % 2 == 0 && TW % 2 == 0)) && WM * TM * 16 >= T && (WM * TM - 2) * 16 < T && NW <= 16,
+                "shape");
+  static_assert(SM + NO * 4 <= 160 * 1024 && RED % 1024 == 0 && RED + NG * TM * 4 * X3_STG_ROW * 4 <= SM, "LDS");
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[SM + NO * 4];
+  int* const orow = reinterpret_cast<int*>(smem + SM);
+
+  KT_STAMP(0)
+  const int lane = threadIdx.x & 63;
+  const int eflags = FL < 0 ? epi.flags : FL;
+  const int wid = wave_uniform(threadIdx.x >> 6);
+  const int kg = wid / NG, wg = wid - kg * NG, wn = wg % WN, wm = wg / WN;
+  // column-group-major inside each XCD's contiguous range: the workgroups of one 64-column group
+  // (the same weights) share an L2
+  const int ntile = (int)gridDim.x / tilesN;
+  int t = xcd_tile(blockIdx.x, gridDim.x);
+  const int tn = t / ntile;
+  t -= tn * ntile;
+  const int tx = t % tilesX;
+  t /= tilesX;
+  const int ty = t % tilesY;
+  const int b = t / tilesY;
+  const int y0 = ty * TH, x0 = tx * TW;
+  const int n0 = tn * (32 * WN) + wn * 32;
+  const int Wp = g.W + 2;
+  const int fr = lane & 15, fq = lane >> 4;
+
+  int rowoff[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    int r = (wm * TM + i) * 16 + fr;
+    r = r < T ? r : T - 1;
+    int ly, lx;
+    if constexpr (POOL) {
+      const int w = r >> 2, q = r & 3;
+      ly = 2 * (w / (TW / 2)) + (q >> 1);
+      lx = 2 * (w % (TW / 2)) + (q & 1);
+    } else {
+      ly = r / TW;
+      lx = r % TW;
+    }
+    rowoff[i] = (ly * PW2 + lx) * LP + 16 * fq;
+  }
+
+  // the whole patch, every chunk: piece q = wid + NW k of the NCH NPC pieces (past the last:
+  // the last again) -> chunk q / NPC, LDS units U = 64 (q % NPC) + lane of that chunk's buffer
+  const int nk = K / 32;
+  const unsigned rowB = 6u * (unsigned)g.C;
+  const auto rsA = __builtin_amdgcn_make_buffer_rsrc((void*)in, 0, (int)in_bytes, 0x00020000);
+  const unsigned pbase = (unsigned)((b * (g.H + 2) + y0) * Wp + x0);
+#pragma unroll
+  for (int k = 0; k < NPW; ++k) {
+    int q = wid + NW * k;
+    q = q < NCH * NPC ? q : NCH * NPC - 1;
+    const int c = q / NPC, pq = q - c * NPC;
+    const unsigned U = 64u * (unsigned)pq + (unsigned)lane;
+    unsigned r = U / PU;
+    const unsigned u = U - r * PU;
+    r = r < (unsigned)PR ? r : (unsigned)PR - 1;
+    const unsigned py = r / PW2, px = r - py * PW2;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (__attribute__((address_space(3))) void*)(smem + c * BUFB + 1024 * pq),
+                                             16, (int)((pbase + py * (unsigned)Wp + px) * rowB + 16u * u),
+                                             (int)(c * 192), 0, 0);
+  }
+
+  // weights: this wave's 32 columns, steps 9 (kg CPK) .. 9 (kg CPK + CPK) - 1, NB - 1 ahead in an
+  // NB-step register ring (steps past the group's last read the next group's, or zeros past K)
+  const unsigned bvo = (unsigned)((n0 / 16) * nk * 3072 + lane * 16);
+  const int bjs = nk * 3072;
+  const int s0 = 9 * kg * CPK;
+  const auto rsB = __builtin_amdgcn_make_buffer_rsrc((void*)Bt, 0, (int)b_bytes, 0x00020000);
+  bf16x8 bq[NB][3][2];
+  auto load_b = [&](int s, bf16x8 (&dst)[3][2]) {
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        dst[p][j] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rsB, bvo, (s0 + s) * 3072 + p * 1024 + j * bjs, 0));
+  };
+#pragma unroll
+  for (int k = 0; k + 1 < NB; ++k) load_b(k, bq[k]);
+  const X3EpiCol ecp[2] = {x3_epi_col(epi, eflags, n0 + fr), x3_epi_col(epi, eflags, n0 + 16 + fr)};  // (prefetched)
+
+  f32x4 acc[TM][2], accc[TM][2];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = accc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();  // every chunk of the patch landed
+  KT_STAMP(1)
+
+  auto frag = [&](const unsigned char* P, int i, int tap, bf16x8 (&a)[3]) {
+    const int toff = ((tap / 3) * PW2 + (tap % 3)) * LP;
+    const unsigned char* q = P + rowoff[i] + toff;
+#pragma unroll
+    for (int p = 0; p < 3; ++p) a[p] = *reinterpret_cast<const bf16x8*>(q + 64 * p);
+  };
+#pragma unroll
+  for (int cc = 0; cc < CPK; ++cc) {
+    const unsigned char* P = smem + (kg * CPK + cc) * BUFB;
+    bf16x8 af[2][3];
+    frag(P, 0, 0, af[0]);
+#pragma unroll
+    for (int tp = 0; tp < 9; ++tp) {
+      const int s = 9 * cc + tp;
+      __builtin_amdgcn_sched_barrier(0);
+      load_b(s + NB - 1, bq[(s + NB - 1) % NB]);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int cur = i & 1, nxt = cur ^ 1;
+        if (i + 1 < TM)
+          frag(P, i + 1, tp, af[nxt]);
+        else if (tp < 8)
+          frag(P, 0, tp + 1, af[nxt]);
+        const bf16x8(&bb)[3][2] = bq[s % NB];
+#pragma unroll
+        for (int jb = 0; jb < 2; ++jb) x3_step<true>(acc[i][jb], accc[i][jb], af[cur], bb, jb);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if constexpr (TM & 1) {
+        if (tp < 8) {
+#pragma unroll
+          for (int p = 0; p < 3; ++p) af[0][p] = af[1][p];
+        }
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  x3_fold(acc, accc);
+  KT_STAMP(2)
+
+  // groups 1 .. KW - 1 hand their sums to group 0 (the patch area is free once every wave is past
+  // its last fragment read); group 0 adds them in group order
+  wait_lgkm0();
+  __syncthreads();
+  f32x4* const red = reinterpret_cast<f32x4*>(smem);
+  if (kg > 0) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int jb = 0; jb < 2; ++jb) red[((((kg - 1) * NG + wg) * TM + i) * 2 + jb) * 64 + lane] = acc[i][jb];
+  }
+  for (int r = threadIdx.x; r < NO; r += NT) {
+    int o;
+    if constexpr (POOL) {
+      const int py = (y0 >> 1) + r / (TW / 2), px = (x0 >> 1) + r % (TW / 2);
+      o = (py >= g.PH || px >= g.PW) ? -1
+          : g.out_mode == 1         ? (b * (g.PH + 2) + py + 1) * (g.PW + 2) + px + 1
+                                    : (b * g.PH + py) * g.PW + px;
+    } else {
+      const int oy = y0 + r / TW, ox = x0 + r % TW;
+      o = (oy >= g.H || ox >= g.W) ? -1 : g.out_mode == 1 ? (b * (g.H + 2) + oy + 1) * Wp + ox + 1 : (b * g.H + oy) * g.W + ox;
+    }
+    orow[r] = o;
+  }
+  __syncthreads();
+  if (kg > 0) return;
+#pragma unroll
+  for (int k = 1; k < KW; ++k)
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int jb = 0; jb < 2; ++jb) acc[i][jb] = acc[i][jb] + red[((((k - 1) * NG + wg) * TM + i) * 2 + jb) * 64 + lane];
+
+  if constexpr (POOL) {
+    if (g.out_mode == 1) {  // staged 16-B split-plane stores (x3_pool_split_store), group 0's waves
+      float* stg = reinterpret_cast<float*>(smem + RED) + wg * (TM * 4 * X3_STG_ROW);  // (past `red`)
+#pragma unroll
+      for (int jb = 0; jb < 2; ++jb) {
+        const float pb = ecp[jb].pb, pm = ecp[jb].pm, ps = ecp[jb].ps, pg = ecp[jb].pg;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+          stg[(4 * i + fq) * X3_STG_ROW + 16 * jb + fr] = pool_then_epilogue_t<FL>(acc[i][jb], pb, pm, ps, pg, epi.flags);
+      }
+      x3_pool_split_store<TM>(stg, orow, NO, 4 * wm * TM, out_split, 3 * (size_t)N, (n0 >> 5) * 96, lane);
+      KT_STAMP(3)
+      return;
+    }
+  }
+#pragma unroll
+  for (int jb = 0; jb < 2; ++jb) {
+    const int n = n0 + 16 * jb + fr;
+    const float pb = ecp[jb].pb, pm = ecp[jb].pm, ps = ecp[jb].ps, pg = ecp[jb].pg;
+    const int cofs = (n >> 5) * 96 + (n & 31);
+    auto put = [&](int o, float v) {
+      if (g.out_mode == 1) {
+        unsigned short s0_, s1_, s2_;
+        split3(v, s0_, s1_, s2_);
+        bf16_bits* d = out_split + (size_t)o * (3 * N) + cofs;
+        d[0] = s0_;
+        d[32] = s1_;
+        d[64] = s2_;
+      } else {
+        out[(size_t)o * N + n] = v;
+      }
+    };
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int rb = 16 * (wm * TM + i);
+      if constexpr (POOL) {
+        const int w = rb / 4 + fq;
+        const int o = w < NO ? orow[w] : -1;
+        if (o >= 0) put(o, pool_then_epilogue_t<FL>(acc[i][jb], pb, pm, ps, pg, epi.flags));
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = rb + 4 * fq + r;
+          const int o = row < NO ? orow[row] : -1;
+          if (o >= 0) put(o, apply_epilogue_t<FL>(acc[i][jb][r], pb, pm, ps, pg, epi.flags));
+        }
+      }
+    }
+  }
+  KT_STAMP(3)
+}
+#undef KT_STAMP
+
+}  // namespace dnnhip

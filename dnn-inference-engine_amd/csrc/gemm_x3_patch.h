@@ -96,6 +96,21 @@ __device__ __forceinline__ void x3_fold(f32x4 (&acc)[TM][NB], const f32x4 (&accc
       for (int r = 0; r < 4; ++r) acc[i][j][r] = acc[i][j][r] + accc[i][j][r];
 }
 
+// One output column's epilogue parameters (bias, mean, sqrt(var + eps), gamma; absent terms the
+// identity).  The single-frame kernels load them with their first operands, not at the epilogue:
+// at one frame a load issued there is a whole memory round trip (~1.5 us) on the critical path.
+struct X3EpiCol {
+  float pb, pm, ps, pg;
+};
+__device__ __forceinline__ X3EpiCol x3_epi_col(const EpiParams& epi, int eflags, int n) {
+  X3EpiCol c;
+  c.pb = (eflags & EPI_BIAS) ? epi.bias[n] : 0.f;
+  c.pm = (eflags & (EPI_BN | EPI_BN_AB)) ? epi.mean[n] : 0.f;
+  c.ps = (eflags & (EPI_BN | EPI_BN_AB)) ? epi.sq[n] : 1.f;
+  c.pg = (eflags & EPI_BN) ? epi.gamma[n] : 1.f;
+  return c;
+}
+
 // Pooled split-plane store through LDS (the narrow x3 kernels' epilogue): a wave's pooled values
 // of TM row blocks (4 windows x 32 columns each) are written to a wave-private stage in the MFMA
 // layout (lane (fr, fq) of block i: window 4 i + fq, column 16 jb + fr; 48-float rows, so the
@@ -808,6 +823,13 @@ conv3x3_x3_tile2_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __res
   issue_chunk(0, 0);
   load_b(0, bq[0]);
   load_b(1, bq[1]);
+  // small tiles (the single-frame plans): the epilogue parameters with the first operands
+  constexpr bool PREP = TM <= 2;
+  X3EpiCol ecp[2] = {};
+  if constexpr (PREP) {
+    ecp[0] = x3_epi_col(epi, eflags, n0 + fr);
+    ecp[1] = x3_epi_col(epi, eflags, n0 + 16 + fr);
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
@@ -885,10 +907,8 @@ conv3x3_x3_tile2_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __res
 #pragma unroll
       for (int jb = 0; jb < 2; ++jb) {
         const int n = n0 + 16 * jb + fr;
-        const float pb = (eflags & EPI_BIAS) ? epi.bias[n] : 0.f;
-        const float pm = (eflags & (EPI_BN | EPI_BN_AB)) ? epi.mean[n] : 0.f;
-        const float ps = (eflags & (EPI_BN | EPI_BN_AB)) ? epi.sq[n] : 1.f;
-        const float pg = (eflags & EPI_BN) ? epi.gamma[n] : 1.f;
+        const X3EpiCol ec = PREP ? ecp[jb] : x3_epi_col(epi, eflags, n);
+        const float pb = ec.pb, pm = ec.pm, ps = ec.ps, pg = ec.pg;
 #pragma unroll
         for (int i = 0; i < TM; ++i)
           stg[(4 * i + fq) * X3_STG_ROW + 16 * jb + fr] = pool_then_epilogue_t<FL>(acc[i][jb], pb, pm, ps, pg, epi.flags);
@@ -900,10 +920,8 @@ conv3x3_x3_tile2_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __res
 #pragma unroll
   for (int jb = 0; jb < 2; ++jb) {
     const int n = n0 + 16 * jb + fr;  // < N: N % (32 WN) == 0 (launcher)
-    const float pb = (eflags & EPI_BIAS) ? epi.bias[n] : 0.f;
-    const float pm = (eflags & (EPI_BN | EPI_BN_AB)) ? epi.mean[n] : 0.f;
-    const float ps = (eflags & (EPI_BN | EPI_BN_AB)) ? epi.sq[n] : 1.f;
-    const float pg = (eflags & EPI_BN) ? epi.gamma[n] : 1.f;
+    const X3EpiCol ec = PREP ? ecp[jb] : x3_epi_col(epi, eflags, n);
+    const float pb = ec.pb, pm = ec.pm, ps = ec.ps, pg = ec.pg;
     const int cofs = (n >> 5) * 96 + (n & 31);
     auto put = [&](int o, float v) {
       if (g.out_mode == 1) {

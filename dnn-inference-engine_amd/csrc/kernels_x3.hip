@@ -6,6 +6,7 @@
 #include "gemm_x3_acc2.h"
 #include "gemm_x3_lat.h"
 #include "gemm_x3_1x1.h"
+#include "gemm_x3_ktile.h"
 
 #include <cfloat>
 #include <cstdlib>
@@ -591,6 +592,72 @@ bool conv_x3_lat_supported(long long batch, int C, int OC, int H, int W, int OH,
   return M <= 0x7fffffffLL && x3_span(M, H, W) <= X3_NPR;
 }
 
+// ---- K split inside the workgroup (latency plans' conv4 / conv5, gemm_x3_ktile.h): 32-column
+// workgroups of 4 waves = 4 K groups, one wave per SIMD (two waves of a workgroup sharing a SIMD
+// serialize their MFMA chains: 64-column, 8-wave workgroups measured 13.3 / 14.8 us with half
+// the chip idle).  Two shapes: frames up to 26 wide with 4 chunks (conv4: 26 x 26 x 128, pooled
+// or not; 2 x 26 tiles, 4 row blocks, one chunk per group) and up to 13 wide with 8 chunks
+// (conv5: 13 x 13 x 256; one-row tiles, one row block, two chunks per group).
+static int x3_ktile_shape(int C, int OC, int H, int W, bool pool) {
+  if (OC % 64 != 0 || !x3_enabled()) return -1;
+  if (C == 128 && W > 13 && W <= 26 && (!pool || (H % 2 == 0 && W % 2 == 0))) return 0;
+  if (C == 256 && W <= 13 && !pool) return 1;
+  return -1;
+}
+
+bool conv_x3_ktile_supported(long long batch, int C, int OC, int H, int W, int OH, int OW, int kh, int kw, int sh,
+                             int sw, int pt, int pl, bool pool) {
+  if (!(kh == 3 && kw == 3 && sh == 1 && sw == 1 && pt == 1 && pl == 1 && OH == H && OW == W)) return false;
+  if (x3_ktile_shape(C, OC, H, W, pool) < 0) return false;
+  return (long long)x3_act_bytes(batch, H, W, C) < 0x80000000LL &&
+         (long long)(OC / 16) * (9 * C / 32) * 3072 < 0x80000000LL;
+}
+
+int launch_conv_x3_ktile(const bf16_bits* in_split, const bf16_bits* Bt, float* out, bf16_bits* out_split, long long M,
+                         int N, int Npad, int K, int H, int W, int C, const EpiParams& epi, hipStream_t stream,
+                         int pool) {
+  if (M == 0 || N == 0) return 0;
+  const int PH = pool ? (H + 1) / 2 : 0, PW = pool ? (W + 1) / 2 : 0;
+  const long long per_img = pool ? 4LL * PH * PW : (long long)H * W;
+  const long long nimg = M / per_img;
+  const long long in_bytes = (long long)x3_act_bytes(nimg, H, W, C);
+  const long long b_bytes = (long long)(Npad / 16) * (K / 32) * 3072;
+  const int shape = x3_ktile_shape(C, N, H, W, pool != 0);
+  if (shape < 0 || M % per_img != 0 || K != 9 * C || Npad != N || in_bytes >= 0x80000000LL ||
+      b_bytes >= 0x80000000LL || (out_split == nullptr) == (out == nullptr) ||
+      x3_act_bytes(nimg, pool ? PH : H, pool ? PW : W, N) >= 0x80000000ULL) {
+    set_error("conv_x3_ktile: unsupported shape M=%lld N=%d K=%d %dx%dx%d", M, N, K, H, W, C);
+    return -2;
+  }
+  const int TH = shape == 0 ? 2 : 1, TW = shape == 0 ? 26 : 13;
+  const int tilesX = (W + TW - 1) / TW, tilesY = (H + TH - 1) / TH, tilesN = N / 32;
+  const long long blocks = nimg * tilesX * tilesY * tilesN;
+  if (blocks > 0x7fffffffLL) {
+    set_error("conv_x3_ktile: grid too large");
+    return -2;
+  }
+  const X3Geom xg{H, W, C, out_split ? 1 : 0, 1, PH, PW};
+  const bool yolo = epi.flags == X3_YOLO_FL;
+#define X3K(TH_, TW_, TM_, CPK_, POOL_, FL_)                                                                    \
+  hipLaunchKernelGGL((conv3x3_x3_ktile_kernel<TH_, TW_, 1, 1, TM_, 4, CPK_, POOL_, FL_>), dim3((unsigned)blocks),   \
+                     dim3(256), 0, stream, in_split, Bt, out, out_split, N, K, epi, tilesX, tilesY, tilesN, xg,     \
+                     (unsigned)in_bytes, (unsigned)b_bytes)
+  // (a 5-step weight ring measured 1 % slower than 3 at one frame: the chains wait on the patch
+  // and the epilogue, not the weights)
+  if (shape == 0 && pool && yolo)
+    X3K(2, 26, 4, 1, true, X3_YOLO_FL);
+  else if (shape == 0 && pool)
+    X3K(2, 26, 4, 1, true, -1);
+  else if (shape == 0)
+    X3K(2, 26, 4, 1, false, -1);
+  else if (yolo)
+    X3K(1, 13, 1, 2, false, X3_YOLO_FL);
+  else
+    X3K(1, 13, 1, 2, false, -1);
+#undef X3K
+  return check_x3("conv_x3_ktile");
+}
+
 int launch_conv_x3_lat(const bf16_bits* in_split, const bf16_bits* Bt, float* part, long long M, int N, int Npad,
                        int K, int H, int W, int C, int splits, hipStream_t stream) {
   if (M == 0 || N == 0) return 0;
@@ -688,6 +755,18 @@ extern "C" __attribute__((visibility("default"))) int dnn_c16_diag_stamps(unsign
   if (n < 0 || n > dnnhip::C16_DIAG_WGS) return -2;
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(dnnhip::c16_diag_stamps), (size_t)n * dnnhip::C16_DIAG_SLOTS * sizeof(unsigned long long), 0,
                              hipMemcpyDeviceToHost) == hipSuccess
+             ? 0
+             : -1;
+}
+#endif
+
+#if (X3DIAG & 256) != 0
+// diagnostic builds (X3DIAG bit 256): conv3x3_x3_ktile_kernel's per-workgroup s_memrealtime
+// stamps [start, patch landed, MFMAs done, end] of its last launch copied to host[0 .. 4n)
+extern "C" __attribute__((visibility("default"))) int dnn_ktile_diag_stamps(unsigned long long* host, int n) {
+  if (n < 0 || n > dnnhip::KT_DIAG_WGS) return -2;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(dnnhip::ktile_diag_stamps), (size_t)n * 4 * sizeof(unsigned long long),
+                             0, hipMemcpyDeviceToHost) == hipSuccess
              ? 0
              : -1;
 }

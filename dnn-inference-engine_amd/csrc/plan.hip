@@ -105,6 +105,7 @@ struct PlanLayer {
   int splits = 1;  // split-K partial count (> 1: GEMM writes partials, a reduce kernel finishes)
   bool pool = false;  // a 2x2/stride-2 max pool fused into this conv
   bool x3lat = false;  // MODE_X3 on the small-M kernel (latency plans: launch_conv_x3_lat)
+  bool x3k = false;    // MODE_X3 with the K split inside the workgroup (latency plans: launch_conv_x3_ktile)
   bool out_padded = false;  // output written zero-bordered (the next layer is MODE_PATCH16 / MODE_X3;
                             // fp32 plans: as x3 split planes)
   size_t pad_off = 0;       // its zero-bordered output region: float offset inside the pad area
@@ -311,7 +312,7 @@ static void set_cfg(dnn_plan* p, PlanLayer& L) {
     L.cfg = 0;
     L.Kpad = L.C == 16 ? 160 : L.K;  // (16 channels: 5 steps of two taps)
     L.Npad = L.OC;  // (a multiple of 256, or of 32 / 64 / 128 for the tile kernels)
-    L.splits = L.x3lat ? x3_lat_splits(L.OC, L.K) : x3_splits(L.OC, L.K);
+    L.splits = L.x3k ? 1 : L.x3lat ? x3_lat_splits(L.OC, L.K) : x3_splits(L.OC, L.K);
     return;
   }
   if (p->fp16 && L.mode == MODE_PATCH16) {  // one config: 192x256 tiles, no split
@@ -428,7 +429,7 @@ int dnn_plan_add_conv(dnn_plan* p, int kh, int kw, int od, int stride_h, int str
   // one-chunk K slice alone takes ~26 us), elsewhere the small-M x3 kernel (gemm_x3_lat.h: 64
   // columns x one or two chunks per workgroup, 8 waves splitting rows / columns / chunks;
   // conv6 / conv7 of a one-frame plan) when it makes at least two K slices
-  bool x3_cand = false, x3_lat = false;
+  bool x3_cand = false, x3_lat = false, x3_k = false;
   if (!p->fp16 && L.mode == MODE_IMPLICIT && !p->layers.empty()) {
     const bool batch_ok = conv_x3_supported(L.C, od, L.H, L.W, L.OH, L.OW, kh, kw, stride_h, stride_w, L.pt, L.pl);
     // (the N = 64 / 128 tile kernels take small tiles at small batches: batch_ok is enough; the
@@ -437,10 +438,15 @@ int dnn_plan_add_conv(dnn_plan* p, int kh, int kw, int od, int stride_h, int str
     const int xk = conv_x3_kind(od, L.C);
     if (p->latency && fused_splitk(p) &&
         !(batch_ok && (xk == 1 || xk == 2 || x3_tiles(p->batch, L.OH, L.OW, od, L.C, L.K) >= 128))) {
-      x3_lat = conv_x3_lat_supported(p->batch, L.C, od, L.H, L.W, L.OH, L.OW, kh, kw, stride_h, stride_w, L.pt,
+      // conv4 / conv5 of a frame: the K split inside the workgroup (one launch, no partials);
+      // conv6 / conv7: the small-M kernel's K slices + combine
+      x3_k = conv_x3_ktile_supported(p->batch, L.C, od, L.H, L.W, L.OH, L.OW, kh, kw, stride_h, stride_w, L.pt,
+                                     L.pl, false);
+      x3_lat = !x3_k &&
+               conv_x3_lat_supported(p->batch, L.C, od, L.H, L.W, L.OH, L.OW, kh, kw, stride_h, stride_w, L.pt,
                                      L.pl) &&
                x3_lat_splits(od, L.K) >= 2;
-      x3_cand = x3_lat;
+      x3_cand = x3_lat || x3_k;
     } else {
       x3_cand = batch_ok;
     }
@@ -469,6 +475,7 @@ int dnn_plan_add_conv(dnn_plan* p, int kh, int kw, int od, int stride_h, int str
         (prev.type == 0 && prev.mode == MODE_PATCH && prev.pool)) {
       L.mode = MODE_X3;
       L.x3lat = x3_lat;
+      L.x3k = x3_k;
       prev.out_padded = true;
     }
   }
@@ -554,7 +561,10 @@ int dnn_plan_add_max_pool(dnn_plan* p, int kh, int kw, int stride_h, int stride_
                                                                       prev.sw)) {
         prev.mode = MODE_DIRECT;
         ok = true;
-      } else if (prev.mode == MODE_X3 && !p->fp16 && conv_x3_pool_supported(prev.OC, prev.C, prev.H, prev.W)) {
+      } else if (prev.mode == MODE_X3 && !p->fp16 &&
+                 (prev.x3k ? conv_x3_ktile_supported(p->batch, prev.C, prev.OC, prev.H, prev.W, prev.OH, prev.OW,
+                                                     prev.kh, prev.kw, prev.sh, prev.sw, prev.pt, prev.pl, true)
+                           : conv_x3_pool_supported(prev.OC, prev.C, prev.H, prev.W))) {
         ok = true;  // pool-window-major rows, pooled before the epilogue in the x3 kernel
       }
       if (ok) {
@@ -862,7 +872,12 @@ int dnn_plan_run(dnn_plan* p, int n, const float* d_in, float* d_out, void* stre
                                   L.C, epi, s);
           break;
         case MODE_X3:
-          if (L.splits > 1) {  // raw partials into the slab; the next pool or a combine kernel finishes
+          if (L.x3k) {
+            rc = launch_conv_x3_ktile(reinterpret_cast<const unsigned short*>(cur),
+                                      reinterpret_cast<const unsigned short*>(wt), dsplit ? nullptr : dst, dsplit,
+                                      L.pool ? 4LL * n * L.PH * L.PW : Mc, L.OC, L.Npad, L.K, L.H, L.W, L.C, epi, s,
+                                      L.pool ? 1 : 0);
+          } else if (L.splits > 1) {  // raw partials into the slab; the next pool or a combine kernel finishes
             rc = L.x3lat ? launch_conv_x3_lat(reinterpret_cast<const unsigned short*>(cur),
                                               reinterpret_cast<const unsigned short*>(wt), slab, Mc, L.OC, L.Npad, L.K,
                                               L.H, L.W, L.C, L.splits, s)
@@ -988,7 +1003,7 @@ int dnn_plan_describe(const dnn_plan* p, char* buf, int buf_len) {
       char sk[32] = "";
       if (L.splits > 1) snprintf(sk, sizeof(sk), " splitK=%d", L.splits);
       snprintf(line, sizeof(line), "conv %dx%dx%d -> %dx%dx%d k%dx%d s%d mode=%s cfg=%d K=%d Kpad=%d%s%s%s%s%s\n", L.H,
-               L.W, L.C, L.out_h(), L.out_w(), L.OC, L.kh, L.kw, L.sh, L.x3lat ? "x3_lat" : kModeName[L.mode], L.cfg, L.K, L.Kpad,
+               L.W, L.C, L.out_h(), L.out_w(), L.OC, L.kh, L.kw, L.sh, L.x3lat ? "x3_lat" : L.x3k ? "x3_ktile" : kModeName[L.mode], L.cfg, L.K, L.Kpad,
                L.pool ? " +pool2x2s2" : "", sk,
                L.splits > 1 ? (L.mode == MODE_X3 ? " x3-combine" : fused_splitk(p) ? " combine" : "") : "",
                p->fp16 ? " fp16" : "", p->latency ? " latency" : "");

@@ -903,7 +903,8 @@ def test_latency_split_combine_vs_oracle(monkeypatch, case):
 @pytest.mark.parametrize("frame", [0, 1, 2, 3])
 def test_yolo_latency_plan_vs_reference_golden(yolo_weights, golden_frames, frame, latency_b1_engine=[]):
     """BASELINE config 2 in latency mode: conv2 / conv3 on the x3 tile kernel (2 x 26 tiles at
-    one frame, conv1's patch conv writing their split planes), conv4-conv8 split over the chip; within the net tolerance of the reference goldens
+    one frame, conv1's patch conv writing their split planes), conv4 / conv5 on the x3 kernel with
+    the K split inside the workgroup, conv6 / conv7 on the small-M x3 kernel, conv8 split over the chip; within the net tolerance of the reference goldens
     (not bit-equal to the batch plan's rows)."""
     if not latency_b1_engine:
         g, _ = yolo_graph.build_graph(dnn_hip.DnnGraphBuilder, yolo_weights, in_shape=(1, 416, 416, 3))
@@ -911,11 +912,86 @@ def test_yolo_latency_plan_vs_reference_golden(yolo_weights, golden_frames, fram
     eng = latency_b1_engine[0]
     desc = eng.plan().describe()
     conv = [ln for ln in desc.splitlines() if ln.startswith("conv")]
-    assert all(" combine latency" in conv[i] for i in (4, 5, 8)), desc
+    assert "mode=x3_ktile" in conv[4] and "mode=x3_ktile" in conv[5] and " combine latency" in conv[8], desc
     assert "mode=x3_lat" in conv[6] and "mode=x3_lat" in conv[7], desc  # conv6 / conv7: small-M x3
     assert "mode=patch " in conv[1] and all("mode=patch_x3" in conv[i] for i in (2, 3)), desc  # conv2/3: x3
     y = eng.run(synth.frame(frame))
     assert R.normwise_err(y, golden_frames[frame]) < NET_TOL
+
+
+X3_KTILE_CASES = [
+    # B: pool 2x2 s1 -> conv3x3 128->256 + pool 2x2 s2 (26x26: the pooled 26-wide shape, 4 K
+    # groups of one chunk) -> conv3x3 256->512 (13x13: the 13-wide shape, 4 groups of two chunks)
+    # -> pool 2x2 s1, in a latency plan (YOLO's conv4 / conv5 / pool5)
+    1, 2,
+]
+
+
+@pytest.mark.parametrize("B", X3_KTILE_CASES)
+def test_x3_ktile_kernel_vs_oracle(monkeypatch, B):
+    """conv3x3_x3_ktile_kernel (latency plans' conv4 / conv5): the K split over 4 wave groups
+    inside the workgroup, the groups' folded sums added in group order, then the fused pool /
+    epilogue.  Each chain within the fp32 tolerance of the float64 oracle and within 1.25x of the
+    fp32 MFMA latency plan's error (DNN_HIP_X3=0); repeat runs and graph replays identical; a
+    two-frame run's rows equal to one-frame runs (the tiling has no cross-frame state)."""
+    rng = np.random.default_rng(11 + B)
+    x = rng.standard_normal((B, 26, 26, 128)).astype(np.float32)
+
+    def layer(c, od):
+        k = (rng.standard_normal((3, 3, c, od)) * np.sqrt(2.0 / (9 * c))).astype(np.float32)
+        b = rng.standard_normal(od).astype(np.float32) * 0.1
+        gam = rng.uniform(0.5, 1.5, od).astype(np.float32)
+        gam[::5] *= -1
+        return k, b, (rng.standard_normal(od).astype(np.float32) * 0.1, rng.uniform(0.5, 1.5, od).astype(np.float32),
+                      gam)
+
+    L = [layer(128, 256), layer(256, 512)]
+
+    def graph(shape):
+        g = dnn_hip.DnnGraphBuilder()
+        y = g.create_input(list(shape))
+        y = g.create_max_pool2d(y, [1, 2, 2, 1], [1, 1, 1, 1], "SAME")
+        for j, (k, b, n) in enumerate(L):
+            y = g.create_conv2d(y, k, [1, 1, 1, 1], "SAME")
+            y = g.create_bias_add(y, b)
+            y = g.create_batch_norm(y, *n, 1e-5)
+            y = g.create_leaky_relu(y)
+            y = g.create_max_pool2d(y, [1, 2, 2, 1], [1, 2, 2, 1] if j == 0 else [1, 1, 1, 1], "SAME")
+        g.set_out_node(y)
+        return g
+
+    ref = R.max_pool2d(x, [1, 2, 2, 1], [1, 1, 1, 1], "SAME")
+    for j, (k, b, n) in enumerate(L):
+        ref = R.leaky_relu(R.batch_norm(R.bias_add(R.conv2d(ref, k), b), *n, 1e-5))
+        ref = R.max_pool2d(ref, [1, 2, 2, 1], [1, 2, 2, 1] if j == 0 else [1, 1, 1, 1], "SAME")
+    errs = {}
+    for x3 in ("1", "0"):
+        monkeypatch.setenv("DNN_HIP_X3", x3)
+        eng = dnn_hip.DnnInferenceEngine(graph(x.shape), False, latency=True)
+        desc = eng.plan().describe()
+        conv = [ln for ln in desc.splitlines() if ln.startswith("conv")]
+        if x3 == "1":
+            assert "mode=x3_ktile" in conv[0] and "+pool2x2s2" in conv[0] and "mode=x3_ktile" in conv[1], desc
+        y = eng.run(x)
+        errs[x3] = R.normwise_err(y, ref)
+        if x3 == "1":
+            assert np.array_equal(eng.run(x), y)
+            import torch
+            p = eng.plan()
+            xd = torch.from_numpy(x).cuda()
+            yd = torch.empty((B,) + p.out_shape, device="cuda")
+            st = torch.cuda.Stream()
+            for _ in range(2):
+                p.run_graph(B, xd.data_ptr(), yd.data_ptr(), st.cuda_stream)
+            st.synchronize()
+            assert np.array_equal(yd.cpu().numpy(), y)
+            if B > 1:
+                one = dnn_hip.DnnInferenceEngine(graph((1,) + x.shape[1:]), False, latency=True)
+                for f in range(B):
+                    assert np.array_equal(one.run(x[f:f + 1]), y[f:f + 1]), f
+    print("ktile chain errs", errs)
+    assert errs["1"] < 3 * LAYER_TOL and errs["0"] < 3 * LAYER_TOL, errs
+    assert errs["1"] <= 1.25 * errs["0"], errs
 
 
 X3_LAT_CASES = [
@@ -923,9 +999,9 @@ X3_LAT_CASES = [
     # or None: pool (2x2 s1) -> conv3x3 C->od1 -> conv3x3 od1->od2 [-> conv1x1 + bias] in a
     # latency plan, both 3x3 convs on the small-M x3 kernel (any workgroup count here)
     (1, 13, 13, 512, 1024, 1024, None, 125),  # conv6 / conv7 / conv8 at batch 1
-    (2, 13, 13, 256, 512, 256, None, None),   # two frames: two 176-row tiles, the second straddling
+    (2, 13, 13, 512, 320, 256, None, None),   # two frames: two 176-row tiles, the second straddling
     (1, 9, 11, 64, 192, 320, None, 40),       # non-square frame, N = 192 / 320, 2 and 6 chunks, small head
-    (1, 13, 13, 128, 256, 256, 2, None),      # two chunks per workgroup forced (4 -> 2 slices; 8 -> 4)
+    (1, 13, 13, 128, 192, 256, 2, None),      # two chunks per workgroup forced (4 -> 2 slices; 6 -> 3)
 ]
 
 

@@ -8,6 +8,7 @@ Prints per arm the median over rounds of the device time of one graph replay (HI
 `reps` back-to-back replays, bench.py latency_b1's `graph_device_ms`), the per-kernel HIP-event
 times of eager runs, and the normwise difference of the arm's output from the first arm's."""
 import argparse
+import ctypes
 import json
 import os
 import statistics
@@ -21,6 +22,30 @@ import torch  # noqa: E402
 import dnn_hip  # noqa: E402
 import synth  # noqa: E402
 import yolo_graph  # noqa: E402
+
+
+def ktile_stamps(lib):
+    """X3DIAG bit 256 builds: conv3x3_x3_ktile_kernel's per-workgroup s_memrealtime stamps (100 MHz)
+    of the last launch of each shape: start skew, patch, MFMA and epilogue phases (us)."""
+    fn = getattr(lib, "dnn_ktile_diag_stamps", None)
+    if fn is None:
+        return None
+    fn.restype = ctypes.c_int
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    buf = (ctypes.c_ulonglong * (4 * 1024))()
+    if fn(buf, 1024) != 0:
+        return None
+    out = {}
+    for name, base in (("w26", 0), ("w13", 512)):
+        rows = [buf[4 * w:4 * w + 4] for w in range(base, base + 512) if buf[4 * w] and buf[4 * w + 3] >= buf[4 * w]]
+        if not rows:
+            continue
+        t0 = min(r[0] for r in rows)
+        med = lambda f: round(statistics.median(f(r) for r in rows) / 100.0, 2)  # noqa: E731
+        out[name] = {"workgroups": len(rows), "start_skew_max": round(max(r[0] - t0 for r in rows) / 100.0, 2),
+                     "patch": med(lambda r: r[1] - r[0]), "mfma": med(lambda r: r[2] - r[1]),
+                     "epilogue": med(lambda r: r[3] - r[2]), "span": round((max(r[3] for r in rows) - t0) / 100.0, 2)}
+    return out
 
 
 def main():
@@ -91,6 +116,9 @@ def main():
             ms, cnt = p.timing_end()
             for k, m, c in zip(p.kernels(), ms, cnt):
                 d["k"].setdefault(k["name"], []).append(m / max(c, 1))
+            kt = ktile_stamps(p.lib)
+            if kt:
+                d["ktile"] = kt
     # a tail of graph replays of arm 0 (a kernel trace of this run ends with whole replays:
     # tools/trace_timeline.py)
     d = plans[0]
@@ -106,6 +134,8 @@ def main():
                "graph_device_ms_min": round(min(d["graph"]), 4),
                "kernels_ms_median": {k: round(statistics.median(v), 4) for k, v in d["k"].items()},
                "normwise_vs_arm0": err}
+        if d.get("ktile"):
+            rec["ktile_stamps_us_last_round"] = d["ktile"]
         out[json.dumps(d["arm"])] = rec
         print(json.dumps(d["arm"]), json.dumps(rec), flush=True)
     print(json.dumps(out))
