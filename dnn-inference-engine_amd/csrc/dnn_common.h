@@ -247,7 +247,7 @@ long long x3_tiles(long long batch, int OH, int OW, int OC, int C, int K);
 // latency plans' mid layers: x3 with the K split inside the workgroup (gemm_x3_ktile.h), one
 // launch, no partials; deterministic, tolerance against the batch plans
 bool conv_x3_ktile_supported(long long batch, int C, int OC, int H, int W, int OH, int OW, int kh, int kw, int sh,
-                             int sw, int pt, int pl, bool pool);
+                             int sw, int pt, int pl, int pool);  // pool: 0, 1 (2x2/s2), 2 (2x2/s1 SAME)
 int launch_conv_x3_ktile(const unsigned short* in_split, const unsigned short* Bt, float* out,
                          unsigned short* out_split, long long M, int N, int Npad, int K, int H, int W, int C,
                          const EpiParams& epi, hipStream_t stream, int pool);

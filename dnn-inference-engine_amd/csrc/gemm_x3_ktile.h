@@ -30,13 +30,15 @@ __device__ unsigned long long ktile_diag_stamps[KT_DIAG_WGS * 4];
 #define KT_STAMP(k)
 #endif
 
-template <int TH, int TW, int WM, int WN, int TM, int KW, int CPK, bool POOL, int FL = -1, int NB = 3>
+template <int TH, int TW, int WM, int WN, int TM, int KW, int CPK, bool POOL, int FL = -1, int NB = 3, bool PL1 = false>
 __global__ void __launch_bounds__(64 * WM * WN * KW, 1)
 conv3x3_x3_ktile_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __restrict__ Bt, float* __restrict__ out,
                         bf16_bits* __restrict__ out_split, int N, int K, EpiParams epi, int tilesX, int tilesY,
                         int tilesN, X3Geom g, unsigned in_bytes, unsigned b_bytes) {
   constexpr int NG = WM * WN, NW = NG * KW, NT = 64 * NW, LP = 224, PU = LP / 16, PW2 = TW + 2;
-  constexpr int PR = (TH + 2) * PW2, T = TH * TW, NCH = KW * CPK;
+  // PL1: a 2x2 stride-1 SAME pool fused (YOLO's pool5): the tile also computes the row below it
+  constexpr int TR = PL1 ? (TH + 1) * TW : TH * TW;
+  constexpr int PR = (TH + 2 + (PL1 ? 1 : 0)) * PW2, T = TH * TW, NCH = KW * CPK;
   constexpr int NPC = (PR * PU + 63) / 64;           // 1-KiB DMA pieces per chunk
   constexpr int BUFB = NPC * 1024;                   // one chunk's patch
   constexpr int NPW = (NCH * NPC + NW - 1) / NW;     // pieces per wave, all chunks
@@ -44,8 +46,9 @@ conv3x3_x3_ktile_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __res
   constexpr int NO = POOL ? T / 4 : T;
   constexpr int PATCH = NCH * BUFB;
   constexpr int SM = (PATCH > RED ? PATCH : RED);
-  static_assert((!POOL || (TH % 2 == 0 && TW % 2 == 0)) && WM * TM * 16 >= T && (WM * TM - 2) * 16 < T && NW <= 16,
+  static_assert((!POOL || (TH % 2 == 0 && TW % 2 == 0)) && WM * TM * 16 >= TR && (WM * TM - 2) * 16 < TR && NW <= 16,
                 "shape");
+  static_assert(!PL1 || (!POOL && NG == 1 && 4 * T <= 64 && RED + TR * 36 * 4 <= SM), "stride-1 pool");
   static_assert(SM + NO * 4 <= 160 * 1024 && RED % 1024 == 0 && RED + NG * TM * 4 * X3_STG_ROW * 4 <= SM, "LDS");
   __shared__ __attribute__((aligned(1024))) unsigned char smem[SM + NO * 4];
   int* const orow = reinterpret_cast<int*>(smem + SM);
@@ -74,7 +77,7 @@ conv3x3_x3_ktile_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __res
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     int r = (wm * TM + i) * 16 + fr;
-    r = r < T ? r : T - 1;
+    r = r < TR ? r : TR - 1;
     int ly, lx;
     if constexpr (POOL) {
       const int w = r >> 2, q = r & 3;
@@ -125,6 +128,21 @@ conv3x3_x3_ktile_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __res
 #pragma unroll
   for (int k = 0; k + 1 < NB; ++k) load_b(k, bq[k]);
   const X3EpiCol ecp[2] = {x3_epi_col(epi, eflags, n0 + fr), x3_epi_col(epi, eflags, n0 + 16 + fr)};  // (prefetched)
+  // PL1: this lane's pooled task (pixel lane / 4 of the tile row, channels n0 + 8 (lane % 4) ..
+  // + 7) and its 8 channels' epilogue parameters
+  f32x4 p1[4][2];
+  if constexpr (PL1) {
+    const int c = n0 + 8 * (lane & 3);
+    const float* src[4] = {epi.bias, epi.mean, epi.sq, epi.gamma};
+    const bool use[4] = {(eflags & EPI_BIAS) != 0, (eflags & (EPI_BN | EPI_BN_AB)) != 0,
+                         (eflags & (EPI_BN | EPI_BN_AB)) != 0, (eflags & EPI_BN) != 0};
+    const float dflt[4] = {0.f, 0.f, 1.f, 1.f};
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+        p1[q][h] = use[q] ? *reinterpret_cast<const f32x4*>(src[q] + c + 4 * h) : f32x4{dflt[q], dflt[q], dflt[q], dflt[q]};
+  }
 
   f32x4 acc[TM][2], accc[TM][2];
 #pragma unroll
@@ -207,6 +225,66 @@ conv3x3_x3_ktile_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __res
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int jb = 0; jb < 2; ++jb) acc[i][jb] = acc[i][jb] + red[((((k - 1) * NG + wg) * TM + i) * 2 + jb) * 64 + lane];
+
+  if constexpr (PL1) {
+    // raw sums of the TH + 1 computed rows into a wave-private stage (rows of 36 floats, past
+    // `red`), then per lane one task: pixel x of the tile's row, 8 channels; window (y, x), (y,
+    // x + 1), (y + 1, x), (y + 1, x + 1) with x + 1 / y + 1 clamped into the frame (SAME: the
+    // pad never wins a max), pooled before the epilogue (pool_then_epilogue, as the 2x2/s2 pools)
+    float* stg = reinterpret_cast<float*>(smem + RED);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int jb = 0; jb < 2; ++jb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = 16 * i + 4 * fq + r;
+          if (row < TR) stg[row * 36 + 16 * jb + fr] = acc[i][jb][r];
+        }
+    wait_lgkm0();
+    const int x = lane >> 2, c8 = 8 * (lane & 3);
+    if (lane < 4 * T) {
+      const int y = y0 + x / TW, xx = x0 + x % TW;  // (TH = 1: x / TW = 0)
+      if (y < g.H && xx < g.W) {
+        const int lx = x % TW, ly = x / TW;
+        const int lx1 = xx + 1 < g.W ? lx + 1 : lx, ly1 = y + 1 < g.H ? ly + 1 : ly;
+        const int ra = ly * TW + lx, rb = ly * TW + lx1, rc = ly1 * TW + lx, rd = ly1 * TW + lx1;
+        float o[8];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const f32x4 va = *reinterpret_cast<const f32x4*>(stg + ra * 36 + c8 + 4 * h);
+          const f32x4 vb = *reinterpret_cast<const f32x4*>(stg + rb * 36 + c8 + 4 * h);
+          const f32x4 vc = *reinterpret_cast<const f32x4*>(stg + rc * 36 + c8 + 4 * h);
+          const f32x4 vd = *reinterpret_cast<const f32x4*>(stg + rd * 36 + c8 + 4 * h);
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            o[4 * h + e] = pool_then_epilogue_t<FL>(f32x4{va[e], vb[e], vc[e], vd[e]}, p1[0][h][e], p1[1][h][e],
+                                                    p1[2][h][e], p1[3][h][e], epi.flags);
+        }
+        if (g.out_mode == 1) {
+          const size_t op = ((size_t)b * (g.H + 2) + y + 1) * (size_t)Wp + xx + 1;
+          u32x4 q[3];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            unsigned w0, w1, w2;
+            split3_pack2(false, o[2 * e], o[2 * e + 1], w0, w1, w2);
+            q[0][e] = w0;
+            q[1][e] = w1;
+            q[2][e] = w2;
+          }
+          bf16_bits* d = out_split + op * (3 * (size_t)N) + (n0 >> 5) * 96 + c8;
+#pragma unroll
+          for (int pc = 0; pc < 3; ++pc) *reinterpret_cast<u32x4*>(d + 32 * pc) = q[pc];
+        } else {
+          float* d = out + (((size_t)b * g.H + y) * g.W + xx) * N + n0 + c8;
+          *reinterpret_cast<f32x4*>(d) = f32x4{o[0], o[1], o[2], o[3]};
+          *reinterpret_cast<f32x4*>(d + 4) = f32x4{o[4], o[5], o[6], o[7]};
+        }
+      }
+    }
+    KT_STAMP(3)
+    return;
+  }
 
   if constexpr (POOL) {
     if (g.out_mode == 1) {  // staged 16-B split-plane stores (x3_pool_split_store), group 0's waves

@@ -598,15 +598,16 @@ bool conv_x3_lat_supported(long long batch, int C, int OC, int H, int W, int OH,
 // the chip idle).  Two shapes: frames up to 26 wide with 4 chunks (conv4: 26 x 26 x 128, pooled
 // or not; 2 x 26 tiles, 4 row blocks, one chunk per group) and up to 13 wide with 8 chunks
 // (conv5: 13 x 13 x 256; one-row tiles, one row block, two chunks per group).
-static int x3_ktile_shape(int C, int OC, int H, int W, bool pool) {
+// pool: 0 none, 1 a fused 2x2/s2 pool, 2 a fused 2x2/s1 SAME pool (YOLO's pool5; 13-wide shape)
+static int x3_ktile_shape(int C, int OC, int H, int W, int pool) {
   if (OC % 64 != 0 || !x3_enabled()) return -1;
-  if (C == 128 && W > 13 && W <= 26 && (!pool || (H % 2 == 0 && W % 2 == 0))) return 0;
-  if (C == 256 && W <= 13 && !pool) return 1;
+  if (C == 128 && W > 13 && W <= 26 && (pool == 0 || (pool == 1 && H % 2 == 0 && W % 2 == 0))) return 0;
+  if (C == 256 && W <= 13 && pool != 1) return 1;
   return -1;
 }
 
 bool conv_x3_ktile_supported(long long batch, int C, int OC, int H, int W, int OH, int OW, int kh, int kw, int sh,
-                             int sw, int pt, int pl, bool pool) {
+                             int sw, int pt, int pl, int pool) {
   if (!(kh == 3 && kw == 3 && sh == 1 && sw == 1 && pt == 1 && pl == 1 && OH == H && OW == W)) return false;
   if (x3_ktile_shape(C, OC, H, W, pool) < 0) return false;
   return (long long)x3_act_bytes(batch, H, W, C) < 0x80000000LL &&
@@ -617,16 +618,17 @@ int launch_conv_x3_ktile(const bf16_bits* in_split, const bf16_bits* Bt, float* 
                          int N, int Npad, int K, int H, int W, int C, const EpiParams& epi, hipStream_t stream,
                          int pool) {
   if (M == 0 || N == 0) return 0;
-  const int PH = pool ? (H + 1) / 2 : 0, PW = pool ? (W + 1) / 2 : 0;
-  const long long per_img = pool ? 4LL * PH * PW : (long long)H * W;
+  const bool p2 = pool == 1;  // (pool 2, stride 1: the output frame is the input frame)
+  const int PH = p2 ? (H + 1) / 2 : 0, PW = p2 ? (W + 1) / 2 : 0;
+  const long long per_img = p2 ? 4LL * PH * PW : (long long)H * W;
   const long long nimg = M / per_img;
   const long long in_bytes = (long long)x3_act_bytes(nimg, H, W, C);
   const long long b_bytes = (long long)(Npad / 16) * (K / 32) * 3072;
-  const int shape = x3_ktile_shape(C, N, H, W, pool != 0);
+  const int shape = x3_ktile_shape(C, N, H, W, pool);
   if (shape < 0 || M % per_img != 0 || K != 9 * C || Npad != N || in_bytes >= 0x80000000LL ||
       b_bytes >= 0x80000000LL || (out_split == nullptr) == (out == nullptr) ||
-      x3_act_bytes(nimg, pool ? PH : H, pool ? PW : W, N) >= 0x80000000ULL) {
-    set_error("conv_x3_ktile: unsupported shape M=%lld N=%d K=%d %dx%dx%d", M, N, K, H, W, C);
+      x3_act_bytes(nimg, p2 ? PH : H, p2 ? PW : W, N) >= 0x80000000ULL) {
+    set_error("conv_x3_ktile: unsupported shape M=%lld N=%d K=%d %dx%dx%d pool=%d", M, N, K, H, W, C, pool);
     return -2;
   }
   const int TH = shape == 0 ? 2 : 1, TW = shape == 0 ? 26 : 13;
@@ -638,22 +640,25 @@ int launch_conv_x3_ktile(const bf16_bits* in_split, const bf16_bits* Bt, float* 
   }
   const X3Geom xg{H, W, C, out_split ? 1 : 0, 1, PH, PW};
   const bool yolo = epi.flags == X3_YOLO_FL;
-#define X3K(TH_, TW_, TM_, CPK_, POOL_, FL_)                                                                    \
-  hipLaunchKernelGGL((conv3x3_x3_ktile_kernel<TH_, TW_, 1, 1, TM_, 4, CPK_, POOL_, FL_>), dim3((unsigned)blocks),   \
-                     dim3(256), 0, stream, in_split, Bt, out, out_split, N, K, epi, tilesX, tilesY, tilesN, xg,     \
-                     (unsigned)in_bytes, (unsigned)b_bytes)
-  // (a 5-step weight ring measured 1 % slower than 3 at one frame: the chains wait on the patch
-  // and the epilogue, not the weights)
-  if (shape == 0 && pool && yolo)
-    X3K(2, 26, 4, 1, true, X3_YOLO_FL);
-  else if (shape == 0 && pool)
-    X3K(2, 26, 4, 1, true, -1);
+#define X3K(TH_, TW_, TM_, CPK_, POOL_, FL_, PL1_)                                                                 \
+  hipLaunchKernelGGL((conv3x3_x3_ktile_kernel<TH_, TW_, 1, 1, TM_, 4, CPK_, POOL_, FL_, 3, PL1_>),                 \
+                     dim3((unsigned)blocks), dim3(256), 0, stream, in_split, Bt, out, out_split, N, K, epi, tilesX, \
+                     tilesY, tilesN, xg, (unsigned)in_bytes, (unsigned)b_bytes)
+  // (a 5-step weight ring measured 1 % slower than 3 in the earlier 8-wave form)
+  if (shape == 0 && p2 && yolo)
+    X3K(2, 26, 4, 1, true, X3_YOLO_FL, false);
+  else if (shape == 0 && p2)
+    X3K(2, 26, 4, 1, true, -1, false);
   else if (shape == 0)
-    X3K(2, 26, 4, 1, false, -1);
+    X3K(2, 26, 4, 1, false, -1, false);
+  else if (pool == 2 && yolo)  // (each one-row tile computes the row below it too: 2 row blocks)
+    X3K(1, 13, 2, 2, false, X3_YOLO_FL, true);
+  else if (pool == 2)
+    X3K(1, 13, 2, 2, false, -1, true);
   else if (yolo)
-    X3K(1, 13, 1, 2, false, X3_YOLO_FL);
+    X3K(1, 13, 1, 2, false, X3_YOLO_FL, false);
   else
-    X3K(1, 13, 1, 2, false, -1);
+    X3K(1, 13, 1, 2, false, -1, false);
 #undef X3K
   return check_x3("conv_x3_ktile");
 }

@@ -106,6 +106,7 @@ struct PlanLayer {
   bool pool = false;  // a 2x2/stride-2 max pool fused into this conv
   bool x3lat = false;  // MODE_X3 on the small-M kernel (latency plans: launch_conv_x3_lat)
   bool x3k = false;    // MODE_X3 with the K split inside the workgroup (latency plans: launch_conv_x3_ktile)
+  bool pool1 = false;  // x3k: a 2x2/stride-1 SAME pool fused (same output frame)
   bool out_padded = false;  // output written zero-bordered (the next layer is MODE_PATCH16 / MODE_X3;
                             // fp32 plans: as x3 split planes)
   size_t pad_off = 0;       // its zero-bordered output region: float offset inside the pad area
@@ -441,7 +442,7 @@ int dnn_plan_add_conv(dnn_plan* p, int kh, int kw, int od, int stride_h, int str
       // conv4 / conv5 of a frame: the K split inside the workgroup (one launch, no partials);
       // conv6 / conv7: the small-M kernel's K slices + combine
       x3_k = conv_x3_ktile_supported(p->batch, L.C, od, L.H, L.W, L.OH, L.OW, kh, kw, stride_h, stride_w, L.pt,
-                                     L.pl, false);
+                                     L.pl, 0);
       x3_lat = !x3_k &&
                conv_x3_lat_supported(p->batch, L.C, od, L.H, L.W, L.OH, L.OW, kh, kw, stride_h, stride_w, L.pt,
                                      L.pl) &&
@@ -563,7 +564,7 @@ int dnn_plan_add_max_pool(dnn_plan* p, int kh, int kw, int stride_h, int stride_
         ok = true;
       } else if (prev.mode == MODE_X3 && !p->fp16 &&
                  (prev.x3k ? conv_x3_ktile_supported(p->batch, prev.C, prev.OC, prev.H, prev.W, prev.OH, prev.OW,
-                                                     prev.kh, prev.kw, prev.sh, prev.sw, prev.pt, prev.pl, true)
+                                                     prev.kh, prev.kw, prev.sh, prev.sw, prev.pt, prev.pl, 1)
                            : conv_x3_pool_supported(prev.OC, prev.C, prev.H, prev.W))) {
         ok = true;  // pool-window-major rows, pooled before the epilogue in the x3 kernel
       }
@@ -575,6 +576,18 @@ int dnn_plan_add_max_pool(dnn_plan* p, int kh, int kw, int stride_h, int stride_
         p->cur_w = L.OW;
         return 0;
       }
+    }
+  }
+  // a 2x2/stride-1 SAME pool (YOLO's pool5) into a single-frame x3k conv before it: the conv
+  // computes the row below each tile too and pools before its epilogue
+  if (p->fuse && !p->layers.empty() && kh == 2 && kw == 2 && stride_h == 1 && stride_w == 1 && L.pt == 0 &&
+      L.pl == 0 && L.OH == L.H && L.OW == L.W) {
+    PlanLayer& prev = p->layers.back();
+    if (prev.type == 0 && prev.mode == MODE_X3 && prev.x3k && !prev.pool && !prev.pool1 &&
+        conv_x3_ktile_supported(p->batch, prev.C, prev.OC, prev.H, prev.W, prev.OH, prev.OW, prev.kh, prev.kw,
+                                prev.sh, prev.sw, prev.pt, prev.pl, 2)) {
+      prev.pool1 = true;
+      return 0;
     }
   }
   p->layers.push_back(std::move(L));
@@ -876,7 +889,7 @@ int dnn_plan_run(dnn_plan* p, int n, const float* d_in, float* d_out, void* stre
             rc = launch_conv_x3_ktile(reinterpret_cast<const unsigned short*>(cur),
                                       reinterpret_cast<const unsigned short*>(wt), dsplit ? nullptr : dst, dsplit,
                                       L.pool ? 4LL * n * L.PH * L.PW : Mc, L.OC, L.Npad, L.K, L.H, L.W, L.C, epi, s,
-                                      L.pool ? 1 : 0);
+                                      L.pool ? 1 : L.pool1 ? 2 : 0);
           } else if (L.splits > 1) {  // raw partials into the slab; the next pool or a combine kernel finishes
             rc = L.x3lat ? launch_conv_x3_lat(reinterpret_cast<const unsigned short*>(cur),
                                               reinterpret_cast<const unsigned short*>(wt), slab, Mc, L.OC, L.Npad, L.K,
@@ -1004,7 +1017,7 @@ int dnn_plan_describe(const dnn_plan* p, char* buf, int buf_len) {
       if (L.splits > 1) snprintf(sk, sizeof(sk), " splitK=%d", L.splits);
       snprintf(line, sizeof(line), "conv %dx%dx%d -> %dx%dx%d k%dx%d s%d mode=%s cfg=%d K=%d Kpad=%d%s%s%s%s%s\n", L.H,
                L.W, L.C, L.out_h(), L.out_w(), L.OC, L.kh, L.kw, L.sh, L.x3lat ? "x3_lat" : L.x3k ? "x3_ktile" : kModeName[L.mode], L.cfg, L.K, L.Kpad,
-               L.pool ? " +pool2x2s2" : "", sk,
+               L.pool ? " +pool2x2s2" : L.pool1 ? " +pool2x2s1" : "", sk,
                L.splits > 1 ? (L.mode == MODE_X3 ? " x3-combine" : fused_splitk(p) ? " combine" : "") : "",
                p->fp16 ? " fp16" : "", p->latency ? " latency" : "");
     } else

@@ -904,7 +904,8 @@ def test_latency_split_combine_vs_oracle(monkeypatch, case):
 def test_yolo_latency_plan_vs_reference_golden(yolo_weights, golden_frames, frame, latency_b1_engine=[]):
     """BASELINE config 2 in latency mode: conv2 / conv3 on the x3 tile kernel (2 x 26 tiles at
     one frame, conv1's patch conv writing their split planes), conv4 / conv5 on the x3 kernel with
-    the K split inside the workgroup, conv6 / conv7 on the small-M x3 kernel, conv8 split over the chip; within the net tolerance of the reference goldens
+    the K split inside the workgroup (pool5 fused into conv5), conv6 / conv7 on the small-M x3
+    kernel, conv8 split over the chip; within the net tolerance of the reference goldens
     (not bit-equal to the batch plan's rows)."""
     if not latency_b1_engine:
         g, _ = yolo_graph.build_graph(dnn_hip.DnnGraphBuilder, yolo_weights, in_shape=(1, 416, 416, 3))
@@ -912,7 +913,8 @@ def test_yolo_latency_plan_vs_reference_golden(yolo_weights, golden_frames, fram
     eng = latency_b1_engine[0]
     desc = eng.plan().describe()
     conv = [ln for ln in desc.splitlines() if ln.startswith("conv")]
-    assert "mode=x3_ktile" in conv[4] and "mode=x3_ktile" in conv[5] and " combine latency" in conv[8], desc
+    assert "mode=x3_ktile" in conv[4] and "mode=x3_ktile" in conv[5] and "+pool2x2s1" in conv[5], desc
+    assert " combine latency" in conv[8], desc
     assert "mode=x3_lat" in conv[6] and "mode=x3_lat" in conv[7], desc  # conv6 / conv7: small-M x3
     assert "mode=patch " in conv[1] and all("mode=patch_x3" in conv[i] for i in (2, 3)), desc  # conv2/3: x3
     y = eng.run(synth.frame(frame))
@@ -920,20 +922,22 @@ def test_yolo_latency_plan_vs_reference_golden(yolo_weights, golden_frames, fram
 
 
 X3_KTILE_CASES = [
-    # B: pool 2x2 s1 -> conv3x3 128->256 + pool 2x2 s2 (26x26: the pooled 26-wide shape, 4 K
+    # B, pool5: pool 2x2 s1 -> conv3x3 128->256 + pool 2x2 s2 (26x26: the pooled 26-wide shape, 4 K
     # groups of one chunk) -> conv3x3 256->512 (13x13: the 13-wide shape, 4 groups of two chunks)
-    # -> pool 2x2 s1, in a latency plan (YOLO's conv4 / conv5 / pool5)
-    1, 2,
+    # [-> pool 2x2 s1 SAME, fused into it], in a latency plan (YOLO's conv4 / conv5 / pool5)
+    (1, True), (2, True), (2, False),
 ]
 
 
-@pytest.mark.parametrize("B", X3_KTILE_CASES)
-def test_x3_ktile_kernel_vs_oracle(monkeypatch, B):
+@pytest.mark.parametrize("case", X3_KTILE_CASES)
+def test_x3_ktile_kernel_vs_oracle(monkeypatch, case):
     """conv3x3_x3_ktile_kernel (latency plans' conv4 / conv5): the K split over 4 wave groups
-    inside the workgroup, the groups' folded sums added in group order, then the fused pool /
-    epilogue.  Each chain within the fp32 tolerance of the float64 oracle and within 1.25x of the
-    fp32 MFMA latency plan's error (DNN_HIP_X3=0); repeat runs and graph replays identical; a
-    two-frame run's rows equal to one-frame runs (the tiling has no cross-frame state)."""
+    inside the workgroup, the groups' folded sums added in group order, then the fused pool
+    (2x2/s2, or 2x2/s1 SAME with the row below each tile computed too) and epilogue.  Each chain
+    within the fp32 tolerance of the float64 oracle and within 1.25x of the fp32 MFMA latency
+    plan's error (DNN_HIP_X3=0); repeat runs and graph replays identical; a two-frame run's rows
+    equal to one-frame runs (the tiling has no cross-frame state)."""
+    B, pool5 = case
     rng = np.random.default_rng(11 + B)
     x = rng.standard_normal((B, 26, 26, 128)).astype(np.float32)
 
@@ -956,14 +960,16 @@ def test_x3_ktile_kernel_vs_oracle(monkeypatch, B):
             y = g.create_bias_add(y, b)
             y = g.create_batch_norm(y, *n, 1e-5)
             y = g.create_leaky_relu(y)
-            y = g.create_max_pool2d(y, [1, 2, 2, 1], [1, 2, 2, 1] if j == 0 else [1, 1, 1, 1], "SAME")
+            if j == 0 or pool5:
+                y = g.create_max_pool2d(y, [1, 2, 2, 1], [1, 2, 2, 1] if j == 0 else [1, 1, 1, 1], "SAME")
         g.set_out_node(y)
         return g
 
     ref = R.max_pool2d(x, [1, 2, 2, 1], [1, 1, 1, 1], "SAME")
     for j, (k, b, n) in enumerate(L):
         ref = R.leaky_relu(R.batch_norm(R.bias_add(R.conv2d(ref, k), b), *n, 1e-5))
-        ref = R.max_pool2d(ref, [1, 2, 2, 1], [1, 2, 2, 1] if j == 0 else [1, 1, 1, 1], "SAME")
+        if j == 0 or pool5:
+            ref = R.max_pool2d(ref, [1, 2, 2, 1], [1, 2, 2, 1] if j == 0 else [1, 1, 1, 1], "SAME")
     errs = {}
     for x3 in ("1", "0"):
         monkeypatch.setenv("DNN_HIP_X3", x3)
@@ -972,6 +978,7 @@ def test_x3_ktile_kernel_vs_oracle(monkeypatch, B):
         conv = [ln for ln in desc.splitlines() if ln.startswith("conv")]
         if x3 == "1":
             assert "mode=x3_ktile" in conv[0] and "+pool2x2s2" in conv[0] and "mode=x3_ktile" in conv[1], desc
+            assert ("+pool2x2s1" in conv[1]) == pool5 and desc.count("pool ") == 1, desc
         y = eng.run(x)
         errs[x3] = R.normwise_err(y, ref)
         if x3 == "1":

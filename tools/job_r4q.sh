@@ -9,4 +9,4 @@ grep "ktile chain" $O/pytest.log
 timeout -k 10 300 python -u tools/lat_ab.py --rounds 6 > $O/lat.log 2>&1 || { tail -20 $O/lat.log; exit 1; }
 grep "graph_device" $O/lat.log | grep -v "^{\"{" | cut -c1-700
 (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace -d $O/lt -o lt --output-format csv -- python3 $R/tools/lat_ab.py --rounds 1 --reps 100 > $O/lt.log 2>&1) || { tail -20 $O/lt.log; exit 1; }
-python tools/trace_timeline.py $(find $O/lt -name "*kernel_trace.csv") --len 11 --reps 100
+python tools/trace_timeline.py $(find $O/lt -name "*kernel_trace.csv") --len 10 --reps 100
