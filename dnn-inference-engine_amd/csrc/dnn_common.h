@@ -244,6 +244,10 @@ bool conv_x3_pool_supported(int OC, int C, int H, int W);  // an x3 conv of this
 long long x3_tiles(long long batch, int OH, int OW, int OC, int C, int K);
 // small-M x3 conv of the latency plans (gemm_x3_lat.h): raw partials [splits][M][N] of
 // x3_lat_splits(N, K) K slices into `part`, summed with the epilogue by launch_x3_combine
+// latency plans' 1x1 head on x3 split planes, K split inside the workgroup (gemm_x3_ktile.h)
+bool conv_x3_1x1_ktile_supported(int C, int OC, int H, int W);
+int launch_conv_x3_1x1_ktile(const unsigned short* in_split, const unsigned short* Bt, float* out, long long M, int N,
+                             int Npad, int K, int H, int W, int C, const EpiParams& epi, hipStream_t stream);
 // latency plans' mid layers: x3 with the K split inside the workgroup (gemm_x3_ktile.h), one
 // launch, no partials; deterministic, tolerance against the batch plans
 bool conv_x3_ktile_supported(long long batch, int C, int OC, int H, int W, int OH, int OW, int kh, int kw, int sh,

@@ -339,4 +339,108 @@ conv3x3_x3_ktile_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __res
 }
 #undef KT_STAMP
 
+// The 1x1 form (latency plans' conv8: 13x13x1024 -> 125 on conv7's split planes): 16 pixel rows
+// x 32 columns per workgroup, KW groups of one wave, group k taking chunks k CPK .. k CPK + CPK -
+// 1; every chunk's 16 rows staged by LDS-DMA at once, the groups' folded sums added in group
+// order by group 0, fp32 epilogue into out [M][N] (columns past N, the packing's padding, not
+// stored).  At one frame: 11 x 4 = 44 workgroups with an 8-step chain each, where the batch
+// kernel's 32 x 128 tiles over all of K were 6 (21 us) and the fp32 split-K GEMM 11.5 us.
+template <int KW, int CPK, int FL = -1>
+__global__ void __launch_bounds__(64 * KW, 1)
+conv1x1_x3_ktile_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __restrict__ Bt, float* __restrict__ out,
+                        int M, int N, int K, EpiParams epi, int tilesM, X3Geom g, unsigned in_bytes,
+                        unsigned b_bytes) {
+  constexpr int NW = KW, LP = 224, PU = LP / 16, BM = 16, NCH = KW * CPK;
+  constexpr int NPC = (BM * PU + 63) / 64;        // 1-KiB DMA pieces per chunk (16 rows: 4)
+  constexpr int BUFB = NPC * 1024;
+  constexpr int NPW = (NCH * NPC + NW - 1) / NW;  // pieces per wave, all chunks
+  constexpr int RED = (KW - 1) * 2 * 1024;
+  constexpr int SM = NCH * BUFB > RED ? NCH * BUFB : RED;
+  static_assert(SM <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[SM];
+
+  const int lane = threadIdx.x & 63;
+  const int eflags = FL < 0 ? epi.flags : FL;
+  const int kg = wave_uniform(threadIdx.x >> 6);
+  const int tile = xcd_tile(blockIdx.x, gridDim.x);
+  const int tn = tile / tilesM, tm = tile - tn * tilesM;
+  const int m0 = tm * BM, n0 = tn * 32;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int nk = K / 32, Wp = g.W + 2, HWo = g.H * g.W;
+  auto padded = [&](int m) {
+    m = m < M ? m : M - 1;
+    const int b = m / HWo, r = m - b * HWo, oy = r / g.W, ox = r - oy * g.W;
+    return (b * (g.H + 2) + oy + 1) * Wp + ox + 1;
+  };
+
+  const unsigned rowB = 6u * (unsigned)g.C;
+  const auto rsA = __builtin_amdgcn_make_buffer_rsrc((void*)in, 0, (int)in_bytes, 0x00020000);
+#pragma unroll
+  for (int k = 0; k < NPW; ++k) {
+    int q = kg + NW * k;
+    q = q < NCH * NPC ? q : NCH * NPC - 1;
+    const int c = q / NPC, pq = q - c * NPC;
+    const unsigned U = 64u * (unsigned)pq + (unsigned)lane;
+    unsigned r = U / PU;
+    const unsigned u = U - r * PU;
+    r = r < (unsigned)BM ? r : (unsigned)BM - 1;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (__attribute__((address_space(3))) void*)(smem + c * BUFB + 1024 * pq),
+                                             16, (int)((unsigned)padded(m0 + (int)r) * rowB + 16u * u),
+                                             (int)(c * 192), 0, 0);
+  }
+  const unsigned bvo = (unsigned)((n0 / 16) * nk * 3072 + lane * 16);
+  const int bjs = nk * 3072, s0 = kg * CPK;
+  const auto rsB = __builtin_amdgcn_make_buffer_rsrc((void*)Bt, 0, (int)b_bytes, 0x00020000);
+  bf16x8 bq[CPK][3][2];  // every step of the group's chunks in flight at once (CPK <= 8)
+#pragma unroll
+  for (int c = 0; c < CPK; ++c)
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        bq[c][p][j] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rsB, bvo, (s0 + c) * 3072 + p * 1024 + j * bjs, 0));
+  const X3EpiCol ecp[2] = {x3_epi_col(epi, eflags, n0 + fr < N ? n0 + fr : N - 1),
+                           x3_epi_col(epi, eflags, n0 + 16 + fr < N ? n0 + 16 + fr : N - 1)};
+  f32x4 acc[2], accc[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) acc[j] = accc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+#pragma unroll
+  for (int c = 0; c < CPK; ++c) {
+    const unsigned char* P = smem + (s0 + c) * BUFB + fr * LP + 16 * fq;
+    bf16x8 af[3];
+#pragma unroll
+    for (int p = 0; p < 3; ++p) af[p] = *reinterpret_cast<const bf16x8*>(P + 64 * p);
+#pragma unroll
+    for (int jb = 0; jb < 2; ++jb) x3_step<true>(acc[jb], accc[jb], af, bq[c], jb);
+  }
+#pragma unroll
+  for (int jb = 0; jb < 2; ++jb) acc[jb] = acc[jb] + accc[jb];  // (x3_fold)
+  wait_lgkm0();
+  __syncthreads();
+  f32x4* const red = reinterpret_cast<f32x4*>(smem);
+  if (kg > 0) {
+#pragma unroll
+    for (int jb = 0; jb < 2; ++jb) red[((kg - 1) * 2 + jb) * 64 + lane] = acc[jb];
+  }
+  __syncthreads();
+  if (kg > 0) return;
+#pragma unroll
+  for (int k = 1; k < KW; ++k)
+#pragma unroll
+    for (int jb = 0; jb < 2; ++jb) acc[jb] = acc[jb] + red[((k - 1) * 2 + jb) * 64 + lane];
+#pragma unroll
+  for (int jb = 0; jb < 2; ++jb) {
+    const int n = n0 + 16 * jb + fr;
+    if (n >= N) continue;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = m0 + 4 * fq + r;
+      if (m < M)
+        out[(size_t)m * N + n] = apply_epilogue_t<FL>(acc[jb][r], ecp[jb].pb, ecp[jb].pm, ecp[jb].ps, ecp[jb].pg, epi.flags);
+    }
+  }
+}
+
 }  // namespace dnnhip

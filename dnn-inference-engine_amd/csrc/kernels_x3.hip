@@ -663,6 +663,43 @@ int launch_conv_x3_ktile(const bf16_bits* in_split, const bf16_bits* Bt, float* 
   return check_x3("conv_x3_ktile");
 }
 
+// 1x1 form (latency plans' conv8): 16 rows x 32 columns, 4 K groups of one wave
+bool conv_x3_1x1_ktile_supported(int C, int OC, int H, int W) {
+  const int nch = C / 32;
+  return C % 32 == 0 && nch % 4 == 0 && nch / 4 <= 8 && OC >= 1 && H >= 1 && W >= 1 && x3_enabled() &&
+         !getenv_flag_off("DNN_HIP_X3_1X1");
+}
+
+int launch_conv_x3_1x1_ktile(const bf16_bits* in_split, const bf16_bits* Bt, float* out, long long M, int N, int Npad,
+                             int K, int H, int W, int C, const EpiParams& epi, hipStream_t stream) {
+  if (M == 0 || N == 0) return 0;
+  const long long per_img = (long long)H * W, nimg = M / per_img;
+  const long long in_bytes = (long long)x3_act_bytes(nimg, H, W, C);
+  const long long b_bytes = (long long)(Npad / 16) * (K / 32) * 3072;
+  const int cpk = K / 128;
+  if (M % per_img != 0 || K != C || !conv_x3_1x1_ktile_supported(C, N, H, W) || Npad % 32 != 0 || Npad < N ||
+      in_bytes >= 0x80000000LL || b_bytes >= 0x80000000LL || M > 0x7fffffffLL ||
+      (cpk != 1 && cpk != 2 && cpk != 4 && cpk != 8)) {
+    set_error("conv_x3_1x1_ktile: unsupported shape M=%lld N=%d K=%d %dx%dx%d", M, N, K, H, W, C);
+    return -2;
+  }
+  const int tilesM = (int)((M + 15) / 16), tilesN = Npad / 32;
+  const X3Geom xg{H, W, C, 0, 1, 0, 0};
+#define X3K1(CPK_)                                                                                                  \
+  hipLaunchKernelGGL((conv1x1_x3_ktile_kernel<4, CPK_>), dim3((unsigned)((long long)tilesM * tilesN)), dim3(256), 0, \
+                     stream, in_split, Bt, out, (int)M, N, K, epi, tilesM, xg, (unsigned)in_bytes, (unsigned)b_bytes)
+  if (cpk == 8)
+    X3K1(8);
+  else if (cpk == 4)
+    X3K1(4);
+  else if (cpk == 2)
+    X3K1(2);
+  else
+    X3K1(1);
+#undef X3K1
+  return check_x3("conv_x3_1x1_ktile");
+}
+
 int launch_conv_x3_lat(const bf16_bits* in_split, const bf16_bits* Bt, float* part, long long M, int N, int Npad,
                        int K, int H, int W, int C, int splits, hipStream_t stream) {
   if (M == 0 || N == 0) return 0;

@@ -457,11 +457,14 @@ int dnn_plan_add_conv(dnn_plan* p, int kh, int kw, int od, int stride_h, int str
   // plans of any size run the same arithmetic).  Latency plans keep the fp32 GEMM split over the
   // chip where this kernel's 32 x 128 tiles would not fill it (one frame's 169 rows are 6 tiles:
   // 21 us against 14)
+  // (latency plans whose frame leaves those tiles few: the K-split 1x1 form, 16 x 32 tiles)
   const long long t1x1 = ((long long)p->batch * L.OH * L.OW + 31) / 32 * ((od + 127) / 128);
-  if (!p->fp16 && !(p->latency && fused_splitk(p) && t1x1 < 256) && L.mode == MODE_DIRECT_A && !p->layers.empty() &&
-      p->layers.back().type == 0 &&
-      p->layers.back().mode == MODE_X3 && conv_x3_1x1_supported(L.C, od, L.H, L.W)) {
+  const bool lat1x1 = p->latency && fused_splitk(p) && t1x1 < 256;
+  if (!p->fp16 && L.mode == MODE_DIRECT_A && !p->layers.empty() && p->layers.back().type == 0 &&
+      p->layers.back().mode == MODE_X3 &&
+      (lat1x1 ? conv_x3_1x1_ktile_supported(L.C, od, L.H, L.W) : conv_x3_1x1_supported(L.C, od, L.H, L.W))) {
     L.mode = MODE_X3_1X1;
+    L.x3k = lat1x1;
     p->layers.back().out_padded = true;
   }
   if (x3_cand) {
@@ -880,9 +883,12 @@ int dnn_plan_run(dnn_plan* p, int n, const float* d_in, float* d_out, void* stre
           break;
         }
         case MODE_X3_1X1:
-          rc = launch_conv_x3_1x1(reinterpret_cast<const unsigned short*>(cur),
-                                  reinterpret_cast<const unsigned short*>(wt), dst, Mc, L.OC, L.Npad, L.K, L.H, L.W,
-                                  L.C, epi, s);
+          rc = L.x3k ? launch_conv_x3_1x1_ktile(reinterpret_cast<const unsigned short*>(cur),
+                                                reinterpret_cast<const unsigned short*>(wt), dst, Mc, L.OC, L.Npad,
+                                                L.K, L.H, L.W, L.C, epi, s)
+                     : launch_conv_x3_1x1(reinterpret_cast<const unsigned short*>(cur),
+                                          reinterpret_cast<const unsigned short*>(wt), dst, Mc, L.OC, L.Npad, L.K, L.H,
+                                          L.W, L.C, epi, s);
           break;
         case MODE_X3:
           if (L.x3k) {
