@@ -238,7 +238,7 @@ int launch_pack_weights_x3(const float* w, unsigned short* out, int K, int N, in
 int x3_splits(int N, int K);  // split-K of an x3 batch-plan layer: a function of (N, K) only
 int launch_conv_x3(const unsigned short* in_split, const unsigned short* Bt, float* out, unsigned short* out_split,
                    long long M, int N, int Npad, int K, int H, int W, int C, const EpiParams& epi, hipStream_t stream,
-                   int splits = 1, int pool = 0);
+                   int splits = 1, int pool = 0, bool lat = false);  // lat: latency-plan tile shapes allowed
 bool conv_x3_pool_supported(int OC, int C, int H, int W);  // an x3 conv of this size can fuse a 2x2/s2 pool
 // x3 workgroups of a layer (batch-1 latency plans take x3 only where they fill half the chip)
 long long x3_tiles(long long batch, int OH, int OW, int OC, int C, int K);

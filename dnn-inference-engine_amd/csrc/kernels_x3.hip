@@ -415,7 +415,7 @@ int x3_splits(int N, int K) { return (N % 256 == 0 && N > 256 && N <= 512 && (K 
 
 int launch_conv_x3(const bf16_bits* in_split, const bf16_bits* Bt, float* out, bf16_bits* out_split, long long M,
                    int N, int Npad, int K, int H, int W, int C, const EpiParams& epi, hipStream_t stream, int splits,
-                   int pool) {
+                   int pool, bool lat) {
   if (M == 0 || N == 0) return 0;
   // pool: M counts GEMM rows, 4 per pooled pixel
   const int PH = pool ? (H + 1) / 2 : 0, PW = pool ? (W + 1) / 2 : 0;
@@ -445,7 +445,15 @@ int launch_conv_x3(const bf16_bits* in_split, const bf16_bits* Bt, float* out, b
     // launch, experiments): one tile per workgroup (conv3x3_x3_c16_kernel); default: persistent
     // (conv3x3_x3_c16p_kernel, the last K step on 16x16x16; measured at batch 64: conv1 0.164 ->
     // 0.152 ms, forward -14 us), same bits up to the K = 16 step's summation
-    if (getenv_flag_off("DNN_HIP_X3_C16P") || !pool) {  // (the persistent kernel: the pooled form, conv1)
+    // latency plans (one frame: 104 tiles of 16 x 26): 4 x 26 tiles, 4 waves of 2 row blocks, 416
+    // tiles; tap 8 on the 32-wide MFMA (the batch plans' persistent kernel puts it on the 16-wide
+    // one: not the same bits, so the batch plans never take this shape)
+    const bool small = lat && blocks < 2LL * device_cu_count();
+    if (small && pool) {
+      const int ty4 = (H + 3) / 4;
+      hipLaunchKernelGGL((conv3x3_x3_c16_kernel<4, 26, 4, 2, true>), dim3((unsigned)(nimg * tilesX * ty4)), dim3(256), 0,
+                         stream, in32p, Bt, out, out_split, N, epi, tilesX, ty4, xg, (unsigned)in32);
+    } else if (getenv_flag_off("DNN_HIP_X3_C16P") || !pool) {  // (the persistent kernel: the pooled form, conv1)
       if (pool)
         hipLaunchKernelGGL((conv3x3_x3_c16_kernel<16, 26, 4, 7, true>), dim3((unsigned)blocks), dim3(256), 0, stream,
                            in32p, Bt, out, out_split, N, epi, tilesX, tilesY, xg, (unsigned)in32);

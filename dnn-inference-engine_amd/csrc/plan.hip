@@ -433,12 +433,12 @@ int dnn_plan_add_conv(dnn_plan* p, int kh, int kw, int od, int stride_h, int str
   bool x3_cand = false, x3_lat = false, x3_k = false;
   if (!p->fp16 && L.mode == MODE_IMPLICIT && !p->layers.empty()) {
     const bool batch_ok = conv_x3_supported(L.C, od, L.H, L.W, L.OH, L.OW, kh, kw, stride_h, stride_w, L.pt, L.pl);
-    // (the N = 64 / 128 tile kernels take small tiles at small batches: batch_ok is enough; the
-    // 16-channel kernel's 16 x 26 tiles are 104 at one frame: 11.7 us against the fp32 patch
-    // conv's 10.0, which writes conv2's split planes as well)
+    // (the narrow kernels take small tiles in latency plans: batch_ok is enough.  conv1 at one
+    // frame: the 16-channel kernel's 4 x 26 tiles 10.6 us, its 16 x 26 ones 11.7, the fp32 patch
+    // conv 13.8 (HIP events, same box))
     const int xk = conv_x3_kind(od, L.C);
     if (p->latency && fused_splitk(p) &&
-        !(batch_ok && (xk == 1 || xk == 2 || x3_tiles(p->batch, L.OH, L.OW, od, L.C, L.K) >= 128))) {
+        !(batch_ok && (xk > 0 || x3_tiles(p->batch, L.OH, L.OW, od, L.C, L.K) >= 128))) {
       // conv4 / conv5 of a frame: the K split inside the workgroup (one launch, no partials);
       // conv6 / conv7: the small-M kernel's K slices + combine
       x3_k = conv_x3_ktile_supported(p->batch, L.C, od, L.H, L.W, L.OH, L.OW, kh, kw, stride_h, stride_w, L.pt,
@@ -912,7 +912,7 @@ int dnn_plan_run(dnn_plan* p, int n, const float* d_in, float* d_out, void* stre
             rc = launch_conv_x3(reinterpret_cast<const unsigned short*>(cur),
                                 reinterpret_cast<const unsigned short*>(wt), dsplit ? nullptr : dst, dsplit,
                                 L.pool ? 4LL * n * L.PH * L.PW : Mc, L.OC, L.Npad, L.K, L.H, L.W, L.C, epi, s, 1,
-                                L.pool ? 1 : 0);
+                                L.pool ? 1 : 0, p->latency);
           }
           break;
         default:
