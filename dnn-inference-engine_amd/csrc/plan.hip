@@ -912,7 +912,7 @@ int dnn_plan_run(dnn_plan* p, int n, const float* d_in, float* d_out, void* stre
             rc = launch_conv_x3(reinterpret_cast<const unsigned short*>(cur),
                                 reinterpret_cast<const unsigned short*>(wt), dsplit ? nullptr : dst, dsplit,
                                 L.pool ? 4LL * n * L.PH * L.PW : Mc, L.OC, L.Npad, L.K, L.H, L.W, L.C, epi, s, 1,
-                                L.pool ? 1 : 0, p->latency);
+                                L.pool ? 1 : 0, p->latency && fused_splitk(p));
           }
           break;
         default:
