@@ -611,6 +611,8 @@ static int x3_ktile_shape(int C, int OC, int H, int W, int pool) {
   if (OC % 64 != 0 || !x3_enabled()) return -1;
   if (C == 128 && W > 13 && W <= 26 && (pool == 0 || (pool == 1 && H % 2 == 0 && W % 2 == 0))) return 0;
   if (C == 256 && W <= 13 && pool != 1) return 1;
+  if (C == 64 && OC == 128 && W > 26 && W <= 52 && (pool == 0 || (pool == 1 && H % 2 == 0 && W % 2 == 0)))
+    return 2;  // conv3
   return -1;
 }
 
@@ -639,7 +641,7 @@ int launch_conv_x3_ktile(const bf16_bits* in_split, const bf16_bits* Bt, float* 
     set_error("conv_x3_ktile: unsupported shape M=%lld N=%d K=%d %dx%dx%d pool=%d", M, N, K, H, W, C, pool);
     return -2;
   }
-  const int TH = shape == 0 ? 2 : 1, TW = shape == 0 ? 26 : 13;
+  const int TH = shape == 1 ? 1 : 2, TW = shape == 1 ? 13 : 26;
   const int tilesX = (W + TW - 1) / TW, tilesY = (H + TH - 1) / TH, tilesN = N / 32;
   const long long blocks = nimg * tilesX * tilesY * tilesN;
   if (blocks > 0x7fffffffLL) {
@@ -648,12 +650,19 @@ int launch_conv_x3_ktile(const bf16_bits* in_split, const bf16_bits* Bt, float* 
   }
   const X3Geom xg{H, W, C, out_split ? 1 : 0, 1, PH, PW};
   const bool yolo = epi.flags == X3_YOLO_FL;
-#define X3K(TH_, TW_, TM_, CPK_, POOL_, FL_, PL1_)                                                                 \
-  hipLaunchKernelGGL((conv3x3_x3_ktile_kernel<TH_, TW_, 1, 1, TM_, 4, CPK_, POOL_, FL_, 3, PL1_>),                 \
-                     dim3((unsigned)blocks), dim3(256), 0, stream, in_split, Bt, out, out_split, N, K, epi, tilesX, \
-                     tilesY, tilesN, xg, (unsigned)in_bytes, (unsigned)b_bytes)
+#define X3KW(TH_, TW_, WM_, TM_, KW_, CPK_, POOL_, FL_, PL1_)                                                       \
+  hipLaunchKernelGGL((conv3x3_x3_ktile_kernel<TH_, TW_, WM_, 1, TM_, KW_, CPK_, POOL_, FL_, 3, PL1_>),                \
+                     dim3((unsigned)blocks), dim3(64 * WM_ * KW_), 0, stream, in_split, Bt, out, out_split, N, K, epi,  \
+                     tilesX, tilesY, tilesN, xg, (unsigned)in_bytes, (unsigned)b_bytes)
+#define X3K(TH_, TW_, TM_, CPK_, POOL_, FL_, PL1_) X3KW(TH_, TW_, 1, TM_, 4, CPK_, POOL_, FL_, PL1_)
   // (a 5-step weight ring measured 1 % slower than 3 in the earlier 8-wave form)
-  if (shape == 0 && p2 && yolo)
+  if (shape == 2 && p2 && yolo)  // (conv3: 2 chunks = 2 K groups of 2 x 2 row blocks, 4 waves)
+    X3KW(2, 26, 2, 2, 2, 1, true, X3_YOLO_FL, false);
+  else if (shape == 2 && p2)
+    X3KW(2, 26, 2, 2, 2, 1, true, -1, false);
+  else if (shape == 2)
+    X3KW(2, 26, 2, 2, 2, 1, false, -1, false);
+  else if (shape == 0 && p2 && yolo)
     X3K(2, 26, 4, 1, true, X3_YOLO_FL, false);
   else if (shape == 0 && p2)
     X3K(2, 26, 4, 1, true, -1, false);
@@ -668,6 +677,7 @@ int launch_conv_x3_ktile(const bf16_bits* in_split, const bf16_bits* Bt, float* 
   else
     X3K(1, 13, 1, 2, false, -1, false);
 #undef X3K
+#undef X3KW
   return check_x3("conv_x3_ktile");
 }
 

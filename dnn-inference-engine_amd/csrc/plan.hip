@@ -437,17 +437,20 @@ int dnn_plan_add_conv(dnn_plan* p, int kh, int kw, int od, int stride_h, int str
     // frame: the 16-channel kernel's 4 x 26 tiles 10.6 us, its 16 x 26 ones 11.7, the fp32 patch
     // conv 13.8 (HIP events, same box))
     const int xk = conv_x3_kind(od, L.C);
-    if (p->latency && fused_splitk(p) &&
-        !(batch_ok && (xk > 0 || x3_tiles(p->batch, L.OH, L.OW, od, L.C, L.K) >= 128))) {
-      // conv4 / conv5 of a frame: the K split inside the workgroup (one launch, no partials);
-      // conv6 / conv7: the small-M kernel's K slices + combine
-      x3_k = conv_x3_ktile_supported(p->batch, L.C, od, L.H, L.W, L.OH, L.OW, kh, kw, stride_h, stride_w, L.pt,
-                                     L.pl, 0);
-      x3_lat = !x3_k &&
-               conv_x3_lat_supported(p->batch, L.C, od, L.H, L.W, L.OH, L.OW, kh, kw, stride_h, stride_w, L.pt,
+    const bool lat = p->latency && fused_splitk(p);
+    // latency plans: conv3-conv5 of a frame with the K split inside the workgroup (one launch, no
+    // partials), first; conv1 / conv2 on the narrow kernels' small tiles; conv6 / conv7 on the
+    // small-M kernel's K slices + combine
+    const bool fills = batch_ok && x3_tiles(p->batch, L.OH, L.OW, od, L.C, L.K) >= 128;  // the batch tiles fill the chip
+    x3_k = lat && !fills &&
+           conv_x3_ktile_supported(p->batch, L.C, od, L.H, L.W, L.OH, L.OW, kh, kw, stride_h, stride_w, L.pt, L.pl, 0);
+    if (x3_k) {
+      x3_cand = true;
+    } else if (lat && !(batch_ok && (xk > 0 || x3_tiles(p->batch, L.OH, L.OW, od, L.C, L.K) >= 128))) {
+      x3_lat = conv_x3_lat_supported(p->batch, L.C, od, L.H, L.W, L.OH, L.OW, kh, kw, stride_h, stride_w, L.pt,
                                      L.pl) &&
                x3_lat_splits(od, L.K) >= 2;
-      x3_cand = x3_lat || x3_k;
+      x3_cand = x3_lat;
     } else {
       x3_cand = batch_ok;
     }

@@ -209,13 +209,13 @@ def test_plan_x3_structure_host_only(monkeypatch):
     assert "splitK=2 x3-combine" in conv[5] and sum("splitK" in ln for ln in lines) == 1
     assert all("+pool2x2s2" in conv[i] for i in (1, 2, 3, 4))  # pools fused into the x3 convs
     assert sum(ln.startswith("pool") for ln in lines) == 1  # pool5 (s1, combines conv5's slices)
-    # latency plans (one frame): conv1-conv3 on the narrow x3 kernels (small tiles), conv4 / conv5
+    # latency plans (one frame): conv1 / conv2 on the narrow x3 kernels (small tiles), conv3-conv5
     # and conv8 on the K-split x3 kernels (pool5 fused into conv5), conv6 / conv7 on the small-M
     # x3 kernel; conv0 stays on its fp32 direct kernel
     latl = _describe_yolo(1, True)
     lat = [ln for ln in latl if ln.startswith("conv")]
-    assert [i for i, ln in enumerate(lat) if "mode=patch_x3" in ln] == [1, 2, 3]
-    assert [i for i, ln in enumerate(lat) if "mode=x3_ktile" in ln] == [4, 5, 8]
+    assert [i for i, ln in enumerate(lat) if "mode=patch_x3" in ln] == [1, 2]
+    assert [i for i, ln in enumerate(lat) if "mode=x3_ktile" in ln] == [3, 4, 5, 8]
     assert [i for i, ln in enumerate(lat) if "mode=x3_lat" in ln] == [6, 7]
     assert "+pool2x2s1" in lat[5] and not any(ln.startswith("pool") for ln in latl)
     # DNN_HIP_X3_TILE=0: conv2/conv3 back on the fp32 MFMA, conv3's pooled epilogue splits;
@@ -332,16 +332,16 @@ def _describe_yolo(batch, latency, env=None):
 
 
 def test_latency_plan_layout():
-    """dnn_plan_set_latency_mode: at batch 1 conv1-conv3 on the narrow x3 kernels (small tiles
-    chosen at launch), conv4 / conv5 on the x3 kernel with the K split inside the workgroup (conv4
-    with its 2x2/s2 pool, conv5 with pool5), conv6/conv7 on the small-M x3 kernel, conv8 on the
+    """dnn_plan_set_latency_mode: at batch 1 conv1 / conv2 on the narrow x3 kernels (small tiles
+    chosen at launch), conv3-conv5 on the x3 kernel with the K split inside the workgroup (conv3 /
+    conv4 with their 2x2/s2 pools, conv5 with pool5), conv6/conv7 on the small-M x3 kernel, conv8 on the
     1x1 K-split kernel, conv0 on its direct kernel; batch plans are unchanged."""
     lat = _describe_yolo(1, True)
     base = _describe_yolo(1, False)
     assert all(l.endswith(" latency") for l in lat if l.startswith("conv"))
     conv = [l for l in lat if l.startswith("conv")]
-    assert "mode=direct" in conv[0] and all("mode=patch_x3" in conv[i] for i in (1, 2, 3))
-    for i in (4, 5):
+    assert "mode=direct" in conv[0] and all("mode=patch_x3" in conv[i] for i in (1, 2))
+    for i in (3, 4, 5):
         assert "mode=x3_ktile" in conv[i] and " splitK=" not in conv[i], conv[i]
     assert "+pool2x2s2" in conv[4] and "+pool2x2s1" in conv[5]
     # conv6 / conv7: the small-M x3 kernel in 16 K slices; conv8 the 1x1 K-split kernel

@@ -902,8 +902,8 @@ def test_latency_split_combine_vs_oracle(monkeypatch, case):
 
 @pytest.mark.parametrize("frame", [0, 1, 2, 3])
 def test_yolo_latency_plan_vs_reference_golden(yolo_weights, golden_frames, frame, latency_b1_engine=[]):
-    """BASELINE config 2 in latency mode: conv1 on the 16-channel x3 kernel's 4 x 26 tiles, conv2 /
-    conv3 on the x3 tile kernel's 2 x 26 tiles, conv4 / conv5 on the x3 kernel with
+    """BASELINE config 2 in latency mode: conv1 on the 16-channel x3 kernel's 4 x 26 tiles, conv2
+    on the x3 tile kernel's 2 x 26 tiles, conv3 / conv4 / conv5 on the x3 kernel with
     the K split inside the workgroup (pool5 fused into conv5), conv6 / conv7 on the small-M x3
     kernel, conv8 on the 1x1 form of the K-split kernel; within the net tolerance of the reference goldens
     (not bit-equal to the batch plan's rows)."""
@@ -916,7 +916,7 @@ def test_yolo_latency_plan_vs_reference_golden(yolo_weights, golden_frames, fram
     assert "mode=x3_ktile" in conv[4] and "mode=x3_ktile" in conv[5] and "+pool2x2s1" in conv[5], desc
     assert "mode=x3_ktile" in conv[8], desc  # conv8: the 1x1 K-split x3 kernel
     assert "mode=x3_lat" in conv[6] and "mode=x3_lat" in conv[7], desc  # conv6 / conv7: small-M x3
-    assert all("mode=patch_x3" in conv[i] for i in (1, 2, 3)), desc  # conv1-conv3: x3, small tiles
+    assert all("mode=patch_x3" in conv[i] for i in (1, 2)) and "mode=x3_ktile" in conv[3], desc  # conv1-conv3: x3
     y = eng.run(synth.frame(frame))
     assert R.normwise_err(y, golden_frames[frame]) < NET_TOL
 
@@ -999,6 +999,46 @@ def test_x3_ktile_kernel_vs_oracle(monkeypatch, case):
     print("ktile chain errs", errs)
     assert errs["1"] < 3 * LAYER_TOL and errs["0"] < 3 * LAYER_TOL, errs
     assert errs["1"] <= 1.25 * errs["0"], errs
+
+
+@pytest.mark.parametrize("B", [1, 3])
+def test_x3_ktile_conv3_shape_vs_oracle(B):
+    """The K-split x3 kernel's conv3 shape (latency plans: 52x52x64 -> 128 + 2x2/s2 pool, two
+    26-wide tile columns, 2 K groups of 2 x 2 row blocks): within the fp32 tolerance of the
+    float64 oracle, repeat runs identical, a 3-frame run's rows equal to one-frame runs."""
+    rng = np.random.default_rng(5 + B)
+    x = rng.standard_normal((B, 52, 52, 64)).astype(np.float32)
+    k = (rng.standard_normal((3, 3, 64, 128)) * np.sqrt(2.0 / 576)).astype(np.float32)
+    b = rng.standard_normal(128).astype(np.float32) * 0.1
+    gam = rng.uniform(0.5, 1.5, 128).astype(np.float32)
+    gam[::5] *= -1
+    n = (rng.standard_normal(128).astype(np.float32) * 0.1, rng.uniform(0.5, 1.5, 128).astype(np.float32), gam)
+
+    def graph(shape):
+        g = dnn_hip.DnnGraphBuilder()
+        y = g.create_input(list(shape))
+        y = g.create_max_pool2d(y, [1, 2, 2, 1], [1, 1, 1, 1], "SAME")
+        y = g.create_conv2d(y, k, [1, 1, 1, 1], "SAME")
+        y = g.create_bias_add(y, b)
+        y = g.create_batch_norm(y, *n, 1e-5)
+        y = g.create_leaky_relu(y)
+        y = g.create_max_pool2d(y, [1, 2, 2, 1], [1, 2, 2, 1], "SAME")
+        g.set_out_node(y)
+        return g
+
+    ref = R.max_pool2d(x, [1, 2, 2, 1], [1, 1, 1, 1], "SAME")
+    ref = R.leaky_relu(R.batch_norm(R.bias_add(R.conv2d(ref, k), b), *n, 1e-5))
+    ref = R.max_pool2d(ref, [1, 2, 2, 1], [1, 2, 2, 1], "SAME")
+    eng = dnn_hip.DnnInferenceEngine(graph(x.shape), False, latency=True)
+    conv = [ln for ln in eng.plan().describe().splitlines() if ln.startswith("conv")]
+    assert "mode=x3_ktile" in conv[0] and "+pool2x2s2" in conv[0], conv
+    y = eng.run(x)
+    assert np.array_equal(eng.run(x), y)
+    assert R.normwise_err(y, ref) < LAYER_TOL
+    if B > 1:
+        one = dnn_hip.DnnInferenceEngine(graph((1,) + x.shape[1:]), False, latency=True)
+        for f in range(B):
+            assert np.array_equal(one.run(x[f:f + 1]), y[f:f + 1]), f
 
 
 X3_LAT_CASES = [

@@ -5,7 +5,7 @@ O=$R/gpurun_out/r4t; mkdir -p $O
 timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "x3_latency_kernel" > $O/pytest1.log 2>&1; rc=$?
 tail -2 $O/pytest1.log
 [ $rc -eq 0 ] || { grep -E "FAILED|Error|assert" $O/pytest1.log | head -20; exit 1; }
-timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "ktile or latency or x3_lat or tile or small or golden" > $O/pytest.log 2>&1; rc=$?
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "ktile or latency or x3_lat or tile or small or golden or conv3_shape" > $O/pytest.log 2>&1; rc=$?
 tail -2 $O/pytest.log
 [ $rc -eq 0 ] || { grep -E "FAILED|Error|assert" $O/pytest.log | head -20; exit 1; }
 timeout -k 10 300 python -u tools/lat_ab.py --rounds 6  > $O/lat.log 2>&1 || { tail -20 $O/lat.log; exit 1; }
