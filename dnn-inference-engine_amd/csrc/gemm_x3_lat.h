@@ -23,6 +23,15 @@
 
 namespace dnnhip {
 
+#if (X3DIAG & 512) != 0  // diagnostic builds: per workgroup s_memrealtime at start, patch landed, MFMAs done, end
+constexpr int LAT_DIAG_WGS = 1024;
+__device__ unsigned long long lat_diag_stamps[LAT_DIAG_WGS * 4];
+#define LAT_STAMP(k) \
+  if (threadIdx.x == 0 && blockIdx.x < LAT_DIAG_WGS) lat_diag_stamps[4 * blockIdx.x + (k)] = __builtin_amdgcn_s_memrealtime();
+#else
+#define LAT_STAMP(k)
+#endif
+
 template <int NCP, int CPW, int NPR, int NB = 3, int LP = 224>
 __global__ void __launch_bounds__(512, 1)
 conv3x3_x3_lat_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __restrict__ Bt, float* __restrict__ part,
@@ -38,6 +47,7 @@ conv3x3_x3_lat_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __restr
   static_assert(SMEM <= 160 * 1024, "LDS");
   constexpr int LPB = (3 * NJ + TMW - 1) / TMW;  // next-tap weight loads issued per row block
   __shared__ __attribute__((aligned(1024))) unsigned char smem[SMEM];
+  LAT_STAMP(0)
 
   const int lane = threadIdx.x & 63;
   const int wid = wave_uniform(threadIdx.x >> 6);
@@ -110,6 +120,7 @@ conv3x3_x3_lat_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __restr
     }
   vm_wait<0>();
   __syncthreads();
+  LAT_STAMP(1)
 
   // the last row group's surplus block (RG TMW > 11) is skipped (a uniform branch)
   const bool tail = TMW * RG > TM && rg == RG - 1;
@@ -145,6 +156,7 @@ conv3x3_x3_lat_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __restr
     }
   }
   vm_wait<0>();
+  LAT_STAMP(2)
 
 #pragma unroll
   for (int i = 0; i < TMW; ++i)
@@ -175,7 +187,11 @@ conv3x3_x3_lat_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __restr
       }
   }
 
-  // raw partial of slice `split`: part[split][m][n] (x3_combine_kernel sums and runs the epilogue)
+  // raw partial of slice `split`: part[split][m][n] (x3_combine_kernel sums and runs the epilogue).
+  // (Round 4, X3DIAG 512 at one frame, conv7: patch 4.4 us, MFMA loop 8.5-9.3 us for wave 0, the
+  // rest of the waves' loops + these stores 4.7 us -- two waves per SIMD make a SIMD's MFMA work
+  // ~10 us, and a frame's x3 conv7 is ~9 us of MFMA on all 1,024 SIMDs at 2 GHz; staging these
+  // stores through LDS as whole 16-B row pieces measured the same.)
   float* dst = part + (size_t)split * M * N;
 #pragma unroll
   for (int i = 0; i < TMW; ++i) {
@@ -190,6 +206,8 @@ conv3x3_x3_lat_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __restr
       }
     }
   }
+  LAT_STAMP(3)
 }
+#undef LAT_STAMP
 
 }  // namespace dnnhip

@@ -831,3 +831,15 @@ extern "C" __attribute__((visibility("default"))) int dnn_ktile_diag_stamps(unsi
              : -1;
 }
 #endif
+
+#if (X3DIAG & 512) != 0
+// diagnostic builds (X3DIAG bit 512): conv3x3_x3_lat_kernel's per-workgroup s_memrealtime stamps
+// [start, patch landed, MFMAs done, end] of its last launch copied to host[0 .. 4n)
+extern "C" __attribute__((visibility("default"))) int dnn_lat_diag_stamps(unsigned long long* host, int n) {
+  if (n < 0 || n > dnnhip::LAT_DIAG_WGS) return -2;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(dnnhip::lat_diag_stamps), (size_t)n * 4 * sizeof(unsigned long long), 0,
+                             hipMemcpyDeviceToHost) == hipSuccess
+             ? 0
+             : -1;
+}
+#endif

@@ -48,6 +48,29 @@ def ktile_stamps(lib):
     return out
 
 
+def lat_stamps(lib):
+    """X3DIAG bit 512 builds: conv3x3_x3_lat_kernel's per-workgroup s_memrealtime stamps of its last
+    launch (conv7): start skew, patch, MFMA and store phases (us)."""
+    fn = getattr(lib, "dnn_lat_diag_stamps", None)
+    if fn is None:
+        return None
+    fn.restype = ctypes.c_int
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    buf = (ctypes.c_ulonglong * (4 * 1024))()
+    if fn(buf, 1024) != 0:
+        return None
+    rows = [buf[4 * w:4 * w + 4] for w in range(1024) if buf[4 * w] and buf[4 * w + 3] >= buf[4 * w]]
+    if not rows:
+        return None
+    t0 = min(r[0] for r in rows)
+    med = lambda f: round(statistics.median(f(r) for r in rows) / 100.0, 2)  # noqa: E731
+    mx = lambda f: round(max(f(r) for r in rows) / 100.0, 2)  # noqa: E731
+    return {"workgroups": len(rows), "start_skew_max": mx(lambda r: r[0] - t0),
+            "patch": med(lambda r: r[1] - r[0]), "patch_max": mx(lambda r: r[1] - r[0]),
+            "mfma": med(lambda r: r[2] - r[1]), "mfma_max": mx(lambda r: r[2] - r[1]),
+            "store": med(lambda r: r[3] - r[2]), "span": mx(lambda r: r[3] - t0)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--env", action="append", default=[], help="VAR=v1;v2;... (arms; an empty value unsets)")
@@ -119,6 +142,9 @@ def main():
             kt = ktile_stamps(p.lib)
             if kt:
                 d["ktile"] = kt
+            lt = lat_stamps(p.lib)
+            if lt:
+                d["lat"] = lt
     # a tail of graph replays of arm 0 (a kernel trace of this run ends with whole replays:
     # tools/trace_timeline.py)
     d = plans[0]
@@ -136,6 +162,8 @@ def main():
                "normwise_vs_arm0": err}
         if d.get("ktile"):
             rec["ktile_stamps_us_last_round"] = d["ktile"]
+        if d.get("lat"):
+            rec["lat_stamps_us_last_round"] = d["lat"]
         out[json.dumps(d["arm"])] = rec
         print(json.dumps(d["arm"]), json.dumps(rec), flush=True)
     print(json.dumps(out))
