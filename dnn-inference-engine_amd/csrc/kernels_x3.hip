@@ -249,7 +249,7 @@ int launch_x3_combine(const float* part, int splits, long long slab, const EpiPa
     set_error("x3_combine: %lld outputs", total);
     return -2;
   }
-  const dim3 grid((unsigned)((total + 255) / 256));
+  const dim3 grid((unsigned)((total + 255) / 256));  // (64- / 128-thread blocks: same time, measured)
 #define X3C(KH, KW, S, CPT) \
   hipLaunchKernelGGL((x3_combine_kernel<KH, KW, S, CPT>), grid, dim3(256), 0, s, part, splits, slab, epi, g, out, out_split, total)
   if (win == 2 && splits == 2)
@@ -681,7 +681,7 @@ int launch_conv_x3_ktile(const bf16_bits* in_split, const bf16_bits* Bt, float* 
   return check_x3("conv_x3_ktile");
 }
 
-// 1x1 form (latency plans' conv8): 16 rows x 32 columns, 4 K groups of one wave
+// 1x1 form (latency plans' conv8): 16 rows x 32 columns, K groups of one wave (4; 16 at K = 1024)
 bool conv_x3_1x1_ktile_supported(int C, int OC, int H, int W) {
   const int nch = C / 32;
   return C % 32 == 0 && nch % 4 == 0 && nch / 4 <= 8 && OC >= 1 && H >= 1 && W >= 1 && x3_enabled() &&
@@ -703,11 +703,14 @@ int launch_conv_x3_1x1_ktile(const bf16_bits* in_split, const bf16_bits* Bt, flo
   }
   const int tilesM = (int)((M + 15) / 16), tilesN = Npad / 32;
   const X3Geom xg{H, W, C, 0, 1, 0, 0};
-#define X3K1(CPK_)                                                                                                  \
-  hipLaunchKernelGGL((conv1x1_x3_ktile_kernel<4, CPK_>), dim3((unsigned)((long long)tilesM * tilesN)), dim3(256), 0, \
-                     stream, in_split, Bt, out, (int)M, N, K, epi, tilesM, xg, (unsigned)in_bytes, (unsigned)b_bytes)
+#define X3K1W(KW_, CPK_)                                                                                              \
+  hipLaunchKernelGGL((conv1x1_x3_ktile_kernel<KW_, CPK_>), dim3((unsigned)((long long)tilesM * tilesN)), dim3(64 * KW_), \
+                     0, stream, in_split, Bt, out, (int)M, N, K, epi, tilesM, xg, (unsigned)in_bytes, (unsigned)b_bytes)
+#define X3K1(CPK_) X3K1W(4, CPK_)
+  // K = 1024 (conv8): 16 groups of two chunks -- the loads of 16 waves in flight per CU, not 4
+  // (graph replay -1.9 us, -1.5 us with 8 groups, same call; the groups' order changes the sums)
   if (cpk == 8)
-    X3K1(8);
+    X3K1W(16, 2);
   else if (cpk == 4)
     X3K1(4);
   else if (cpk == 2)
@@ -715,6 +718,7 @@ int launch_conv_x3_1x1_ktile(const bf16_bits* in_split, const bf16_bits* Bt, flo
   else
     X3K1(1);
 #undef X3K1
+#undef X3K1W
   return check_x3("conv_x3_1x1_ktile");
 }
 
