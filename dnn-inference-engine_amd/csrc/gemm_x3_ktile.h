@@ -345,7 +345,7 @@ conv3x3_x3_ktile_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __res
 // order by group 0, fp32 epilogue into out [M][N] (columns past N, the packing's padding, not
 // stored).  At one frame: 11 x 4 = 44 workgroups with an 8-step chain each, where the batch
 // kernel's 32 x 128 tiles over all of K were 6 (21 us) and the fp32 split-K GEMM 11.5 us.
-template <int KW, int CPK, int FL = -1>
+template <int KW, int CPK, int FL = -1, int NJ = 2>  // NJ: 16-column blocks per workgroup (1 or 2)
 __global__ void __launch_bounds__(64 * KW, 1)
 conv1x1_x3_ktile_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __restrict__ Bt, float* __restrict__ out,
                         int M, int N, int K, EpiParams epi, int tilesM, X3Geom g, unsigned in_bytes,
@@ -364,7 +364,7 @@ conv1x1_x3_ktile_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __res
   const int kg = wave_uniform(threadIdx.x >> 6);
   const int tile = xcd_tile(blockIdx.x, gridDim.x);
   const int tn = tile / tilesM, tm = tile - tn * tilesM;
-  const int m0 = tm * BM, n0 = tn * 32;
+  const int m0 = tm * BM, n0 = tn * 16 * NJ;
   const int fr = lane & 15, fq = lane >> 4;
   const int nk = K / 32, Wp = g.W + 2, HWo = g.H * g.W;
   auto padded = [&](int m) {
@@ -397,7 +397,7 @@ conv1x1_x3_ktile_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __res
 #pragma unroll
     for (int p = 0; p < 3; ++p)
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
+      for (int j = 0; j < NJ; ++j)
         bq[c][p][j] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rsB, bvo, (s0 + c) * 3072 + p * 1024 + j * bjs, 0));
   const X3EpiCol ecp[2] = {x3_epi_col(epi, eflags, n0 + fr < N ? n0 + fr : N - 1),
                            x3_epi_col(epi, eflags, n0 + 16 + fr < N ? n0 + 16 + fr : N - 1)};
@@ -413,25 +413,25 @@ conv1x1_x3_ktile_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __res
 #pragma unroll
     for (int p = 0; p < 3; ++p) af[p] = *reinterpret_cast<const bf16x8*>(P + 64 * p);
 #pragma unroll
-    for (int jb = 0; jb < 2; ++jb) x3_step<true>(acc[jb], accc[jb], af, bq[c], jb);
+    for (int jb = 0; jb < NJ; ++jb) x3_step<true>(acc[jb], accc[jb], af, bq[c], jb);
   }
 #pragma unroll
-  for (int jb = 0; jb < 2; ++jb) acc[jb] = acc[jb] + accc[jb];  // (x3_fold)
+  for (int jb = 0; jb < NJ; ++jb) acc[jb] = acc[jb] + accc[jb];  // (x3_fold)
   wait_lgkm0();
   __syncthreads();
   f32x4* const red = reinterpret_cast<f32x4*>(smem);
   if (kg > 0) {
 #pragma unroll
-    for (int jb = 0; jb < 2; ++jb) red[((kg - 1) * 2 + jb) * 64 + lane] = acc[jb];
+    for (int jb = 0; jb < NJ; ++jb) red[((kg - 1) * 2 + jb) * 64 + lane] = acc[jb];
   }
   __syncthreads();
   if (kg > 0) return;
 #pragma unroll
   for (int k = 1; k < KW; ++k)
 #pragma unroll
-    for (int jb = 0; jb < 2; ++jb) acc[jb] = acc[jb] + red[((k - 1) * 2 + jb) * 64 + lane];
+    for (int jb = 0; jb < NJ; ++jb) acc[jb] = acc[jb] + red[((k - 1) * 2 + jb) * 64 + lane];
 #pragma unroll
-  for (int jb = 0; jb < 2; ++jb) {
+  for (int jb = 0; jb < NJ; ++jb) {
     const int n = n0 + 16 * jb + fr;
     if (n >= N) continue;
 #pragma unroll

@@ -681,7 +681,8 @@ int launch_conv_x3_ktile(const bf16_bits* in_split, const bf16_bits* Bt, float* 
   return check_x3("conv_x3_ktile");
 }
 
-// 1x1 form (latency plans' conv8): 16 rows x 32 columns, K groups of one wave (4; 16 at K = 1024)
+// 1x1 form (latency plans' conv8): 16 rows x 32 columns, K groups of one wave (4; at K = 1024: 16
+// groups, 16 columns)
 bool conv_x3_1x1_ktile_supported(int C, int OC, int H, int W) {
   const int nch = C / 32;
   return C % 32 == 0 && nch % 4 == 0 && nch / 4 <= 8 && OC >= 1 && H >= 1 && W >= 1 && x3_enabled() &&
@@ -701,16 +702,20 @@ int launch_conv_x3_1x1_ktile(const bf16_bits* in_split, const bf16_bits* Bt, flo
     set_error("conv_x3_1x1_ktile: unsupported shape M=%lld N=%d K=%d %dx%dx%d", M, N, K, H, W, C);
     return -2;
   }
-  const int tilesM = (int)((M + 15) / 16), tilesN = Npad / 32;
+  // K = 1024 (conv8): 16-column workgroups (88 at one frame, not 44: -1.4 us per replay, same bits)
+  const int nj = cpk == 8 ? 1 : 2;
+  const int tilesM = (int)((M + 15) / 16), tilesN = Npad / (16 * nj);
   const X3Geom xg{H, W, C, 0, 1, 0, 0};
-#define X3K1W(KW_, CPK_)                                                                                              \
-  hipLaunchKernelGGL((conv1x1_x3_ktile_kernel<KW_, CPK_>), dim3((unsigned)((long long)tilesM * tilesN)), dim3(64 * KW_), \
-                     0, stream, in_split, Bt, out, (int)M, N, K, epi, tilesM, xg, (unsigned)in_bytes, (unsigned)b_bytes)
+#define X3K1J(KW_, CPK_, NJ_)                                                                                         \
+  hipLaunchKernelGGL((conv1x1_x3_ktile_kernel<KW_, CPK_, -1, NJ_>), dim3((unsigned)((long long)tilesM * tilesN)),      \
+                     dim3(64 * KW_), 0, stream, in_split, Bt, out, (int)M, N, K, epi, tilesM, xg, (unsigned)in_bytes,    \
+                     (unsigned)b_bytes)
+#define X3K1W(KW_, CPK_) X3K1J(KW_, CPK_, 2)
 #define X3K1(CPK_) X3K1W(4, CPK_)
   // K = 1024 (conv8): 16 groups of two chunks -- the loads of 16 waves in flight per CU, not 4
   // (graph replay -1.9 us, -1.5 us with 8 groups, same call; the groups' order changes the sums)
   if (cpk == 8)
-    X3K1W(16, 2);
+    X3K1J(16, 2, 1);
   else if (cpk == 4)
     X3K1(4);
   else if (cpk == 2)
@@ -719,6 +724,7 @@ int launch_conv_x3_1x1_ktile(const bf16_bits* in_split, const bf16_bits* Bt, flo
     X3K1(1);
 #undef X3K1
 #undef X3K1W
+#undef X3K1J
   return check_x3("conv_x3_1x1_ktile");
 }
 
