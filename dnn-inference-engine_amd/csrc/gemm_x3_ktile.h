@@ -20,12 +20,12 @@
 namespace dnnhip {
 
 #if (X3DIAG & 256) != 0  // diagnostic builds: per workgroup s_memrealtime at start, patch landed, MFMAs done,
-                         // end; 26-wide shape at workgroups 0-511, 13-wide at 512-1023
+                         // end; 14/26-wide tiles at workgroups 0-511, 13-wide at 512-1023
 constexpr int KT_DIAG_WGS = 1024;
 __device__ unsigned long long ktile_diag_stamps[KT_DIAG_WGS * 4];
 #define KT_STAMP(k)                                                       \
   if (threadIdx.x == 0 && blockIdx.x < KT_DIAG_WGS / 2)                   \
-    ktile_diag_stamps[4 * (blockIdx.x + (TW == 26 ? 0 : KT_DIAG_WGS / 2)) + (k)] = __builtin_amdgcn_s_memrealtime();
+    ktile_diag_stamps[4 * (blockIdx.x + (TW > 13 ? 0 : KT_DIAG_WGS / 2)) + (k)] = __builtin_amdgcn_s_memrealtime();
 #else
 #define KT_STAMP(k)
 #endif

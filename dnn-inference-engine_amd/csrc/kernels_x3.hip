@@ -604,7 +604,7 @@ bool conv_x3_lat_supported(long long batch, int C, int OC, int H, int W, int OH,
 // workgroups of 4 waves = 4 K groups, one wave per SIMD (two waves of a workgroup sharing a SIMD
 // serialize their MFMA chains: 64-column, 8-wave workgroups measured 13.3 / 14.8 us with half
 // the chip idle).  Two shapes: frames up to 26 wide with 4 chunks (conv4: 26 x 26 x 128, pooled
-// or not; 2 x 26 tiles, 4 row blocks, one chunk per group) and up to 13 wide with 8 chunks
+// or not; 2 x 14 tiles, 2 row blocks, one chunk per group) and up to 13 wide with 8 chunks
 // (conv5: 13 x 13 x 256; one-row tiles, one row block, two chunks per group).
 // pool: 0 none, 1 a fused 2x2/s2 pool, 2 a fused 2x2/s1 SAME pool (YOLO's pool5; 13-wide shape)
 static int x3_ktile_shape(int C, int OC, int H, int W, int pool) {
@@ -641,7 +641,9 @@ int launch_conv_x3_ktile(const bf16_bits* in_split, const bf16_bits* Bt, float* 
     set_error("conv_x3_ktile: unsupported shape M=%lld N=%d K=%d %dx%dx%d pool=%d", M, N, K, H, W, C, pool);
     return -2;
   }
-  const int TH = shape == 1 ? 1 : 2, TW = shape == 1 ? 13 : 26;
+  // (conv4: 2 x 14 tiles, two per 26-wide row -- 208 workgroups at one frame, not 104, each wave
+  // two row blocks, not four: -2.8 us per replay, same bits; conv3 on 2 x 14 tiles measured slower)
+  const int TH = shape == 1 ? 1 : 2, TW = shape == 1 ? 13 : shape == 0 ? 14 : 26;
   const int tilesX = (W + TW - 1) / TW, tilesY = (H + TH - 1) / TH, tilesN = N / 32;
   const long long blocks = nimg * tilesX * tilesY * tilesN;
   if (blocks > 0x7fffffffLL) {
@@ -663,11 +665,11 @@ int launch_conv_x3_ktile(const bf16_bits* in_split, const bf16_bits* Bt, float* 
   else if (shape == 2)
     X3KW(2, 26, 2, 2, 2, 1, false, -1, false);
   else if (shape == 0 && p2 && yolo)
-    X3K(2, 26, 4, 1, true, X3_YOLO_FL, false);
+    X3K(2, 14, 2, 1, true, X3_YOLO_FL, false);
   else if (shape == 0 && p2)
-    X3K(2, 26, 4, 1, true, -1, false);
+    X3K(2, 14, 2, 1, true, -1, false);
   else if (shape == 0)
-    X3K(2, 26, 4, 1, false, -1, false);
+    X3K(2, 14, 2, 1, false, -1, false);
   else if (pool == 2 && yolo)  // (each one-row tile computes the row below it too: 2 row blocks)
     X3K(1, 13, 2, 2, false, X3_YOLO_FL, true);
   else if (pool == 2)
