@@ -223,7 +223,7 @@ int launch_f16_to_f32(const half_t* in, float* out, long long n, hipStream_t s);
 int launch_maxpool16(const half_t* in, half_t* out, const PoolGeom& g, hipStream_t s, int opad = 0);
 // fp16 3x3/s1/SAME conv with a zero-bordered input [B][H+2][W+2][C] (C % 64 == 0, N % 256 == 0),
 // weights packed K-order (chunk, tap, c) (launch_pack_weights order 2); out_padded: write the
-// output zero-bordered too (gemm_f16_patch.h)
+// output zero-bordered too (gemm_f16_acc.h)
 bool conv_patch16_supported(int C, int OC, int H, int W, int OH, int OW, int kh, int kw, int sh, int sw, int pt,
                             int pl);
 // fp32 path "x3" conv (kernels_x3.hip, gemm_x3_patch.h): fp32 operands split exactly into three
@@ -280,6 +280,12 @@ int launch_conv0_mfma(const float* in, const float* w, float* out, const DirectG
                       const EpiParams& epi, hipStream_t s);
 int launch_conv0_mfma_f16(const float* in, const float* w, half_t* out, const DirectGeom& g, int cin,
                           const EpiParams& epi, hipStream_t s);
+// conv_front.hip: conv0 (3 -> 16, pool) + conv1 (16 -> 32 on the x3 arithmetic, pool) as one kernel,
+// fp32 frames [B][H][W][3] in, conv1's pooled output as split planes of a zero-bordered
+// [B][H/4+2][W/4+2][32] buffer out; w0 HWIO [27][16], Bt1 packed by launch_pack_weights_x3 (C = 16)
+bool conv01_front_supported(int B, int H, int W);
+int launch_conv01_front(const float* in, const float* w0, const EpiParams& epi0, const unsigned short* Bt1,
+                        const EpiParams& epi1, unsigned short* out_split, int B, int H, int W, hipStream_t s);
 bool conv1_patch_f16_supported(int C, int OC, int H, int W, int OH, int OW, int kh, int kw, int sh, int sw, int pt,
                                int pl);
 int launch_conv1_patch_f16(const half_t* in, const half_t* Bt, int ldb, half_t* out, const DirectGeom& g,

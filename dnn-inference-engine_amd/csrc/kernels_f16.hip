@@ -5,7 +5,6 @@
 #include <cfloat>
 #include "dnn_common.h"
 #include "gemm_f16.h"
-#include "gemm_f16_patch.h"
 #include "gemm_f16_acc.h"
 
 namespace dnnhip {
@@ -278,12 +277,6 @@ static bool patch16_enabled() {
   return e ? e[0] == '1' : P16_DEFAULT;
 }
 
-bool conv_patch16_supported(int C, int OC, int H, int W, int OH, int OW, int kh, int kw, int sh, int sw, int pt,
-                            int pl) {
-  return kh == 3 && kw == 3 && sh == 1 && sw == 1 && pt == 1 && pl == 1 && OH == H && OW == W && C % 64 == 0 &&
-         OC % 256 == 0 && patch16_enabled();
-}
-
 // rows of the padded input one BM-row tile spans (tap offsets included)
 static int patch16_span(long long M, int H, int W) {
   const int Wp = W + 2;
@@ -301,22 +294,35 @@ static int patch16_span(long long M, int H, int W) {
   return (int)(mx < 0x7fffffff ? mx : 0x7fffffff);
 }
 
+// the launcher's patch limits for any batch: spans grow with M only until a tile
+// crosses whole images, so two images' worth of rows decides it; the row-skewed LDS patch holds
+// span * 10 + 12 * (span / Wp + 2) 16-B units (56 KiB).  A layer past them stays on the fp16 GEMM.
+static bool patch16_fits(long long span, int W) {
+  return span <= P16_NPR && span * 10 + 12 * (span / (W + 2) + 2) <= 7 * 8 * 64;
+}
+
+bool conv_patch16_supported(int C, int OC, int H, int W, int OH, int OW, int kh, int kw, int sh, int sw, int pt,
+                            int pl) {
+  return kh == 3 && kw == 3 && sh == 1 && sw == 1 && pt == 1 && pl == 1 && OH == H && OW == W && C % 64 == 0 &&
+         OC % 256 == 0 && patch16_enabled() && H > 0 && W > 0 &&
+         patch16_fits(patch16_span(2LL * H * W + P16_BM, H, W), W);
+}
+
 int launch_conv_patch16(const half_t* in_padded, const half_t* Bt, int ldb, half_t* out, int out_padded, long long M,
                         int N, int K, int H, int W, int C, const EpiParams& epi, hipStream_t stream) {
   if (M == 0 || N == 0) return 0;
   const long long nimg = M / ((long long)H * W);
   const long long in_bytes = nimg * (H + 2) * (W + 2) * (long long)C * 2;
   if (M % ((long long)H * W) != 0 || K != 9 * C || C % 64 != 0 || N % 256 != 0 || ldb < K || ldb % 8 != 0 ||
-      in_bytes >= 0x80000000LL || M > 0x7fffffffLL || patch16_span(M, H, W) > P16_NPR) {
+      in_bytes >= 0x80000000LL || M > 0x7fffffffLL || !patch16_fits(patch16_span(M, H, W), W)) {
     set_error("conv_patch16: unsupported shape M=%lld N=%d K=%d %dx%dx%d", M, N, K, H, W, C);
     return -2;
   }
   const int bm = P16_BM;
   const int tilesM = (int)((M + bm - 1) / bm), tilesN = N / 256;
   const Patch16Geom pg{H, W, C, out_padded};
-  // the row-skewed patch: span * 10 + 12 * (span / Wp + 2) 16-B units in the 56-KiB buffer
-  const long long span = patch16_span(M, H, W), b_bytes = (long long)N * ldb * 2;
-  if (span * 10 + 12 * (span / (W + 2) + 2) > 7 * 8 * 64 || b_bytes >= 0x80000000LL) {
+  const long long b_bytes = (long long)N * ldb * 2;
+  if (b_bytes >= 0x80000000LL) {
     set_error("conv_patch16: unsupported shape M=%lld N=%d K=%d %dx%dx%d", M, N, K, H, W, C);
     return -2;
   }

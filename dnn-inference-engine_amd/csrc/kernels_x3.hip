@@ -686,8 +686,10 @@ int launch_conv_x3_ktile(const bf16_bits* in_split, const bf16_bits* Bt, float* 
 // 1x1 form (latency plans' conv8): 16 rows x 32 columns, K groups of one wave (4; at K = 1024: 16
 // groups, 16 columns)
 bool conv_x3_1x1_ktile_supported(int C, int OC, int H, int W) {
-  const int nch = C / 32;
-  return C % 32 == 0 && nch % 4 == 0 && nch / 4 <= 8 && OC >= 1 && H >= 1 && W >= 1 && x3_enabled() &&
+  // the launcher's instantiations: K / 128 = 1, 2, 4 or 8 chunk quads (other widths, e.g. C = 384
+  // after a kind-2 tile conv, stay on the fp32 GEMM)
+  const int nq = C / 128;
+  return C % 128 == 0 && (nq == 1 || nq == 2 || nq == 4 || nq == 8) && OC >= 1 && H >= 1 && W >= 1 && x3_enabled() &&
          !getenv_flag_off("DNN_HIP_X3_1X1");
 }
 

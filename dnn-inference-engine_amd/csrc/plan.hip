@@ -107,6 +107,8 @@ struct PlanLayer {
   bool x3lat = false;  // MODE_X3 on the small-M kernel (latency plans: launch_conv_x3_lat)
   bool x3k = false;    // MODE_X3 with the K split inside the workgroup (latency plans: launch_conv_x3_ktile)
   bool pool1 = false;  // x3k: a 2x2/stride-1 SAME pool fused (same output frame)
+  bool front = false;  // conv0 (MODE_DIRECT) run together with the next layer (the 16-channel x3
+                       // conv1) as one kernel (conv_front.hip); the next layer launches nothing
   bool out_padded = false;  // output written zero-bordered (the next layer is MODE_PATCH16 / MODE_X3;
                             // fp32 plans: as x3 split planes)
   size_t pad_off = 0;       // its zero-bordered output region: float offset inside the pad area
@@ -173,7 +175,31 @@ static void drop_graph(dnn_plan* p) {
 
 static bool fused_splitk(const dnn_plan* p) { return p->splitk_fused; }
 
+// conv0 -> conv1 as one kernel (conv_front.hip) where the plan has YOLO's front: a 3-channel 3x3
+// SAME conv to 16 channels with its 2x2/s2 pool on the direct kernel, then the 16-channel x3 conv
+// to 32 channels with its pool, writing the next x3 layer's split planes.  Batch plans only (the
+// latency plans keep their single-frame conv1 shape); DNN_HIP_FRONT=0 keeps two kernels.
+static void mark_front(dnn_plan* p) {
+  for (auto& L : p->layers) L.front = false;
+  if (p->fp16 || p->latency || !p->fuse) return;
+  for (size_t i = 0; i + 1 < p->layers.size(); ++i) {
+    const PlanLayer& a = p->layers[i];
+    const PlanLayer& c = p->layers[i + 1];
+    const bool conv0 = a.type == 0 && a.mode == MODE_DIRECT && a.pool && a.C == 3 && a.OC == 16 && a.kh == 3 &&
+                       a.kw == 3 && a.sh == 1 && a.sw == 1 && a.pt == 1 && a.pl == 1 && a.OH == a.H && a.OW == a.W &&
+                       a.PH * 2 == a.OH && a.PW * 2 == a.OW;
+    const bool conv1 = c.type == 0 && c.mode == MODE_X3 && c.C == 16 && c.OC == 32 && c.pool && !c.x3k && !c.x3lat &&
+                       c.splits == 1 && c.out_padded && c.H == a.PH && c.W == a.PW && c.kh == 3 && c.kw == 3 &&
+                       c.pt == 1 && c.pl == 1 && c.OH == c.H && c.OW == c.W;
+    if (conv0 && conv1 && conv01_front_supported(p->batch, a.H, a.W)) {
+      p->layers[i].front = true;
+      ++i;
+    }
+  }
+}
+
 static void layout(dnn_plan* p) {
+  mark_front(p);
   size_t off = 0, act = (size_t)p->in_h * p->in_w * p->in_c, col = 0, slab = 0, slab_fused = 0, tickets = 0;
   int nconv = 0, npool = 0;  // kernel names use conv / pool ordinals: "conv7.gemm" is YOLO's conv7
   p->kernels.clear();
@@ -185,6 +211,19 @@ static void layout(dnn_plan* p) {
     const double in_b = 4.0 * B * L.H * L.W * L.C, out_b = 4.0 * B * L.out_h() * L.out_w() * L.OC;
     L.kernel_idx = (int)p->kernels.size();
     char nm[64];
+    if (i > 0 && p->layers[i - 1].front) {  // conv1 inside the front kernel: its weights, no kernel
+      L.kernel_idx = p->layers[i - 1].kernel_idx;
+      L.w_off = off;
+      off = align_up(off + (size_t)L.Npad * L.Kpad * 3 / 2, 64);
+      L.epi_off = off;
+      off = align_up(off + 4 * (size_t)L.Npad, 64);
+      KernelDesc& f = p->kernels.back();
+      f.flops += 2.0 * M * L.OC * L.K;
+      f.bytes += 6.0 * B * (L.out_h() + 2) * (L.out_w() + 2) * L.OC + 4.0 * L.K * L.OC;  // split planes out
+      if (L.pool) npool++;
+      ++nconv;
+      continue;
+    }
     if (L.type == 0) {
       L.w_off = off;
       // fp16 GEMM layers hold Bt in halves (2 per float slot); conv0's direct kernel reads fp32
@@ -203,6 +242,10 @@ static void layout(dnn_plan* p) {
         p->kernels.push_back({nm, (int)i, 0, 0.0, 4.0 * M * L.K + in_b});
         snprintf(nm, sizeof(nm), "conv%d.gemm", nconv++);
         p->kernels.push_back({nm, (int)i, 1, flops, 4.0 * M * L.K + w_b + out_b});
+      } else if (L.front) {  // frames in (conv1's output bytes added with conv1)
+        snprintf(nm, sizeof(nm), "conv%d+%d.gemm", nconv, nconv + 1);
+        ++nconv;
+        p->kernels.push_back({nm, (int)i, 1, flops, in_b + w_b});
       } else if (L.mode == MODE_DIRECT || L.mode == MODE_PATCH) {
         snprintf(nm, sizeof(nm), L.mode == MODE_DIRECT ? "conv%d.direct" : "conv%d.patch", nconv++);
         p->kernels.push_back({nm, (int)i, 1, flops, in_b + w_b + out_b});
@@ -874,6 +917,18 @@ int dnn_plan_run(dnn_plan* p, int n, const float* d_in, float* d_out, void* stre
           break;
         }
         case MODE_DIRECT: {
+          if (L.front) {  // conv0 + conv1 (conv_front.hip) into conv1's split planes
+            PlanLayer& L1 = p->layers[i + 1];
+            const float* e1 = p->weights + L1.epi_off;
+            const EpiParams epi1{e1, e1 + L1.Npad, e1 + 2 * L1.Npad, e1 + 3 * L1.Npad, L1.epi_flags};
+            unsigned short* ds1 = padr + L1.pad_off * 2;
+            rc = launch_conv01_front(cur, wt, epi, reinterpret_cast<const unsigned short*>(p->weights + L1.w_off),
+                                     epi1, ds1, n, L.H, L.W, s);
+            if (rc) return rc;
+            ++i;
+            cur = reinterpret_cast<const float*>(ds1);
+            continue;
+          }
           DirectGeom g{n, L.H, L.W, L.OH, L.OW, L.PH, L.PW, L.pt, L.pl};
           rc = conv0_mfma_supported(L.C, L.OC, L.kh, L.kw, L.sh, L.sw)
                    ? launch_conv0_mfma(cur, wt, dst, g, L.C, zero, epi, s)
@@ -1024,9 +1079,10 @@ int dnn_plan_describe(const dnn_plan* p, char* buf, int buf_len) {
     if (L.type == 0) {
       char sk[32] = "";
       if (L.splits > 1) snprintf(sk, sizeof(sk), " splitK=%d", L.splits);
-      snprintf(line, sizeof(line), "conv %dx%dx%d -> %dx%dx%d k%dx%d s%d mode=%s cfg=%d K=%d Kpad=%d%s%s%s%s%s\n", L.H,
+      const bool fr = L.front || (i > 0 && p->layers[i - 1].front);
+      snprintf(line, sizeof(line), "conv %dx%dx%d -> %dx%dx%d k%dx%d s%d mode=%s cfg=%d K=%d Kpad=%d%s%s%s%s%s%s\n", L.H,
                L.W, L.C, L.out_h(), L.out_w(), L.OC, L.kh, L.kw, L.sh, L.x3lat ? "x3_lat" : L.x3k ? "x3_ktile" : kModeName[L.mode], L.cfg, L.K, L.Kpad,
-               L.pool ? " +pool2x2s2" : L.pool1 ? " +pool2x2s1" : "", sk,
+               L.pool ? " +pool2x2s2" : L.pool1 ? " +pool2x2s1" : "", fr ? " front01" : "", sk,
                L.splits > 1 ? (L.mode == MODE_X3 ? " x3-combine" : fused_splitk(p) ? " combine" : "") : "",
                p->fp16 ? " fp16" : "", p->latency ? " latency" : "");
     } else

@@ -385,3 +385,48 @@ def test_latency_env_default_only_for_fp32(monkeypatch):
     assert not dnn_hip.DnnInferenceEngine(g, False, latency=False).latency
     monkeypatch.setenv("DNN_HIP_LATENCY", "0")
     assert not dnn_hip.DnnInferenceEngine(g, False).latency
+
+
+@pytest.mark.parametrize("c_mid,want_x3", [(384, False), (512, True), (640, False), (1024, True)])
+def test_latency_1x1_ktile_only_for_launchable_widths(c_mid, want_x3):
+    """a latency plan's 1x1 head after an x3 conv takes the K-split x3 kernel only for
+    the widths its launcher instantiates (K / 128 = 1, 2, 4, 8 chunk quads); other widths (C = 384
+    after a kind-2 tile conv, 640, ...) stay on the fp32 GEMM instead of failing at run time."""
+    lib = dnn_hip.mylib
+    h = ctypes.c_void_p()
+    assert lib.dnn_plan_create(1, 13, 13, 256, ctypes.byref(h)) == 0
+    try:
+        assert lib.dnn_plan_set_latency_mode(h, 1) == 0
+        assert lib.dnn_plan_add_max_pool(h, 2, 2, 1, 1, 1) == 0  # split-plane producer of the 3x3 conv
+        assert lib.dnn_plan_add_conv(h, 3, 3, c_mid, 1, 1, 1, None, None, None, None, None, 0.0, 1) == 0
+        assert lib.dnn_plan_add_conv(h, 1, 1, 125, 1, 1, 1, None, None, None, None, None, 0.0, 0) == 0
+        buf = ctypes.create_string_buffer(4096)
+        assert lib.dnn_plan_describe(h, buf, 4096) == 0
+        conv = [ln for ln in buf.value.decode().splitlines() if ln.startswith("conv")]
+        assert "mode=patch_x3" in conv[0] or "mode=x3_" in conv[0], conv
+        assert ("mode=x3_ktile" in conv[1]) == want_x3, conv
+        if not want_x3:
+            assert "mode=direct_a" in conv[1], conv
+    finally:
+        lib.dnn_plan_destroy(h)
+
+
+@pytest.mark.parametrize("hw,want_patch", [((64, 3), False), ((64, 2), False), ((64, 4), True), ((13, 13), True)])
+def test_fp16_patch_kernel_only_where_its_patch_fits(hw, want_patch):
+    """the fp16 patch kernel's row-skewed LDS patch holds span * 10 + 12 (span / Wp + 2)
+    16-B units; narrow frames whose tiles span more (W = 3: 306 rows, 3,816 units) or more than
+    its 320 rows (W = 2) stay on the fp16 implicit GEMM instead of failing at launch."""
+    H, W = hw
+    lib = dnn_hip.mylib
+    h = ctypes.c_void_p()
+    assert lib.dnn_plan_create(2, H, W, 64, ctypes.byref(h)) == 0
+    try:
+        assert lib.dnn_plan_set_precision(h, 1) == 0
+        assert lib.dnn_plan_add_max_pool(h, 2, 2, 1, 1, 1) == 0  # a pool producer (zero-bordered output)
+        assert lib.dnn_plan_add_conv(h, 3, 3, 256, 1, 1, 1, None, None, None, None, None, 0.0, 1) == 0
+        buf = ctypes.create_string_buffer(4096)
+        assert lib.dnn_plan_describe(h, buf, 4096) == 0
+        conv = [ln for ln in buf.value.decode().splitlines() if ln.startswith("conv")]
+        assert ("mode=patch16" in conv[0]) == want_patch, conv
+    finally:
+        lib.dnn_plan_destroy(h)

@@ -1740,6 +1740,74 @@ def test_conv0_conv1_chain(monkeypatch, case):
     assert R.normwise_err(outs["1"], ref) <= 1.25 * max(R.normwise_err(outs["0"], ref), 1e-7)
 
 
+FRONT_CASES = [
+    # B, H, W (multiples of 32): conv0 + conv1 as one kernel (conv_front.hip), 16 x 16 conv1 tiles
+    (2, 96, 128),   # 6 x 8 tiles per frame: the frame patch's zero border on every side
+    (5, 64, 32),    # narrow frames, several rounds of tiles per workgroup on small grids
+    (1, 416, 416),  # YOLO's frame: 169 tiles, fewer than the CUs
+]
+
+
+@pytest.mark.parametrize("case", FRONT_CASES)
+def test_front_fused_conv0_conv1(monkeypatch, case):
+    """conv0 + conv1 fused into one kernel (conv_front.hip, opt-in DNN_HIP_FRONT=1: producer waves
+    run conv0 into conv1's LDS patch, consumer waves run conv1's x3 MFMAs) equal, bit for bit, the
+    two kernels they replace (conv0_packed_pool -> conv3x3_x3_c16p), with a third x3 layer reading
+    the split planes the fused kernel writes; batch rows equal batch-1 runs; repeat runs equal;
+    within the layer tolerance of the float64 oracle; negative-gamma channels."""
+    B, H, W = case
+    rng = np.random.default_rng(B * 7 + H + W)
+    monkeypatch.setenv("DNN_HIP_FRONT", "1")  # (opt-in)
+    x = rng.uniform(0.0, 1.0, (B, H, W, 3)).astype(np.float32)
+    x[0, 0, :5] = 0.0  # zero pixels at a frame corner, exact 1.0 inside
+    x[-1, H // 2, W // 2] = 1.0
+
+    def layer(c, od):
+        k = (rng.standard_normal((3, 3, c, od)) * np.sqrt(2.0 / (9 * c))).astype(np.float32)
+        b = rng.standard_normal(od).astype(np.float32) * 0.1
+        gam = rng.uniform(0.5, 1.5, od).astype(np.float32)
+        gam[::5] *= -1
+        return k, b, (rng.standard_normal(od).astype(np.float32) * 0.1, rng.uniform(0.5, 1.5, od).astype(np.float32),
+                      gam)
+
+    layers = [(layer(3, 16), True), (layer(16, 32), True), (layer(32, 64), False)]
+
+    def graph(shape):
+        g = dnn_hip.DnnGraphBuilder()
+        y = g.create_input(list(shape))
+        for (k, b, n), pool in layers:
+            y = g.create_conv2d(y, k, [1, 1, 1, 1], "SAME")
+            y = g.create_bias_add(y, b)
+            y = g.create_batch_norm(y, *n, 1e-5)
+            y = g.create_leaky_relu(y)
+            if pool:
+                y = g.create_max_pool2d(y, [1, 2, 2, 1], [1, 2, 2, 1], "SAME")
+        g.set_out_node(y)
+        return g
+
+    outs = {}
+    for fr in ("0", "1"):
+        monkeypatch.setenv("DNN_HIP_FRONT", fr)
+        eng = dnn_hip.DnnInferenceEngine(graph(x.shape), False)
+        conv = [ln for ln in eng.plan().describe().splitlines() if ln.startswith("conv")]
+        assert ("front01" in conv[0] and "front01" in conv[1]) == (fr == "1"), conv
+        names = [k["name"] for k in eng.plan().kernels()]
+        assert ("conv0+1.gemm" in names) == (fr == "1") and ("conv1.gemm" in names) == (fr == "0"), names
+        outs[fr] = eng.run(x)
+        assert np.array_equal(eng.run(x), outs[fr]), fr
+    assert np.array_equal(outs["1"], outs["0"])
+    monkeypatch.setenv("DNN_HIP_FRONT", "1")
+    f = B - 1
+    y1 = dnn_hip.DnnInferenceEngine(graph((1,) + x.shape[1:]), False).run(x[f:f + 1])
+    assert np.array_equal(y1, outs["1"][f:f + 1])
+    ref = x
+    for (k, b, n), pool in layers:
+        ref = R.leaky_relu(R.batch_norm(R.bias_add(R.conv2d(ref, k), b), *n, 1e-5))
+        if pool:
+            ref = R.max_pool2d(ref, [1, 2, 2, 1], [1, 2, 2, 1], "SAME")
+    assert R.normwise_err(outs["1"], ref) < 3 * LAYER_TOL
+
+
 @pytest.mark.parametrize("kind", ["huge", "tiny"])
 def test_x3_split_total_over_finite_fp32(monkeypatch, kind):
     """split3 (gemm_f32.h) is total over finite fp32: an operand above the largest bf16

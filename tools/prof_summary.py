@@ -61,14 +61,17 @@ def dispatch_sequence(rows, key_start="Start_Timestamp", key_end="End_Timestamp"
     seq.sort(key=lambda r: int(r.get("Dispatch_Id") or 0))
     out, i = [], 0
     first = None
+    order = ORDER
     while i < len(seq):
         name = seq[i]["Kernel_Name"]
         if first is None:
             first = name  # the first dispatch of the first forward defines the start marker
-        if name == first and i + len(ORDER) <= len(seq):
-            for j, pk in enumerate(ORDER):
+            if "conv01_front" in name:  # conv0 + conv1 as one kernel (conv_front.hip)
+                order = ["conv0+1.gemm"] + [k for k in ORDER if k not in ("conv0.direct", "conv1.gemm")]
+        if name == first and i + len(order) <= len(seq):
+            for j, pk in enumerate(order):
                 out.append((pk, seq[i + j]))
-            i += len(ORDER)
+            i += len(order)
         else:
             i += 1
     return out
