@@ -30,7 +30,8 @@
 
 // X3DIAG (diagnostic builds only, tools/build_diag.sh; see also gemm_x3_acc2.h): bit 32 records
 // conv3x3_x3_c16p_kernel's per-workgroup phase cycles (results unchanged), bit 64 drops its pool /
-// epilogue math, bit 128 replaces its input split by a 2-instruction truncation (wrong results)
+// epilogue math, bit 128 replaces its input split by a 2-instruction truncation (wrong results),
+// bit 1024 records conv3x3_x3_tile2_kernel's per-workgroup phase stamps (results unchanged)
 #ifndef X3DIAG
 #define X3DIAG 0
 #endif
@@ -43,6 +44,19 @@ constexpr int C16_DIAG_SLOTS = 10;
 // table + next loads, 2 barrier, 3 MFMAs, 4 barrier, 5 epilogue math + stage, 6 split-plane
 // stores, 7 barrier; 8 tiles
 __device__ unsigned long long c16_diag_stamps[C16_DIAG_WGS * C16_DIAG_SLOTS];
+#endif
+
+#if (X3DIAG & 1024) != 0  // conv3x3_x3_tile2_kernel phase stamps
+constexpr int T2_DIAG_WGS = 4096;
+constexpr int T2_DIAG_SLOTS = 8;
+// [layer (0: N = 64, 1: wider)][workgroup][slot], wave 0: 0 s_memrealtime at start, 1-4 s_memtime at
+// start, patch landed, MFMAs done, end; 5 s_memrealtime at end; 6 HW_ID; 7 XCC_ID
+__device__ unsigned long long tile2_diag_stamps[2 * T2_DIAG_WGS * T2_DIAG_SLOTS];
+#define T2_STAMP(k, v)                                                                               \
+  if (threadIdx.x == 0 && blockIdx.x < T2_DIAG_WGS)                                                  \
+    tile2_diag_stamps[((N == 64 ? 0 : 1) * T2_DIAG_WGS + blockIdx.x) * T2_DIAG_SLOTS + (k)] = (v);
+#else
+#define T2_STAMP(k, v)
 #endif
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -762,6 +776,10 @@ conv3x3_x3_tile2_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __res
   const int n0 = tn * (32 * WN) + wn * 32;
   const int Wp = g.W + 2;
   const int fr = lane & 15, fq = lane >> 4;
+  T2_STAMP(0, __builtin_amdgcn_s_memrealtime())
+  T2_STAMP(1, __builtin_amdgcn_s_memtime())
+  T2_STAMP(6, (unsigned)__builtin_amdgcn_s_getreg(4 | (31 << 11)))
+  T2_STAMP(7, (unsigned)__builtin_amdgcn_s_getreg(20 | (31 << 11)))
 
   // fragment rows: byte offset of the lane's tap-(0, 0) pixel row of block i (+ 16 fq)
   int rowoff[TM];
@@ -832,6 +850,7 @@ conv3x3_x3_tile2_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __res
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  T2_STAMP(2, __builtin_amdgcn_s_memtime())
 
   auto frag = [&](const unsigned char* P, int i, int tap, bf16x8 (&a)[3]) {
     const int toff = ((tap / 3) * PW2 + (tap % 3)) * LP;
@@ -881,6 +900,7 @@ conv3x3_x3_tile2_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __res
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  T2_STAMP(3, __builtin_amdgcn_s_memtime())
 
   x3_fold(acc, accc);
   int* orow = reinterpret_cast<int*>(smem);
@@ -914,6 +934,8 @@ conv3x3_x3_tile2_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __res
           stg[(4 * i + fq) * X3_STG_ROW + 16 * jb + fr] = pool_then_epilogue_t<FL>(acc[i][jb], pb, pm, ps, pg, epi.flags);
       }
       x3_pool_split_store<TM>(stg, orow, NO, 4 * wm * TM, out_split, 3 * (size_t)N, (n0 >> 5) * 96, lane);
+      T2_STAMP(4, __builtin_amdgcn_s_memtime())
+      T2_STAMP(5, __builtin_amdgcn_s_memrealtime())
       return;
     }
   }
@@ -952,6 +974,9 @@ conv3x3_x3_tile2_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __res
       }
     }
   }
+  T2_STAMP(4, __builtin_amdgcn_s_memtime())
+  T2_STAMP(5, __builtin_amdgcn_s_memrealtime())
 }
+#undef T2_STAMP
 
 }  // namespace dnnhip

@@ -846,6 +846,18 @@ extern "C" __attribute__((visibility("default"))) int dnn_ktile_diag_stamps(unsi
 }
 #endif
 
+#if (X3DIAG & 1024) != 0
+// diagnostic builds (X3DIAG bit 1024): conv3x3_x3_tile2_kernel's per-workgroup stamps of its last
+// launch per layer class (T2_DIAG_SLOTS per workgroup, gemm_x3_patch.h) copied to host[0 .. slots n)
+extern "C" __attribute__((visibility("default"))) int dnn_tile2_diag_stamps(unsigned long long* host, int n) {
+  if (n < 0 || n > 2 * dnnhip::T2_DIAG_WGS * dnnhip::T2_DIAG_SLOTS) return -2;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(dnnhip::tile2_diag_stamps), (size_t)n * sizeof(unsigned long long), 0,
+                             hipMemcpyDeviceToHost) == hipSuccess
+             ? 0
+             : -1;
+}
+#endif
+
 #if (X3DIAG & 512) != 0
 // diagnostic builds (X3DIAG bit 512): conv3x3_x3_lat_kernel's per-workgroup s_memrealtime stamps
 // [start, patch landed, MFMAs done, end] of its last launch copied to host[0 .. 4n)

@@ -290,11 +290,43 @@ def unpack_detections(dets_u8, counts):
     return out
 
 
+class _HostStream(object):
+    """Stand-in for a HIP stream when the runner's buffers live on the host (the CPU gloo tests
+    drive the pipelined path with host tensors): work is synchronous, waits are no-ops."""
+    cuda_stream = 0
+
+    def wait_event(self, ev):
+        pass
+
+
+class _HostEvent(object):
+    """Stand-in for a HIP event on the host path: always complete, no timing."""
+
+    def record(self, stream=None):
+        pass
+
+    def query(self):
+        return True
+
+    def synchronize(self):
+        pass
+
+    def elapsed_time(self, other):
+        return 0.0
+
+
 class ShardedRunner(object):
     """Runs `compute(inp, out, n)` on this rank's shard of a global batch and gathers.
 
     compute   callable writing outputs for the first n frames of `inp` into `out`
     in_shape  per-frame input shape, out_shape per-frame output shape
+
+    Pipelined form (launch_detections / finish_detections): with the default gather_mode
+    "deferred", finish_detections(handle of step k) returns step k - 1's detections (None for
+    the first step) — the size exchange of a step is read on the host one finish later — and
+    flush_detections() returns the last step's; "sized" and "fixed" return step k's own.  A
+    caller collecting results in order therefore appends every non-None finish and then the
+    flush (tests/test_dist_cpu.py::test_pipelined_runner_deferred_order_gloo).
     """
 
     def __init__(self, compute, global_batch, in_shape, out_shape, device, dtype=torch.float32, timing=True,
@@ -348,33 +380,38 @@ class ShardedRunner(object):
         only for that forward, so step k's postprocessing runs beside step k+1's first
         layers.  Returns a handle for finish_detections."""
         dev = self.out.device
+        host = dev.type != "cuda"
         if not hasattr(self, "_outs"):
             self._outs = [self.out] + [torch.zeros_like(self.out) for _ in range(self.slots - 1)]
             # high-priority streams: HIP gives each its own hardware queue (GPU_MAX_HW_QUEUES
             # = 4 normal queues are shared round-robin by torch's stream pool, RCCL's internal
             # streams and the null stream; tools/stream_queue_probe.py), so neither the
             # postprocess nor the gather can end up serialised behind later forwards
-            self._side = torch.cuda.Stream(dev, priority=-1)
-            self._post = torch.cuda.Stream(dev, priority=-1)
+            self._side = _HostStream() if host else torch.cuda.Stream(dev, priority=-1)
+            self._post = _HostStream() if host else torch.cuda.Stream(dev, priority=-1)
             self._freed = [None] * self.slots
             self._gather = None
             self._deferred = None
             self.reset_stats()
-        cur = torch.cuda.current_stream(dev)
+        cur = _HostStream() if host else torch.cuda.current_stream(dev)
         if self._freed[slot] is not None:
             cur.wait_event(self._freed[slot])
         # ev: 0/1 forward, 2 pack done, 3 gather enqueued (deferred: the size exchange), 4 gather
         # done, 5 payload gather start (deferred mode; the same point as 3 otherwise)
-        ev = [torch.cuda.Event(enable_timing=self.timing) for _ in range(6)]
+        ev = [_HostEvent() if host else torch.cuda.Event(enable_timing=self.timing) for _ in range(6)]
         out = self._outs[slot]
         ev[0].record(cur)
         self.compute(local_in, out, self.count)
         ev[1].record(cur)
         self._post.wait_event(ev[1])
-        with torch.cuda.stream(self._post):
+        with self._on(self._post):
             packed, total, counts = post(out, self.count, slot, self._post.cuda_stream)
             ev[2].record(self._post)
         return slot, packed, total, counts, ev
+
+    @staticmethod
+    def _on(stream):
+        return _nullcontext() if isinstance(stream, _HostStream) else torch.cuda.stream(stream)
 
     def finish_detections(self, handle):
         """Second half, called once the next inflight - 1 steps have been launched (three by
@@ -400,14 +437,14 @@ class ShardedRunner(object):
             # waits for this step's pack; then this step's size exchange
             prev, self._deferred = self._deferred, None
             r = self._complete(prev) if prev is not None else None
-            with torch.cuda.stream(self._side):
+            with self._on(self._side):
                 self._side.wait_event(ev[2])
                 ev[3].record(self._side)
                 ha = self._gather.launch_meta(slot, packed, total, counts, self.count)
             self._deferred = (ha, ev, slot)
             self._host_blocked += time.perf_counter() - t0
             return r
-        with torch.cuda.stream(self._side):
+        with self._on(self._side):
             self._side.wait_event(ev[2])
             ev[3].record(self._side)
             ev[5].record(self._side)
@@ -423,7 +460,7 @@ class ShardedRunner(object):
         """deferred mode: the payload gather of a step whose size exchange was enqueued one
         finish earlier, then (rank 0) its detections."""
         ha, ev, slot = deferred
-        with torch.cuda.stream(self._side):
+        with self._on(self._side):
             ev[5].record(self._side)
             gh = self._gather.launch_payload(ha)
             ev[4].record(self._side)

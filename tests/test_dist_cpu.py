@@ -149,3 +149,90 @@ def test_sharded_detection_gather_gloo(world, total, mode):
     assert root[1] is True and root[2] > 10
     others = [r for r in res if r[1] is None]
     assert len(others) == world - 1 and all(r[2] is True for r in others)
+
+
+def _pipe_worker(rank, world, port, total, steps, q):
+    for p in (REPO, PKG, ORACLE):
+        sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import dist as Dw
+    import post_numpy as PN
+    Dw.init("gloo")
+    try:
+        max_det = 64
+        batches = []
+        for k in range(steps):
+            rng = np.random.default_rng(100 + k)
+            batches.append(np.stack([PN.synthetic_predictions(rng, n_hot=(i * 5 + k * 3) % 40) for i in range(total)]))
+
+        def compute(inp, out, n):
+            out[:n] = inp[:n]
+
+        def post(out, n, slot, stream_ptr):  # the pipelined post signature (bench.py: the HIP post + pack)
+            packed = np.zeros(out.shape[0] * max_det, Dw.DETECTION_DTYPE)
+            counts = np.zeros(out.shape[0], np.int32)
+            p = 0
+            for i in range(n):
+                rows = PN.detect(out[i].numpy())
+                counts[i] = len(rows)
+                for (c, l, t, r, b, sc) in rows:
+                    packed[p] = (c, sc, l, t, r, b)
+                    p += 1
+            return (torch.from_numpy(packed.view(np.uint8).reshape(-1, 40)), torch.tensor([p], dtype=torch.int32),
+                    torch.from_numpy(counts))
+
+        runner = Dw.ShardedRunner(compute, total, (13, 13, 125), (13, 13, 125), device="cpu")
+        assert runner.gather_mode == "deferred" and runner.inflight == runner.slots - 1
+        pending, got, firsts = [], [], []
+        for k in range(steps):  # bench.py's loop: finish step k - inflight + 1 after launching step k
+            pending.append(runner.launch_detections(torch.from_numpy(runner.local_slice(batches[k])), post,
+                                                    k % runner.slots))
+            if len(pending) == runner.inflight:
+                r = runner.finish_detections(pending.pop(0))
+                firsts.append(r is None)
+                if r is not None:
+                    got.append(r)
+        while pending:
+            r = runner.finish_detections(pending.pop(0))
+            firsts.append(r is None)
+            if r is not None:
+                got.append(r)
+        r = runner.flush_detections()
+        if r is not None:
+            got.append(r)
+        if rank == 0:
+            expect = [[[(c, l, t, rr, b, float(np.float32(sc))) for c, l, t, rr, b, sc in PN.detect(p)] for p in bt]
+                      for bt in batches]
+            q.put(("ok", [Dw.unpack_detections(*g) for g in got] == expect, (len(got), firsts[0], sum(firsts))))
+        else:
+            q.put(("ok", None, (len(got), sum(firsts))))
+    except Exception as e:  # pragma: no cover
+        import traceback
+        q.put(("err", traceback.format_exc(), None))
+    finally:
+        torch.distributed.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,total,steps", [(2, 7, 6), (8, 11, 5)])
+def test_pipelined_runner_deferred_order_gloo(world, total, steps):
+    """ShardedRunner's pipelined path with its default gather ("deferred"): driven as
+    bench.py drives it (launch step k into slot k % slots, finish the oldest once `inflight` steps
+    are pending, then drain and flush), rank 0 receives every step's detections exactly once and
+    in step order: the first finish returns nothing (its sizes are read one finish later) and
+    flush_detections() returns the last step; non-root ranks receive nothing."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_pipe_worker, args=(r, world, port, total, steps, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+    assert all(r[0] == "ok" for r in res), res
+    root = [r for r in res if r[1] is not None][0]
+    assert root[1] is True
+    n_got, first_none, n_none = root[2]
+    assert n_got == steps and first_none and n_none == 1
+    others = [r for r in res if r[1] is None]
+    assert len(others) == world - 1 and all(r[2] == (0, steps) for r in others)

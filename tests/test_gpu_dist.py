@@ -95,3 +95,57 @@ def test_bench_under_torchrun_world1_rccl():
     pr = d["per_rank"]
     assert len(pr) == 1 and pr[0]["forward_ms"] > 0 and pr[0]["gather_ms"] >= 0
     assert d["postprocess"]["detections_last_step"] > 0
+
+
+@pytest.mark.gpu
+def test_bench_eight_ranks_batch64_detections_match_single_process(tmp_path):
+    """BASELINE config 4 at its real per-rank batch, rehearsed on one GPU: `bench.py --gpus 8
+    --batch 64` (8 ranks x 64 frames = 512, each rank's own device plan, weight arena by
+    broadcast, on-GPU postprocessing, packed detections gathered to rank 0; gloo host-staged
+    collectives stand in for RCCL).  Rank 0's gathered detections of the last step equal, byte
+    for byte, a single process running the same 512 frames (the ranks' seeded frames) through
+    one batch-64 plan shard by shard, postprocessing and packing each shard: batch rows are
+    bit-identical whatever the shard, and the gather keeps (rank, image) order."""
+    import numpy as np
+    import torch
+
+    import dnn_hip
+    import synth
+    import yolo_graph
+    import yolo_post
+    dump = str(tmp_path / "dets.npz")
+    env = dict(os.environ, DNN_BENCH_SHARED_GPU="1", DNN_BENCH_BACKEND="gloo")
+    cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "8", "--batch", "64", "--steps", "2",
+           "--warmup", "1", "--preheat", "0", "--sustained", "0", "--no-cpu", "--no-latency", "--no-e2e",
+           "--no-fp16", "--no-unfused", "--no-fp32-mfma", "--dump-detections", dump]
+    r = subprocess.run(cmd, env=env, cwd=REPO, capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert d["n_gpus"] == 8 and d["config"]["global_batch"] == 512 and len(d["per_rank"]) == 8
+    got = np.load(dump)
+    assert got["counts"].shape == (512,)
+
+    dev = torch.device("cuda", 0)
+    B = 64
+    ws = synth.yolo_weights()
+    g, _ = yolo_graph.build_graph(dnn_hip.DnnGraphBuilder, ws, in_shape=(B, 416, 416, 3))
+    plan = dnn_hip.Plan.from_graph(g, device=0)
+    out = torch.empty((B, 13, 13, 125), device=dev)
+    db = yolo_post.DetectionBuffers(B, dev)
+    s = torch.cuda.current_stream(dev).cuda_stream
+    dets, counts = [], []
+    for rank in range(8):
+        gen = torch.Generator(device=dev)
+        gen.manual_seed(1234 + rank)  # bench.py's frames of this rank
+        frames = torch.rand((B, 416, 416, 3), generator=gen, device=dev, dtype=torch.float32)
+        plan.run_device(B, frames.data_ptr(), out.data_ptr(), s)
+        db.run(out.data_ptr(), B, s)
+        packed, total, cnt = db.pack(B, s)
+        torch.cuda.synchronize()
+        dets.append(packed[:int(total.item())].cpu().numpy())
+        counts.append(cnt[:B].cpu().numpy())
+    plan.close()
+    want_d, want_c = np.concatenate(dets, 0), np.concatenate(counts).astype(np.int32)
+    assert np.array_equal(got["counts"], want_c)
+    assert int(np.clip(want_c, 0, None).sum()) > 0 and got["dets"].shape == want_d.shape
+    assert got["dets"].tobytes() == want_d.tobytes()

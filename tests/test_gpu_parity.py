@@ -1041,6 +1041,68 @@ def test_x3_ktile_conv3_shape_vs_oracle(B):
             assert np.array_equal(one.run(x[f:f + 1]), y[f:f + 1]), f
 
 
+KTILE_SHAPE_CASES = [
+    # B, H, W, C, OC, pool (0 none, 1 2x2/s2, 2 2x2/s1 SAME fused): frames the K-split kernel's
+    # shape table (kernels_x3.hip x3_ktile_shape) accepts beyond YOLO's -- partial 13- / 14- / 26-wide
+    # tiles, odd frames under the stride-1 pool, output widths 64 and 192
+    (2, 9, 11, 256, 192, 2),
+    (1, 13, 13, 256, 64, 0),
+    (2, 18, 18, 128, 64, 1),
+    (1, 20, 24, 128, 128, 0),
+    (2, 30, 38, 64, 128, 1),
+]
+
+
+@pytest.mark.parametrize("case", KTILE_SHAPE_CASES)
+def test_x3_ktile_shapes_vs_oracle(case):
+    """conv3x3_x3_ktile_kernel on every shape class it accepts at non-YOLO frame sizes: within the
+    fp32 tolerance of the float64 oracle, repeat runs identical, multi-frame rows equal to one-frame
+    runs."""
+    B, H, W, C, OC, pool = case
+    rng = np.random.default_rng(H * 100 + W + C + OC)
+    x = rng.standard_normal((B, H, W, C)).astype(np.float32)
+    k = (rng.standard_normal((3, 3, C, OC)) * np.sqrt(2.0 / (9 * C))).astype(np.float32)
+    b = rng.standard_normal(OC).astype(np.float32) * 0.1
+    gam = rng.uniform(0.5, 1.5, OC).astype(np.float32)
+    gam[::5] *= -1
+    n = (rng.standard_normal(OC).astype(np.float32) * 0.1, rng.uniform(0.5, 1.5, OC).astype(np.float32), gam)
+    pstride = [1, 2, 2, 1] if pool == 1 else [1, 1, 1, 1]
+
+    def graph(shape):
+        g = dnn_hip.DnnGraphBuilder()
+        y = g.create_input(list(shape))
+        y = g.create_max_pool2d(y, [1, 2, 2, 1], [1, 1, 1, 1], "SAME")  # an x3 producer (split planes)
+        y = g.create_conv2d(y, k, [1, 1, 1, 1], "SAME")
+        y = g.create_bias_add(y, b)
+        y = g.create_batch_norm(y, *n, 1e-5)
+        y = g.create_leaky_relu(y)
+        if pool:
+            y = g.create_max_pool2d(y, [1, 2, 2, 1], pstride, "SAME")
+        g.set_out_node(y)
+        return g
+
+    ref = R.max_pool2d(x, [1, 2, 2, 1], [1, 1, 1, 1], "SAME")
+    ref = R.leaky_relu(R.batch_norm(R.bias_add(R.conv2d(ref, k), b), *n, 1e-5))
+    if pool:
+        ref = R.max_pool2d(ref, [1, 2, 2, 1], pstride, "SAME")
+    eng = dnn_hip.DnnInferenceEngine(graph(x.shape), False, latency=True)
+    desc = eng.plan().describe()
+    conv = [ln for ln in desc.splitlines() if ln.startswith("conv")]
+    assert "mode=x3_ktile" in conv[0], desc
+    if pool:
+        assert ("+pool2x2s2" if pool == 1 else "+pool2x2s1") in conv[0], desc
+    y = eng.run(x)
+    assert y.shape == ref.shape
+    assert np.array_equal(eng.run(x), y)
+    err = R.normwise_err(y, ref)
+    print("ktile shape", case, "err %.3g" % err)
+    assert err < LAYER_TOL, err
+    if B > 1:
+        one = dnn_hip.DnnInferenceEngine(graph((1,) + x.shape[1:]), False, latency=True)
+        for f in range(B):
+            assert np.array_equal(one.run(x[f:f + 1]), y[f:f + 1]), f
+
+
 X3_LAT_CASES = [
     # B, H, W, C, od1, od2, forced chunks per workgroup (DNN_HIP_X3L_CPW) or None, 1x1 outputs
     # or None: pool (2x2 s1) -> conv3x3 C->od1 -> conv3x3 od1->od2 [-> conv1x1 + bias] in a

@@ -14,6 +14,18 @@ python3 tools/prof_summary.py --skip 3 --unfused --trace $D/unf_trace/unf_trace_
 python3 tools/prof_summary.py --skip 3 --fp16 --trace $D/f16_trace/f16_trace_kernel_trace.csv \
   --fetch $D/f16_fetch/f16_fetch_counter_collection.csv --write $D/f16_write/f16_write_counter_collection.csv \
   --note "round ${R#r}: fp16 plan (BASELINE config 5), MI355X" --out $P/pmc_summary_fp16.json
+# the bench line of the SAME gpurun call (same box) beside the trace: its HIP-event duration of the
+# dominant kernel, fraction and img/s (bench.py reports them as roofline.rocprof_same_box)
+python3 - "$B/bench.json" "$P/pmc_summary.json" <<'EOF'
+import json, sys
+b = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
+p = json.load(open(sys.argv[2]))
+r = b["roofline"]
+p["same_box"] = {"images_per_s": b["value"], "ms_per_step": b["ms_per_step"], "dominant_kernel": r["kernel"],
+                 "dominant_event_ms": r["avg_launch_ms"], "event_frac": r["frac"],
+                 "note": "bench.py line of the same gpurun call (same box) as this trace"}
+json.dump(p, open(sys.argv[2], "w"), indent=1)
+EOF
 cp $D/fused_trace/fused_trace_kernel_stats.csv $P/${R}_rocprof_kernel_stats.csv
 cp $D/unf_trace/unf_trace_kernel_stats.csv $P/${R}_rocprof_kernel_stats_unfused.csv
 cp $D/f16_trace/f16_trace_kernel_stats.csv $P/${R}_rocprof_kernel_stats_fp16.csv

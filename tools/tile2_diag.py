@@ -1,0 +1,123 @@
+"""Where conv2 / conv3's time goes (conv3x3_x3_tile2_kernel, X3DIAG bit 1024 builds:
+tools/build_diag.sh 1024, DNN_HIP_LIB=diag/libdnn_hip_d1024.so).  Runs the batch-64 fp32 plan back
+to back for --preheat seconds, then reads the last launch's per-workgroup stamps of each layer
+(gemm_x3_patch.h T2_DIAG_SLOTS) and prints the median cycles per phase, the launch span, and per
+CU: workgroups, busy fraction (union of its workgroups' [start, end] over the span) and mean
+concurrency (sum of durations over its busy time)."""
+import argparse
+import ctypes
+import os
+import statistics
+import sys
+import time
+
+R = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(R, "dnn-inference-engine_amd"))
+
+import torch  # noqa: E402
+
+import dnn_hip  # noqa: E402
+import synth  # noqa: E402
+import yolo_graph  # noqa: E402
+
+WGS, SLOTS = 4096, 8
+
+
+def layer_report(name, rows):
+    if not rows:
+        print(name, ": no stamps")
+        return
+    print("%s: %d workgroups (wave 0, median cycles)" % (name, len(rows)))
+    for nm, a, b in (("prologue (patch landed)", 1, 2), ("MFMA loop", 2, 3), ("epilogue + stores", 3, 4),
+                     ("total", 1, 4)):
+        v = [r[b] - r[a] for r in rows]
+        print("  %-24s %8.0f  (p10 %6.0f, p90 %6.0f)" % (nm, statistics.median(v), sorted(v)[len(v) // 10],
+                                                          sorted(v)[len(v) * 9 // 10]))
+    t0 = min(r[0] for r in rows)
+    t1 = max(r[5] for r in rows)
+    span = (t1 - t0) * 10e-3  # s_memrealtime: 100 MHz -> us
+    cyc = statistics.median([(r[4] - r[1]) / max(r[5] - r[0], 1) for r in rows]) * 100  # MHz
+    last_start = max(r[0] for r in rows)
+    print("  launch span %.1f us (stamped), clock ~%.0f MHz, last workgroup starts at %.1f us" %
+          (span, cyc, (last_start - t0) * 10e-3))
+    cus = {}
+    for r in rows:
+        hw, xcc = r[6], r[7] & 0xf
+        key = (xcc, (hw >> 8) & 0xff)
+        cus.setdefault(key, []).append((r[0], r[5]))
+    busy, conc, nwg = [], [], []
+    for iv in cus.values():
+        iv.sort()
+        u, cs, ce = 0, None, None
+        for s, e in iv:
+            if ce is None or s > ce:
+                if ce is not None:
+                    u += ce - cs
+                cs, ce = s, e
+            else:
+                ce = max(ce, e)
+        u += ce - cs
+        busy.append(u / max(t1 - t0, 1))
+        conc.append(sum(e - s for s, e in iv) / max(u, 1))
+        nwg.append(len(iv))
+    print("  CUs %d: workgroups/CU median %d (min %d, max %d); busy %.2f (min %.2f); concurrency %.2f" %
+          (len(cus), statistics.median(nwg), min(nwg), max(nwg), statistics.median(busy), min(busy),
+           statistics.median(conc)))
+    # start-time histogram in tenths of the span
+    h = [0] * 10
+    for r in rows:
+        h[min(9, int(10 * (r[0] - t0) / max(t1 - t0, 1)))] += 1
+    print("  starts per tenth of span:", h)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--preheat", type=float, default=2.0)
+    ap.add_argument("--batch", type=int, default=64)
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    ws = synth.yolo_weights()
+    g, _ = yolo_graph.build_graph(dnn_hip.DnnGraphBuilder, ws, in_shape=(a.batch, 416, 416, 3))
+    entries = dnn_hip.lower_graph(g)
+    wb, sb = dnn_hip.Plan.memory(a.batch, (416, 416, 3), entries)
+    wbuf = torch.empty(wb, dtype=torch.uint8, device=dev)
+    sbuf = torch.empty(sb, dtype=torch.uint8, device=dev)
+    plan = dnn_hip.Plan(a.batch, (416, 416, 3), entries, device=0, weights_ptr=wbuf.data_ptr(),
+                        workspace_ptr=sbuf.data_ptr())
+    x = torch.rand((a.batch, 416, 416, 3), device=dev)
+    y = torch.empty((a.batch, 13, 13, 125), device=dev)
+    s = torch.cuda.Stream()
+    t0 = time.time()
+    n = 0
+    while time.time() - t0 < a.preheat:
+        for _ in range(10):
+            plan.run_device(a.batch, x.data_ptr(), y.data_ptr(), s.cuda_stream)
+        n += 10
+        s.synchronize()
+    plan.timing_begin(3)
+    for _ in range(3):
+        plan.run_device(a.batch, x.data_ptr(), y.data_ptr(), s.cuda_stream)
+    ms, cnt = plan.timing_end()
+    print("forwards %d" % n)
+    for k, m, c in zip(plan.kernels(), ms, cnt):
+        print("  %-14s %.4f ms" % (k["name"], m / max(c, 1)))
+    fn = getattr(plan.lib, "dnn_tile2_diag_stamps", None)
+    if fn is None:
+        print("no dnn_tile2_diag_stamps: not an X3DIAG 1024 build")
+        return
+    fn.restype = ctypes.c_int
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    nw = 2 * WGS * SLOTS
+    buf = (ctypes.c_ulonglong * nw)()
+    assert fn(buf, nw) == 0
+    for li, name in enumerate(("conv2 (N = 64)", "conv3 (N = 128)")):
+        rows = []
+        for wg in range(WGS):
+            v = list(buf[(li * WGS + wg) * SLOTS:(li * WGS + wg + 1) * SLOTS])
+            if v[5] > 0 and v[4] > 0:
+                rows.append(v)
+        layer_report(name, rows)
+
+
+if __name__ == "__main__":
+    main()
