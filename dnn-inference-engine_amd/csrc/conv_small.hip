@@ -324,7 +324,9 @@ conv0_packed_pool_kernel(const float* __restrict__ in, const float* __restrict__
     const int b = cur.b, y0 = cur.ty * SC_T, x0 = cur.tx * SC_T;
     cur = nxt;
     nxt = nn;
-    // pool + epilogue into the wave's LDS stage, then 16-B coalesced stores
+    // pool + epilogue into the wave's LDS stage (the four windows' divisions behind one
+    // wave-uniform check: pool_epilogue_batch), then 16-B coalesced stores
+    f32x4 pv[4][1];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       f32x4 v = acc[i];
@@ -333,10 +335,15 @@ conv0_packed_pool_kernel(const float* __restrict__ in, const float* __restrict__
         const bool x1 = 2 * wx + 1 < g.OW, y1 = 2 * wy + 1 < g.OH;
         v = f32x4{acc[i][0], x1 ? acc[i][1] : acc[i][0], y1 ? acc[i][2] : acc[i][0], x1 && y1 ? acc[i][3] : acc[i][0]};
       }
-      if constexpr ((C0DIAG & 2) != 0)
-        stage[wid][i >> 1][4 * (i & 1) + fp][n] = v[0] + v[1] + v[2] + v[3];
-      else
-        stage[wid][i >> 1][4 * (i & 1) + fp][n] = pool_then_epilogue_t<FL>(v, pb_, pm, ps, pg, epi.flags);
+      pv[i][0] = v;
+    }
+    if constexpr ((C0DIAG & 2) != 0) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) stage[wid][i >> 1][4 * (i & 1) + fp][n] = pv[i][0][0] + pv[i][0][1] + pv[i][0][2] + pv[i][0][3];
+    } else {
+      const float cb[1] = {pb_}, cm[1] = {pm}, cs[1] = {ps}, cg[1] = {pg};
+      pool_epilogue_batch<FL>(pv, cb, cm, cs, cg, epi.flags,
+                              [&](int i, int, float e) { stage[wid][i >> 1][4 * (i & 1) + fp][n] = e; });
     }
     wait_lgkm0();  // the stage is wave-private
     {  // one 16-B store per lane (2 window rows x 8 windows x 16 channels per wave)

@@ -434,6 +434,82 @@ __device__ __forceinline__ float pool_then_epilogue_t(f32x4 v, float pb, float p
   return apply_epilogue_t<FL>(dec ? lo : hi, pb, pm, ps, pg, flags);
 }
 
+// The epilogue of NV x NC values (NC columns, their parameters per column) in place, with ONE
+// wave-uniform check for all of their divisions: div_rn's fallback branch per value made every
+// value's chain a basic block of its own (a conv2 tile's 14 pooled values per lane took 4.2 k
+// cycles, tile2 stamps).  Same operations per value as apply_epilogue_t, so the same bits.
+template <int FL, int NV, int NC>
+__device__ __forceinline__ void epilogue_batch(float (&v)[NV][NC], const float (&pb)[NC], const float (&pm)[NC],
+                                               const float (&ps)[NC], const float (&pg)[NC], int flags) {
+  if constexpr (FL < 0 || (FL & EPI_BN) == 0) {
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+#pragma unroll
+      for (int i = 0; i < NV; ++i) v[i][c] = apply_epilogue_t<FL>(v[i][c], pb[c], pm[c], ps[c], pg[c], flags);
+  } else {
+    float x[NV][NC];
+    bool bad = false;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const double y = 1.0 / (double)ps[c];
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        float t = v[i][c];
+        if constexpr ((FL & EPI_BIAS) != 0) t = t + pb[c];
+        x[i][c] = t - pm[c];
+        v[i][c] = (float)((double)x[i][c] * y);
+        bad = bad || __builtin_amdgcn_classf(v[i][c], 0x0F0);
+      }
+    }
+    if (__builtin_amdgcn_ballot_w64(bad)) {  // +-0, +-denormal quotients: the IEEE division
+#pragma unroll
+      for (int c = 0; c < NC; ++c)
+#pragma unroll
+        for (int i = 0; i < NV; ++i)
+          if (__builtin_amdgcn_classf(v[i][c], 0x0F0)) v[i][c] = x[i][c] / ps[c];
+    }
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        float t = v[i][c] * pg[c];
+        if constexpr ((FL & EPI_BN_AB) != 0) t = t * pm[c] - ps[c];
+        if constexpr ((FL & EPI_LEAKY_F64) != 0) t = t < 0.f ? (float)(0.1 * (double)t) : t;
+        if constexpr ((FL & EPI_LEAKY_F32) != 0) {
+          const float u = t * 0.1f;
+          t = t > u ? t : u;
+        }
+        v[i][c] = t;
+      }
+  }
+}
+
+// pool_then_epilogue_t over NV windows x NC columns (the window's max, or min for a decreasing
+// channel, then epilogue_batch); put(i, c, value)
+template <int FL, int NV, int NC, typename F>
+__device__ __forceinline__ void pool_epilogue_batch(const f32x4 (&acc)[NV][NC], const float (&pb)[NC],
+                                                    const float (&pm)[NC], const float (&ps)[NC],
+                                                    const float (&pg)[NC], int flags, F&& put) {
+  float t[NV][NC];
+  const int f = FL < 0 ? flags : FL;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const bool dec = ((f & EPI_BN) && pg[c] < 0.f) || ((f & EPI_BN_AB) && pm[c] < 0.f);
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const f32x4 v = acc[i][c];
+      const float hi = __builtin_fmaxf(__builtin_fmaxf(v[0], v[1]), __builtin_fmaxf(v[2], v[3]));
+      const float lo = __builtin_fminf(__builtin_fminf(v[0], v[1]), __builtin_fminf(v[2], v[3]));
+      t[i][c] = dec ? lo : hi;
+    }
+  }
+  epilogue_batch<FL>(t, pb, pm, ps, pg, flags);
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+#pragma unroll
+    for (int i = 0; i < NV; ++i) put(i, c, t[i][c]);
+}
+
 __device__ __forceinline__ float pool_then_epilogue(f32x4 v, float pb, float pm, float ps, float pg, int flags) {
   const bool dec = ((flags & EPI_BN) && pg < 0.f) || ((flags & EPI_BN_AB) && pm < 0.f);
   const float hi = __builtin_fmaxf(__builtin_fmaxf(v[0], v[1]), __builtin_fmaxf(v[2], v[3]));

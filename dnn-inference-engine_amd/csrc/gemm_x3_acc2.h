@@ -289,18 +289,14 @@ conv3x3_x3_acc2_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __rest
     if (g.out_mode == 1) {  // staged 16-B split-plane stores (x3_pool_split_store)
       static_assert(1024 + NW * TM * 4 * X3_STG_ROW * 4 <= 2 * BUFB && BM <= 1024, "stage");
       float* stg = reinterpret_cast<float*>(smem + 1024) + wid * (TM * 4 * X3_STG_ROW);
+      float pb[NJ], pm[NJ], ps[NJ], pg[NJ];
 #pragma unroll
       for (int jb = 0; jb < NJ; ++jb) {
-        const int f = FL < 0 ? epi.flags : FL;
-        const int n = n0 + 16 * jb + fr;
-        const float pb = (f & EPI_BIAS) ? epi.bias[n] : 0.f;
-        const float pm = (f & (EPI_BN | EPI_BN_AB)) ? epi.mean[n] : 0.f;
-        const float ps = (f & (EPI_BN | EPI_BN_AB)) ? epi.sq[n] : 1.f;
-        const float pg = (f & EPI_BN) ? epi.gamma[n] : 1.f;
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-          stg[(4 * i + fq) * X3_STG_ROW + 16 * jb + fr] = pool_then_epilogue_t<FL>(accm[i][jb], pb, pm, ps, pg, epi.flags);
+        const X3EpiCol ec = x3_epi_col(epi, FL < 0 ? epi.flags : FL, n0 + 16 * jb + fr);
+        pb[jb] = ec.pb, pm[jb] = ec.pm, ps[jb] = ec.ps, pg[jb] = ec.pg;
       }
+      pool_epilogue_batch<FL>(accm, pb, pm, ps, pg, epi.flags,
+                              [&](int i, int jb, float v) { stg[(4 * i + fq) * X3_STG_ROW + 16 * jb + fr] = v; });
       x3_pool_split_store<TM>(stg, orow, BM / 4, 0, out_split, 3 * (size_t)N, (n0 >> 5) * 96, lane);
       return;
     }
@@ -356,14 +352,16 @@ conv3x3_x3_acc2_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __rest
   const int rr = lane >> 2, c8 = 8 * (lane & 3);
   static_for<0, TM>([&](auto ic) {
     constexpr int i = decltype(ic)::value;
+    float v[4][NJ];
 #pragma unroll
     for (int jb = 0; jb < NJ; ++jb)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float v = accm[i][jb][r];
-        stg[(4 * fq + r) * 36 + 16 * jb + fr] =
-            g.out_mode == 2 ? v : apply_epilogue_t<FL>(v, pb[jb], pm[jb], ps[jb], pg[jb], epi.flags);
-      }
+      for (int r = 0; r < 4; ++r) v[r][jb] = accm[i][jb][r];
+    if (g.out_mode != 2) epilogue_batch<FL>(v, pb, pm, ps, pg, epi.flags);
+#pragma unroll
+    for (int jb = 0; jb < NJ; ++jb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) stg[(4 * fq + r) * 36 + 16 * jb + fr] = v[r][jb];
     wait_lgkm0();
     const f32x4 lo = *reinterpret_cast<const f32x4*>(stg + rr * 36 + c8);
     const f32x4 hi = *reinterpret_cast<const f32x4*>(stg + rr * 36 + c8 + 4);

@@ -250,6 +250,8 @@ conv3x3_x3_ktile_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __res
         const int lx1 = xx + 1 < g.W ? lx + 1 : lx, ly1 = y + 1 < g.H ? ly + 1 : ly;
         const int ra = ly * TW + lx, rb = ly * TW + lx1, rc = ly1 * TW + lx, rd = ly1 * TW + lx1;
         float o[8];
+        f32x4 win[1][8];
+        float cb[8], cm[8], cs[8], cg[8];
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
           const f32x4 va = *reinterpret_cast<const f32x4*>(stg + ra * 36 + c8 + 4 * h);
@@ -257,10 +259,12 @@ conv3x3_x3_ktile_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __res
           const f32x4 vc = *reinterpret_cast<const f32x4*>(stg + rc * 36 + c8 + 4 * h);
           const f32x4 vd = *reinterpret_cast<const f32x4*>(stg + rd * 36 + c8 + 4 * h);
 #pragma unroll
-          for (int e = 0; e < 4; ++e)
-            o[4 * h + e] = pool_then_epilogue_t<FL>(f32x4{va[e], vb[e], vc[e], vd[e]}, p1[0][h][e], p1[1][h][e],
-                                                    p1[2][h][e], p1[3][h][e], epi.flags);
+          for (int e = 0; e < 4; ++e) {
+            win[0][4 * h + e] = f32x4{va[e], vb[e], vc[e], vd[e]};
+            cb[4 * h + e] = p1[0][h][e], cm[4 * h + e] = p1[1][h][e], cs[4 * h + e] = p1[2][h][e], cg[4 * h + e] = p1[3][h][e];
+          }
         }
+        pool_epilogue_batch<FL>(win, cb, cm, cs, cg, epi.flags, [&](int, int c, float e) { o[c] = e; });
         if (g.out_mode == 1) {
           const size_t op = ((size_t)b * (g.H + 2) + y + 1) * (size_t)Wp + xx + 1;
           u32x4 q[3];
@@ -289,13 +293,10 @@ conv3x3_x3_ktile_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __res
   if constexpr (POOL) {
     if (g.out_mode == 1) {  // staged 16-B split-plane stores (x3_pool_split_store), group 0's waves
       float* stg = reinterpret_cast<float*>(smem + RED) + wg * (TM * 4 * X3_STG_ROW);  // (past `red`)
-#pragma unroll
-      for (int jb = 0; jb < 2; ++jb) {
-        const float pb = ecp[jb].pb, pm = ecp[jb].pm, ps = ecp[jb].ps, pg = ecp[jb].pg;
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-          stg[(4 * i + fq) * X3_STG_ROW + 16 * jb + fr] = pool_then_epilogue_t<FL>(acc[i][jb], pb, pm, ps, pg, epi.flags);
-      }
+      const float cb[2] = {ecp[0].pb, ecp[1].pb}, cm[2] = {ecp[0].pm, ecp[1].pm}, cs[2] = {ecp[0].ps, ecp[1].ps},
+                  cg[2] = {ecp[0].pg, ecp[1].pg};
+      pool_epilogue_batch<FL>(acc, cb, cm, cs, cg, epi.flags,
+                              [&](int i, int jb, float v) { stg[(4 * i + fq) * X3_STG_ROW + 16 * jb + fr] = v; });
       x3_pool_split_store<TM>(stg, orow, NO, 4 * wm * TM, out_split, 3 * (size_t)N, (n0 >> 5) * 96, lane);
       KT_STAMP(3)
       return;

@@ -48,15 +48,21 @@ __device__ unsigned long long c16_diag_stamps[C16_DIAG_WGS * C16_DIAG_SLOTS];
 
 #if (X3DIAG & 1024) != 0  // conv3x3_x3_tile2_kernel phase stamps
 constexpr int T2_DIAG_WGS = 4096;
-constexpr int T2_DIAG_SLOTS = 8;
-// [layer (0: N = 64, 1: wider)][workgroup][slot], wave 0: 0 s_memrealtime at start, 1-4 s_memtime at
-// start, patch landed, MFMAs done, end; 5 s_memrealtime at end; 6 HW_ID; 7 XCC_ID
+constexpr int T2_DIAG_SLOTS = 16;
+// [layer (0: N = 64, 1: wider)][workgroup][slot], wave 0 unless noted: 0 s_memrealtime at start,
+// 1-4 s_memtime at start, patch landed, MFMAs done, end; 5 s_memrealtime at end; 6 HW_ID; 7
+// XCC_ID; 8-11 s_memtime when wave 0-3 finished its MFMAs; 12 after the epilogue's first barrier,
+// 13 after the row-table barrier, 14 after the pooled values are staged
 __device__ unsigned long long tile2_diag_stamps[2 * T2_DIAG_WGS * T2_DIAG_SLOTS];
 #define T2_STAMP(k, v)                                                                               \
   if (threadIdx.x == 0 && blockIdx.x < T2_DIAG_WGS)                                                  \
     tile2_diag_stamps[((N == 64 ? 0 : 1) * T2_DIAG_WGS + blockIdx.x) * T2_DIAG_SLOTS + (k)] = (v);
+#define T2_STAMPW(k, v)                                                                              \
+  if ((threadIdx.x & 63) == 0 && threadIdx.x < 256 && blockIdx.x < T2_DIAG_WGS)                      \
+    tile2_diag_stamps[((N == 64 ? 0 : 1) * T2_DIAG_WGS + blockIdx.x) * T2_DIAG_SLOTS + (k) + (threadIdx.x >> 6)] = (v);
 #else
 #define T2_STAMP(k, v)
+#define T2_STAMPW(k, v)
 #endif
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -428,6 +434,13 @@ conv3x3_x3_c16p_kernel(const float* __restrict__ in, const bf16_bits* __restrict
   const int wm = wave_uniform(threadIdx.x >> 6);
   const int fr = lane & 15, fq = lane >> 4, th = fq >> 1;
   const int Wp = g.W + 2;
+  // the 32 columns' epilogue parameters, into LDS once per workgroup (registers would spill;
+  // a load at each tile's epilogue is a memory round trip there)
+  __shared__ f32x4 epl[32];
+  if (threadIdx.x < 32) {
+    const X3EpiCol c = x3_epi_col(epi, eflags, threadIdx.x);
+    epl[threadIdx.x] = f32x4{c.pb, c.pm, c.ps, c.pg};
+  }
 
   // weights once: the packed [n/16][step][piece][lane][8] block of columns 0-31 is contiguous
   {
@@ -659,18 +672,20 @@ conv3x3_x3_c16p_kernel(const float* __restrict__ in, const bf16_bits* __restrict
     if constexpr (POOL) {
       if (g.out_mode == 1) {  // staged 16-B split-plane stores (x3_pool_split_store)
         float* stgp = reinterpret_cast<float*>(patch) + wm * (TM * 4 * X3_STG_ROW);
+        float epb[2], epm[2], eps[2], epg[2];
 #pragma unroll
         for (int jb = 0; jb < 2; ++jb) {
-          const int n = 16 * jb + fr;
-          const float pb = (eflags & EPI_BIAS) ? epi.bias[n] : 0.f;
-          const float pm = (eflags & (EPI_BN | EPI_BN_AB)) ? epi.mean[n] : 0.f;
-          const float ps = (eflags & (EPI_BN | EPI_BN_AB)) ? epi.sq[n] : 1.f;
-          const float pg = (eflags & EPI_BN) ? epi.gamma[n] : 1.f;
+          const f32x4 e = epl[16 * jb + fr];
+          epb[jb] = e[0], epm[jb] = e[1], eps[jb] = e[2], epg[jb] = e[3];
+        }
+        if constexpr ((X3DIAG & 64) != 0) {  // (diagnostic: no pool / epilogue math)
 #pragma unroll
-          for (int i = 0; i < TM; ++i)
-            stgp[(4 * i + fq) * X3_STG_ROW + 16 * jb + fr] =
-                (X3DIAG & 64) != 0 ? acc[i][jb][0] + pb  // (diagnostic: no pool / epilogue math)
-                                   : pool_then_epilogue_t<FL>(acc[i][jb], pb, pm, ps, pg, epi.flags);
+          for (int jb = 0; jb < 2; ++jb)
+#pragma unroll
+            for (int i = 0; i < TM; ++i) stgp[(4 * i + fq) * X3_STG_ROW + 16 * jb + fr] = acc[i][jb][0] + epb[jb];
+        } else {
+          pool_epilogue_batch<FL>(acc, epb, epm, eps, epg, epi.flags,
+                                  [&](int i, int jb, float v) { stgp[(4 * i + fq) * X3_STG_ROW + 16 * jb + fr] = v; });
         }
         C16_STAMP(5)
         x3_pool_split_store<TM>(stgp, orow, NO, 4 * wm * TM, out_split, 96, 0, lane);
@@ -760,6 +775,12 @@ conv3x3_x3_tile2_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __res
                     NPW <= 24,
                 "shape");
   __shared__ __attribute__((aligned(1024))) unsigned char smem[NBUF * BUFB];
+  // batch tiles: the workgroup's 32 WN columns' epilogue parameters, loaded into LDS at the start
+  // (a load issued at the epilogue is a memory round trip of ~2 k cycles there, tile2 stamps), in
+  // the last buffer's unused tail: the DMA pieces past the patch (NPC) are not issued, and the
+  // LDS stays at two workgroups per CU (conv3's pair fills the 160 KiB exactly)
+  static_assert(TM <= 2 || (NPW * NW - NPC) * 1024 >= 32 * WN * 16, "epilogue parameters in the buffer tail");
+  f32x4* const epl = reinterpret_cast<f32x4*>(smem + NBUF * BUFB - 32 * WN * 16);
 
   const int lane = threadIdx.x & 63;
   const int eflags = FL < 0 ? epi.flags : FL;  // FL: the epilogue flag set compiled in (-1: runtime)
@@ -809,6 +830,7 @@ conv3x3_x3_tile2_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __res
   auto issue_chunk = [&](int c, int buf) {
 #pragma unroll
     for (int k = 0; k < NPW; ++k) {
+      if (wid + NW * k >= NPC) break;  // (wave-uniform: pieces past the patch hold no read row)
       const unsigned U = 64u * (unsigned)(wid + NW * k) + (unsigned)lane;
       unsigned r = U / PU;
       const unsigned u = U - r * PU;
@@ -844,6 +866,12 @@ conv3x3_x3_tile2_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __res
   // small tiles (the single-frame plans): the epilogue parameters with the first operands
   constexpr bool PREP = TM <= 2;
   X3EpiCol ecp[2] = {};
+  if constexpr (!PREP) {
+    if (threadIdx.x < 32 * WN) {
+      const X3EpiCol c = x3_epi_col(epi, eflags, tn * (32 * WN) + threadIdx.x);
+      epl[threadIdx.x] = f32x4{c.pb, c.pm, c.ps, c.pg};
+    }
+  }
   if constexpr (PREP) {
     ecp[0] = x3_epi_col(epi, eflags, n0 + fr);
     ecp[1] = x3_epi_col(epi, eflags, n0 + 16 + fr);
@@ -901,10 +929,12 @@ conv3x3_x3_tile2_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __res
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   T2_STAMP(3, __builtin_amdgcn_s_memtime())
+  T2_STAMPW(8, __builtin_amdgcn_s_memtime())
 
   x3_fold(acc, accc);
   int* orow = reinterpret_cast<int*>(smem);
   __syncthreads();
+  T2_STAMP(12, __builtin_amdgcn_s_memtime())
   constexpr int NO = POOL ? T / 4 : T;
   for (int r = threadIdx.x; r < NO; r += NT) {
     int o;
@@ -920,19 +950,24 @@ conv3x3_x3_tile2_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __res
     orow[r] = o;
   }
   __syncthreads();
+  T2_STAMP(13, __builtin_amdgcn_s_memtime())
   if constexpr (POOL) {
     if (g.out_mode == 1) {  // staged 16-B split-plane stores (x3_pool_split_store)
       static_assert(1024 + NW * TM * 4 * X3_STG_ROW * 4 <= NBUF * BUFB && NO * 4 <= 1024, "stage");
       float* stg = reinterpret_cast<float*>(smem + 1024) + wid * (TM * 4 * X3_STG_ROW);
+      float pb[2], pm[2], ps[2], pg[2];
 #pragma unroll
       for (int jb = 0; jb < 2; ++jb) {
-        const int n = n0 + 16 * jb + fr;
-        const X3EpiCol ec = PREP ? ecp[jb] : x3_epi_col(epi, eflags, n);
-        const float pb = ec.pb, pm = ec.pm, ps = ec.ps, pg = ec.pg;
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-          stg[(4 * i + fq) * X3_STG_ROW + 16 * jb + fr] = pool_then_epilogue_t<FL>(acc[i][jb], pb, pm, ps, pg, epi.flags);
+        X3EpiCol ec = ecp[jb];
+        if constexpr (!PREP) {
+          const f32x4 e = epl[wn * 32 + 16 * jb + fr];
+          ec = X3EpiCol{e[0], e[1], e[2], e[3]};
+        }
+        pb[jb] = ec.pb, pm[jb] = ec.pm, ps[jb] = ec.ps, pg[jb] = ec.pg;
       }
+      pool_epilogue_batch<FL>(acc, pb, pm, ps, pg, epi.flags,
+                              [&](int i, int jb, float v) { stg[(4 * i + fq) * X3_STG_ROW + 16 * jb + fr] = v; });
+      T2_STAMP(14, __builtin_amdgcn_s_memtime())
       x3_pool_split_store<TM>(stg, orow, NO, 4 * wm * TM, out_split, 3 * (size_t)N, (n0 >> 5) * 96, lane);
       T2_STAMP(4, __builtin_amdgcn_s_memtime())
       T2_STAMP(5, __builtin_amdgcn_s_memrealtime())
@@ -942,7 +977,11 @@ conv3x3_x3_tile2_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __res
 #pragma unroll
   for (int jb = 0; jb < 2; ++jb) {
     const int n = n0 + 16 * jb + fr;  // < N: N % (32 WN) == 0 (launcher)
-    const X3EpiCol ec = PREP ? ecp[jb] : x3_epi_col(epi, eflags, n);
+    X3EpiCol ec = ecp[jb];
+    if constexpr (!PREP) {
+      const f32x4 e = epl[wn * 32 + 16 * jb + fr];
+      ec = X3EpiCol{e[0], e[1], e[2], e[3]};
+    }
     const float pb = ec.pb, pm = ec.pm, ps = ec.ps, pg = ec.pg;
     const int cofs = (n >> 5) * 96 + (n & 31);
     auto put = [&](int o, float v) {
@@ -978,5 +1017,6 @@ conv3x3_x3_tile2_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __res
   T2_STAMP(5, __builtin_amdgcn_s_memrealtime())
 }
 #undef T2_STAMP
+#undef T2_STAMPW
 
 }  // namespace dnnhip

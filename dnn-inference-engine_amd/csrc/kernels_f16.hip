@@ -277,7 +277,7 @@ static bool patch16_enabled() {
   return e ? e[0] == '1' : P16_DEFAULT;
 }
 
-// rows of the padded input one BM-row tile spans (tap offsets included)
+// rows of the padded input one bm-row tile spans (tap offsets included)
 static int patch16_span(long long M, int H, int W) {
   const int Wp = W + 2;
   auto padded = [&](long long m) {
@@ -294,8 +294,24 @@ static int patch16_span(long long M, int H, int W) {
   return (int)(mx < 0x7fffffff ? mx : 0x7fffffff);
 }
 
-// the launcher's patch limits for any batch: spans grow with M only until a tile
-// crosses whole images, so two images' worth of rows decides it; the row-skewed LDS patch holds
+// the most padded rows a bm-row tile can span at any start (every alignment to the image grid;
+// a batch's tiles start at multiples of bm, which reach many of them)
+static int patch16_span_any(int H, int W, int bm) {
+  const long long HW = (long long)H * W, Wp = W + 2;
+  auto padded = [&](long long m) {
+    const long long b = m / HW, r = m - b * HW, oy = r / W, ox = r - oy * W;
+    return (b * (H + 2) + oy + 1) * Wp + ox + 1;
+  };
+  long long mx = 0;
+  for (long long o = 0; o < HW; ++o) {
+    const long long v = padded(o + bm - 1) - padded(o) + 2 * (Wp + 1) + 1;
+    mx = v > mx ? v : mx;
+  }
+  return (int)(mx < 0x7fffffff ? mx : 0x7fffffff);
+}
+
+// the launcher's patch limits for any batch: the worst alignment decides it
+// (patch16_span_any); the row-skewed LDS patch holds
 // span * 10 + 12 * (span / Wp + 2) 16-B units (56 KiB).  A layer past them stays on the fp16 GEMM.
 static bool patch16_fits(long long span, int W) {
   return span <= P16_NPR && span * 10 + 12 * (span / (W + 2) + 2) <= 7 * 8 * 64;
@@ -305,7 +321,7 @@ bool conv_patch16_supported(int C, int OC, int H, int W, int OH, int OW, int kh,
                             int pl) {
   return kh == 3 && kw == 3 && sh == 1 && sw == 1 && pt == 1 && pl == 1 && OH == H && OW == W && C % 64 == 0 &&
          OC % 256 == 0 && patch16_enabled() && H > 0 && W > 0 &&
-         patch16_fits(patch16_span(2LL * H * W + P16_BM, H, W), W);
+         patch16_fits(patch16_span_any(H, W, P16_BM), W);
 }
 
 int launch_conv_patch16(const half_t* in_padded, const half_t* Bt, int ldb, half_t* out, int out_padded, long long M,

@@ -20,7 +20,7 @@ import dnn_hip  # noqa: E402
 import synth  # noqa: E402
 import yolo_graph  # noqa: E402
 
-WGS, SLOTS = 4096, 8
+WGS, SLOTS = 4096, 16
 
 
 def layer_report(name, rows):
@@ -29,10 +29,13 @@ def layer_report(name, rows):
         return
     print("%s: %d workgroups (wave 0, median cycles)" % (name, len(rows)))
     for nm, a, b in (("prologue (patch landed)", 1, 2), ("MFMA loop", 2, 3), ("epilogue + stores", 3, 4),
-                     ("total", 1, 4)):
+                     ("  fold + first barrier", 3, 12), ("  row table + barrier", 12, 13),
+                     ("  pool/epilogue -> stage", 13, 14), ("  split-plane stores", 14, 4), ("total", 1, 4)):
         v = [r[b] - r[a] for r in rows]
         print("  %-24s %8.0f  (p10 %6.0f, p90 %6.0f)" % (nm, statistics.median(v), sorted(v)[len(v) // 10],
                                                           sorted(v)[len(v) * 9 // 10]))
+    sk = [max(r[8:12]) - min(r[8:12]) for r in rows]
+    print("  MFMA-end skew over the 4 waves  median %.0f (p90 %.0f)" % (statistics.median(sk), sorted(sk)[len(sk) * 9 // 10]))
     t0 = min(r[0] for r in rows)
     t1 = max(r[5] for r in rows)
     span = (t1 - t0) * 10e-3  # s_memrealtime: 100 MHz -> us
