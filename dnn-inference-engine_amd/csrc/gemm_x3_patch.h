@@ -65,6 +65,13 @@ __device__ unsigned long long tile2_diag_stamps[2 * T2_DIAG_WGS * T2_DIAG_SLOTS]
 #define T2_STAMPW(k, v)
 #endif
 
+#if (X3DIAG & 2048) != 0  // conv3x3_x3_pp_kernel step cycles
+constexpr int PP_DIAG_WGS = 512;
+// [workgroup][slot]: s_memtime sums of wave 0 (team A) in 0-2 and wave 4 (team B) in 3-5: MFMA
+// step work, store step work, barrier waits; 6 total cycles of wave 0
+__device__ unsigned long long pp_diag_stamps[PP_DIAG_WGS * 8];
+#endif
+
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 struct X3Geom {
@@ -139,14 +146,15 @@ __device__ __forceinline__ X3EpiCol x3_epi_col(const EpiParams& epi, int eflags,
 // piece into the window's 192-B record (3 x 32 bf16 at out_split + o n3 + col0).  The values and
 // splits are those of one scalar store per piece and output.
 constexpr int X3_STG_ROW = 48;
-template <int TM>
-__device__ __forceinline__ void x3_pool_split_store(const float* stg, const int* orow, int no, int wbase,
-                                                    bf16_bits* __restrict__ out_split, size_t n3, int col0,
-                                                    int lane) {
+// (orow_of(w): the output record of the tile's window w < no, or -1)
+template <int TM, typename OF>
+__device__ __forceinline__ void x3_pool_split_store_f(const float* stg, OF&& orow_of, int no, int wbase,
+                                                      bf16_bits* __restrict__ out_split, size_t n3, int col0,
+                                                      int lane) {
   wait_lgkm0();  // the stage is wave-private
   for (int task = lane; task < 16 * TM; task += 64) {
     const int wl = task >> 2, c8 = 8 * (task & 3), w = wbase + wl;
-    const int o = w < no ? orow[w] : -1;
+    const int o = w < no ? orow_of(w) : -1;
     if (o < 0) continue;
     const f32x4 lo = *reinterpret_cast<const f32x4*>(stg + wl * X3_STG_ROW + c8);
     const f32x4 hi = *reinterpret_cast<const f32x4*>(stg + wl * X3_STG_ROW + c8 + 4);
@@ -167,6 +175,12 @@ __device__ __forceinline__ void x3_pool_split_store(const float* stg, const int*
 #pragma unroll
     for (int pc = 0; pc < 3; ++pc) *reinterpret_cast<u32x4*>(d + 32 * pc) = q[pc];
   }
+}
+template <int TM>
+__device__ __forceinline__ void x3_pool_split_store(const float* stg, const int* orow, int no, int wbase,
+                                                    bf16_bits* __restrict__ out_split, size_t n3, int col0,
+                                                    int lane) {
+  x3_pool_split_store_f<TM>(stg, [&](int w) { return orow[w]; }, no, wbase, out_split, n3, col0, lane);
 }
 
 // POOL (all x3 conv kernels): a fused 2x2/s2 max pool -- GEMM rows pool-window-major (row 4 w +
@@ -1018,5 +1032,219 @@ conv3x3_x3_tile2_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __res
 }
 #undef T2_STAMP
 #undef T2_STAMPW
+
+// Ping-pong form of the N = 64, one-chunk tile kernel (conv2 of YOLOv2-tiny at batch 64), round 5.
+// tile2 stamps (tools/tile2_diag.py): a tile's workgroup spends ~5 k cycles waiting for its patch,
+// ~19 k in its MFMA loop (12.1 k of its own MFMAs, the rest the other workgroup's on the same
+// SIMDs) and ~6.6 k in the epilogue; two independent workgroups per CU line those phases up at
+// random, so the MFMA pipes were busy ~65 % of the kernel.  Here ONE workgroup per CU runs two
+// teams of 4 waves (one wave of each team per SIMD) over a contiguous range of the CU's tiles
+// (team A the even ones, team B the odd ones) in lock step: every step ends at a workgroup
+// barrier, and in each step exactly one team runs its MFMA loop while the other stores its
+// previous tile (fold, pool + epilogue through its waves' LDS stages, split-plane stores) and
+// loads its next patch and first weights.  Per team the same loop as conv3x3_x3_tile2_kernel<8,
+// 26, 2, 2, 7, 1, POOL>: same products, order and epilogue -- the same bits.  LDS: a patch buffer
+// per team (64 KiB), one stage area (the teams' epilogues never overlap), the 64 columns'
+// epilogue parameters.  The row table is computed per window (no team-wide barrier inside a step).
+template <int TH, int TW, int TM, int FL = -1>
+__global__ void __launch_bounds__(512, 1)
+conv3x3_x3_pp_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __restrict__ Bt,
+                     bf16_bits* __restrict__ out_split, int N, EpiParams epi, int tilesX, int tilesY, int ntiles,
+                     X3Geom g, unsigned in_bytes, unsigned b_bytes, int ppprio) {
+  constexpr int WM = 2, WN = 2, NW = WM * WN, LP = 224, PU = LP / 16, PW2 = TW + 2, PR = (TH + 2) * PW2, T = TH * TW;
+  constexpr int NPC = (PR * PU + 63) / 64, NPW = (NPC + NW - 1) / NW;
+  constexpr int BUFB = NPW * NW * 1024, STGB = NW * TM * 4 * X3_STG_ROW * 4, NO = T / 4;
+  static_assert(TH % 2 == 0 && TW % 2 == 0 && WM * TM * 16 >= T && (WM * TM - 2) * 16 < T && NPW <= 24, "shape");
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * BUFB + STGB];
+  __shared__ f32x4 epl[32 * WN];
+
+  const int lane = threadIdx.x & 63;
+  const int eflags = FL < 0 ? epi.flags : FL;
+  const int wid = wave_uniform(threadIdx.x >> 6);
+  const int team = wid >> 2, wt = wid & 3;
+  const int wn = wt % WN, wm = wt / WN;
+  const int n0 = wn * 32;  // N = 32 WN (launcher)
+  const int Wp = g.W + 2;
+  const int fr = lane & 15, fq = lane >> 4;
+  // this workgroup's tiles [lo, hi) (balanced, XCD-local order); the team's k-th is lo + team + 2 k
+  const int wg = xcd_tile(blockIdx.x, gridDim.x);
+  const int lo = (int)((long long)ntiles * wg / gridDim.x), hi = (int)((long long)ntiles * (wg + 1) / gridDim.x);
+  const int nmine = (hi - lo - team + 1) / 2;
+  unsigned char* const P = smem + team * BUFB;
+  float* const stg = reinterpret_cast<float*>(smem + 2 * BUFB) + wt * (TM * 4 * X3_STG_ROW);
+
+  int rowoff[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    int r = (wm * TM + i) * 16 + fr;
+    r = r < T ? r : T - 1;
+    const int w = r >> 2, q = r & 3;
+    const int ly = 2 * (w / (TW / 2)) + (q >> 1), lx = 2 * (w % (TW / 2)) + (q & 1);
+    rowoff[i] = (ly * PW2 + lx) * LP + 16 * fq;
+  }
+  auto tile_of = [&](int k, int& b, int& y0, int& x0) {
+    const int t = lo + team + 2 * k;
+    const int tx = t % tilesX, tt = t / tilesX, ty = tt % tilesY;
+    b = tt / tilesY;
+    y0 = ty * TH;
+    x0 = tx * TW;
+  };
+
+  const unsigned rowB = 6u * (unsigned)g.C;
+  const auto rsA = __builtin_amdgcn_make_buffer_rsrc((void*)in, 0, (int)in_bytes, 0x00020000);
+  auto issue_patch = [&](int k) {  // the team's k-th tile into its buffer
+    int b, y0, x0;
+    tile_of(k, b, y0, x0);
+    const unsigned pbase = (unsigned)((b * (g.H + 2) + y0) * Wp + x0);
+    // (an opaque copy of the lane index: the per-piece row / unit arithmetic is recomputed per
+    // tile instead of hoisted out of the tile loop into ~40 registers live across the MFMAs)
+    unsigned ln = (unsigned)lane;
+    asm volatile("" : "+v"(ln));
+#pragma unroll
+    for (int kk = 0; kk < NPW; ++kk) {
+      if (wt + NW * kk >= NPC) break;  // (wave-uniform)
+      const unsigned U = 64u * (unsigned)(wt + NW * kk) + ln;
+      unsigned r = U / PU;
+      const unsigned u = U - r * PU;
+      r = r < (unsigned)PR ? r : (unsigned)PR - 1;
+      const unsigned py = r / PW2, px = r - py * PW2;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rsA, (__attribute__((address_space(3))) void*)(P + 1024 * (wt + NW * kk)), 16,
+          (int)((pbase + py * (unsigned)Wp + px) * rowB + 16u * u), 0, 0, 0);
+    }
+  };
+
+  constexpr int nk = 9;  // one 32-channel chunk (launcher: C == 32)
+  const unsigned bvo = (unsigned)((n0 / 16) * nk * 3072 + lane * 16);
+  const int bjs = nk * 3072;
+  const auto rsB = __builtin_amdgcn_make_buffer_rsrc((void*)Bt, 0, (int)b_bytes, 0x00020000);
+  bf16x8 bq[3][3][2];
+  auto load_b = [&](int s, bf16x8 (&dst)[3][2]) {
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        dst[p][j] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rsB, bvo, s * 3072 + p * 1024 + j * bjs, 0));
+  };
+
+  if (threadIdx.x < 32 * WN) {
+    const X3EpiCol c = x3_epi_col(epi, eflags, threadIdx.x);
+    epl[threadIdx.x] = f32x4{c.pb, c.pm, c.ps, c.pg};
+  }
+  if (nmine > 0) issue_patch(0);
+  load_b(0, bq[0]);
+  load_b(1, bq[1]);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  f32x4 acc[TM][2], accc[TM][2];
+  auto frag = [&](int i, int tap, bf16x8 (&a)[3]) {
+    const int toff = ((tap / 3) * PW2 + (tap % 3)) * LP;
+    const unsigned char* q = P + rowoff[i] + toff;
+#pragma unroll
+    for (int p = 0; p < 3; ++p) a[p] = *reinterpret_cast<const bf16x8*>(q + 64 * p);
+  };
+  // team A: steps 0, 1 = MFMAs of tile 0, store of tile 0 (+ load of tile 1), ...; team B one step
+  // later.  Each team's loop is MFMA step, barrier, store step, barrier (accumulators live within
+  // an iteration only); the leading / trailing barriers pad both teams to the same step count
+  const int nA = (hi - lo + 1) / 2, nB = (hi - lo) / 2;
+  const int nsteps = 2 * nA > 2 * nB + 1 ? 2 * nA : 2 * nB + 1;
+#if (X3DIAG & 2048) != 0
+  unsigned long long dg[4] = {0, 0, 0, 0}, t_in = __builtin_amdgcn_s_memtime(), t_start = t_in;
+  const bool dwave = (threadIdx.x & 255) == 0;
+#define PP_MARK(slot)                                      \
+  {                                                        \
+    const unsigned long long t_now = __builtin_amdgcn_s_memtime(); \
+    dg[slot] += t_now - t_in;                              \
+    t_in = t_now;                                          \
+  }
+#else
+#define PP_MARK(slot)
+#endif
+  if (team == 1) {
+    PP_MARK(1)
+    __syncthreads();
+    PP_MARK(2)
+  }
+  for (int k = 0; k < nmine; ++k) {
+    // MFMA step of tile k, at a higher issue priority than the other team's store step on the same
+    // SIMDs (MI355X_MICROARCH: VALU issue between two waves goes by priority, then age)
+    {
+      if (ppprio) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = accc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      bf16x8 af[2][3];
+      frag(0, 0, af[0]);
+#pragma unroll
+      for (int tp = 0; tp < 9; ++tp) {
+        __builtin_amdgcn_sched_barrier(0);
+        if (tp + 2 < 9) load_b(tp + 2, bq[(tp + 2) % 3]);
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const int cur = i & 1, nxt = cur ^ 1;
+          if (i + 1 < TM)
+            frag(i + 1, tp, af[nxt]);
+          else if (tp < 8)
+            frag(0, tp + 1, af[nxt]);
+          const bf16x8(&bb)[3][2] = bq[tp % 3];
+#pragma unroll
+          for (int jb = 0; jb < 2; ++jb) x3_step<true>(acc[i][jb], accc[i][jb], af[cur], bb, jb);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        if constexpr (TM & 1) {
+          if (tp < 8) {
+#pragma unroll
+            for (int p = 0; p < 3; ++p) af[0][p] = af[1][p];
+          }
+        }
+      }
+      wait_lgkm0();
+      if (ppprio) __builtin_amdgcn_s_setprio(0);
+    }
+    PP_MARK(0)
+    __syncthreads();
+    PP_MARK(2)
+    // store step: tile k out, tile k + 1's patch and first weights in
+    {
+      if (k + 1 < nmine) issue_patch(k + 1);
+      x3_fold(acc, accc);
+      int b, y0, x0;
+      tile_of(k, b, y0, x0);
+      float pb[2], pm[2], ps[2], pg[2];
+#pragma unroll
+      for (int jb = 0; jb < 2; ++jb) {
+        const f32x4 e = epl[n0 + 16 * jb + fr];
+        pb[jb] = e[0], pm[jb] = e[1], ps[jb] = e[2], pg[jb] = e[3];
+      }
+      pool_epilogue_batch<FL>(acc, pb, pm, ps, pg, epi.flags,
+                              [&](int i, int jb, float v) { stg[(4 * i + fq) * X3_STG_ROW + 16 * jb + fr] = v; });
+      auto orow_of = [&](int w) {
+        const int py = (y0 >> 1) + w / (TW / 2), px = (x0 >> 1) + w % (TW / 2);
+        return (py >= g.PH || px >= g.PW) ? -1 : (b * (g.PH + 2) + py + 1) * (g.PW + 2) + px + 1;
+      };
+      x3_pool_split_store_f<TM>(stg, orow_of, NO, 4 * wm * TM, out_split, 3 * (size_t)N, (n0 >> 5) * 96, lane);
+      if (k + 1 < nmine) {
+        load_b(0, bq[0]);  // (after the epilogue: registers)
+        load_b(1, bq[1]);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's patch pieces and weights
+      wait_lgkm0();
+    }
+    PP_MARK(1)
+    __syncthreads();
+    PP_MARK(2)
+  }
+  for (int st = team + 2 * nmine; st < nsteps; ++st) __syncthreads();
+#if (X3DIAG & 2048) != 0
+  if (dwave && blockIdx.x < PP_DIAG_WGS) {
+    unsigned long long* d = pp_diag_stamps + 8 * blockIdx.x + 3 * team;
+    d[0] = dg[0], d[1] = dg[1], d[2] = dg[2];
+    if (team == 0) pp_diag_stamps[8 * blockIdx.x + 6] = __builtin_amdgcn_s_memtime() - t_start;
+  }
+#endif
+#undef PP_MARK
+}
 
 }  // namespace dnnhip

@@ -507,6 +507,23 @@ int launch_conv_x3(const bf16_bits* in_split, const bf16_bits* Bt, float* out, b
                      xg, (unsigned)in_bytes, (unsigned)b_bytes)
 #define X3T2(TH_, TW_, WM, WN, NBUF, POOL, FL_) X3T2M(TH_, TW_, WM, WN, X3T_TM, NBUF, POOL, FL_)
     const bool yolo = epi.flags == X3_YOLO_FL;  // YOLO's epilogue set compiled in for the pooled forms
+    // N = 64 from one chunk (conv2), pooled into split planes, a batch grid of >= 4 tiles per CU:
+    // the ping-pong kernel, one workgroup per CU (conv3x3_x3_pp_kernel; same bits as the tile
+    // kernel).  DNN_HIP_X3_PP=0 (read per launch, A/B) keeps the tile kernel.
+    if (kind == 1 && pool && out_split && !small && blocks >= 4LL * device_cu_count() &&
+        !getenv_flag_off("DNN_HIP_X3_PP")) {
+      const int G = device_cu_count();
+      const int prio = !getenv_flag_off("DNN_HIP_X3_PP_PRIO");  // (A/B, read per launch)
+      if (yolo)
+        hipLaunchKernelGGL((conv3x3_x3_pp_kernel<8, 26, X3T_TM, X3_YOLO_FL>), dim3((unsigned)G), dim3(512), 0, stream,
+                           in_split, Bt, out_split, N, epi, tilesX, tilesY, (int)blocks, xg, (unsigned)in_bytes,
+                           (unsigned)b_bytes, prio);
+      else
+        hipLaunchKernelGGL((conv3x3_x3_pp_kernel<8, 26, X3T_TM, -1>), dim3((unsigned)G), dim3(512), 0, stream, in_split,
+                           Bt, out_split, N, epi, tilesX, tilesY, (int)blocks, xg, (unsigned)in_bytes, (unsigned)b_bytes,
+                           prio);
+      return check_x3("conv_x3 (ping-pong)");
+    }
     if (small) {
       if (pool && yolo && kind == 2)
         X3T2M(2, 26, 2, 2, 2, 2, true, X3_YOLO_FL);
@@ -852,6 +869,18 @@ extern "C" __attribute__((visibility("default"))) int dnn_ktile_diag_stamps(unsi
 extern "C" __attribute__((visibility("default"))) int dnn_tile2_diag_stamps(unsigned long long* host, int n) {
   if (n < 0 || n > 2 * dnnhip::T2_DIAG_WGS * dnnhip::T2_DIAG_SLOTS) return -2;
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(dnnhip::tile2_diag_stamps), (size_t)n * sizeof(unsigned long long), 0,
+                             hipMemcpyDeviceToHost) == hipSuccess
+             ? 0
+             : -1;
+}
+#endif
+
+#if (X3DIAG & 2048) != 0
+// diagnostic builds (X3DIAG bit 2048): conv3x3_x3_pp_kernel's per-workgroup step cycle sums of its
+// last launch (8 per workgroup, gemm_x3_patch.h) copied to host[0 .. 8 n)
+extern "C" __attribute__((visibility("default"))) int dnn_pp_diag_stamps(unsigned long long* host, int n) {
+  if (n < 0 || n > dnnhip::PP_DIAG_WGS) return -2;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(dnnhip::pp_diag_stamps), (size_t)n * 8 * sizeof(unsigned long long), 0,
                              hipMemcpyDeviceToHost) == hipSuccess
              ? 0
              : -1;

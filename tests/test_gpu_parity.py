@@ -1690,6 +1690,48 @@ def test_x3_tile_kernel_vs_oracle(monkeypatch, case):
     assert errs["1"] <= 1.25 * errs["0"] and errs.get("lat", 0.0) <= 1.25 * errs["0"], errs
 
 
+@pytest.mark.parametrize("B", [24, 21])
+def test_x3_pingpong_equals_tile_kernel(monkeypatch, B):
+    """conv3x3_x3_pp_kernel (N = 64 from one 32-channel chunk, pooled into split planes, batch
+    grids of >= 4 tiles per CU: one workgroup per CU whose two wave teams alternate MFMA and store
+    steps over the CU's tile range) against the tile kernel (DNN_HIP_X3_PP=0): bit-identical
+    outputs, including uneven team tile counts (B = 24: 1,248 tiles over 256 workgroups, 4 or 5
+    each; B = 21: 1,092); within the fp32 tolerance of the float64 oracle; repeat runs identical."""
+    rng = np.random.default_rng(B)
+    x = rng.standard_normal((B, 104, 104, 32)).astype(np.float32)
+    k = (rng.standard_normal((3, 3, 32, 64)) * np.sqrt(2.0 / 288)).astype(np.float32)
+    b = rng.standard_normal(64).astype(np.float32) * 0.1
+    gam = rng.uniform(0.5, 1.5, 64).astype(np.float32)
+    gam[::5] *= -1
+    n = (rng.standard_normal(64).astype(np.float32) * 0.1, rng.uniform(0.5, 1.5, 64).astype(np.float32), gam)
+    k2 = (rng.standard_normal((3, 3, 64, 128)) * np.sqrt(2.0 / 576)).astype(np.float32)  # (x3 consumer)
+    g = dnn_hip.DnnGraphBuilder()
+    y = g.create_input(list(x.shape))
+    y = g.create_max_pool2d(y, [1, 2, 2, 1], [1, 1, 1, 1], "SAME")
+    y = g.create_conv2d(y, k, [1, 1, 1, 1], "SAME")
+    y = g.create_bias_add(y, b)
+    y = g.create_batch_norm(y, *n, 1e-5)
+    y = g.create_leaky_relu(y)
+    y = g.create_max_pool2d(y, [1, 2, 2, 1], [1, 2, 2, 1], "SAME")
+    y = g.create_conv2d(y, k2, [1, 1, 1, 1], "SAME")
+    y = g.create_leaky_relu(y)
+    g.set_out_node(y)
+    eng = dnn_hip.DnnInferenceEngine(g, False)
+    conv = [ln for ln in eng.plan().describe().splitlines() if ln.startswith("conv")]
+    assert "mode=patch_x3" in conv[0] and "+pool2x2s2" in conv[0] and "mode=patch_x3" in conv[1], conv
+    outs = {}
+    for pp in ("1", "0"):
+        monkeypatch.setenv("DNN_HIP_X3_PP", pp)
+        outs[pp] = eng.run(x)
+        assert np.array_equal(eng.run(x), outs[pp])
+    assert np.array_equal(outs["1"], outs["0"])
+    ref = R.max_pool2d(x, [1, 2, 2, 1], [1, 1, 1, 1], "SAME")
+    ref = R.max_pool2d(R.leaky_relu(R.batch_norm(R.bias_add(R.conv2d(ref, k), b), *n, 1e-5)),
+                       [1, 2, 2, 1], [1, 2, 2, 1], "SAME")
+    ref = R.leaky_relu(R.conv2d(ref, k2))
+    assert R.normwise_err(outs["1"], ref) < 3 * LAYER_TOL
+
+
 def test_x3_tile_small_tiles_same_bits():
     """The narrow x3 tile kernel's two tile shapes (kernels_x3.hip: 8 x 26 / 4 x 26 tiles when a
     launch has at least two workgroups per CU, else 2 x 26 tiles of 2 x 2 waves -- the single-frame

@@ -104,6 +104,18 @@ def main():
     print("forwards %d" % n)
     for k, m, c in zip(plan.kernels(), ms, cnt):
         print("  %-14s %.4f ms" % (k["name"], m / max(c, 1)))
+    fp = getattr(plan.lib, "dnn_pp_diag_stamps", None)
+    if fp is not None:  # X3DIAG 2048: the ping-pong kernel's step cycles (conv2)
+        fp.restype = ctypes.c_int
+        fp.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        pb = (ctypes.c_ulonglong * (256 * 8))()
+        assert fp(pb, 256) == 0
+        rows = [list(pb[8 * w:8 * w + 8]) for w in range(256) if pb[8 * w + 6] > 0]
+        print("ping-pong conv2: %d workgroups, median cycles per workgroup" % len(rows))
+        for nm, i in (("team A MFMA steps", 0), ("team A store steps", 1), ("team A barrier waits", 2),
+                      ("team B MFMA steps", 3), ("team B store steps", 4), ("team B barrier waits", 5),
+                      ("total (wave 0)", 6)):
+            print("  %-22s %10.0f" % (nm, statistics.median(r[i] for r in rows)))
     fn = getattr(plan.lib, "dnn_tile2_diag_stamps", None)
     if fn is None:
         print("no dnn_tile2_diag_stamps: not an X3DIAG 1024 build")
