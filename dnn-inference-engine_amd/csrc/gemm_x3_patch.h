@@ -1033,29 +1033,34 @@ conv3x3_x3_tile2_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __res
 #undef T2_STAMP
 #undef T2_STAMPW
 
-// Ping-pong form of the N = 64, one-chunk tile kernel (conv2 of YOLOv2-tiny at batch 64), round 5.
-// tile2 stamps (tools/tile2_diag.py): a tile's workgroup spends ~5 k cycles waiting for its patch,
-// ~19 k in its MFMA loop (12.1 k of its own MFMAs, the rest the other workgroup's on the same
-// SIMDs) and ~6.6 k in the epilogue; two independent workgroups per CU line those phases up at
-// random, so the MFMA pipes were busy ~65 % of the kernel.  Here ONE workgroup per CU runs two
-// teams of 4 waves (one wave of each team per SIMD) over a contiguous range of the CU's tiles
-// (team A the even ones, team B the odd ones) in lock step: every step ends at a workgroup
-// barrier, and in each step exactly one team runs its MFMA loop while the other stores its
-// previous tile (fold, pool + epilogue through its waves' LDS stages, split-plane stores) and
-// loads its next patch and first weights.  Per team the same loop as conv3x3_x3_tile2_kernel<8,
-// 26, 2, 2, 7, 1, POOL>: same products, order and epilogue -- the same bits.  LDS: a patch buffer
-// per team (64 KiB), one stage area (the teams' epilogues never overlap), the 64 columns'
-// epilogue parameters.  The row table is computed per window (no team-wide barrier inside a step).
-template <int TH, int TW, int TM, int FL = -1>
+// Ping-pong form of the narrow tile kernel for batch grids (round 5): conv2 of YOLOv2-tiny at batch
+// 64 (N = 64, one 32-channel chunk, 8 x 26 tiles; the NCH / PU / SK parameters also took conv3's
+// shape, bit-exact but slower than the tile kernel: kernels_x3.hip).
+// tile2 stamps (tools/tile2_diag.py): a tile's workgroup spends ~5 k cycles waiting for its patch
+// and ~6.6 k in the epilogue beside its MFMA loop; two independent workgroups per CU line those
+// phases up at random.  Here ONE workgroup per CU runs two teams of WM x WN = 4 waves (one wave of
+// each team per SIMD) over a contiguous range of the CU's tiles (team A the even ones, team B the
+// odd ones) in lock step: every step ends at a workgroup barrier, and in each step one team runs
+// its MFMA loop over the tile's chunks while the other stores its previous tile (fold, pool +
+// epilogue through its waves' LDS stages, split-plane stores) and loads every chunk of its next
+// patch and its first weights.  Per team the same loop as conv3x3_x3_tile2_kernel (same
+// products and order, same epilogue): the same bits.  LDS per team: NCH patch buffers of PU-unit
+// pixel rows, the image row skewed by SK units (conv2: 224-B rows; conv3: 192-B rows + 2, so
+// that four buffers fit: 0.92 modelled extra cycles per fragment read either way); one stage area
+// (the teams' store steps never overlap) and the epilogue parameters.  The row table is computed
+// per window (no team-wide barrier inside a step).
+template <int TH, int TW, int WM, int WN, int TM, int NCH, int PU, int SK, int FL = -1>
 __global__ void __launch_bounds__(512, 1)
 conv3x3_x3_pp_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __restrict__ Bt,
                      bf16_bits* __restrict__ out_split, int N, EpiParams epi, int tilesX, int tilesY, int ntiles,
                      X3Geom g, unsigned in_bytes, unsigned b_bytes, int ppprio) {
-  constexpr int WM = 2, WN = 2, NW = WM * WN, LP = 224, PU = LP / 16, PW2 = TW + 2, PR = (TH + 2) * PW2, T = TH * TW;
-  constexpr int NPC = (PR * PU + 63) / 64, NPW = (NPC + NW - 1) / NW;
-  constexpr int BUFB = NPW * NW * 1024, STGB = NW * TM * 4 * X3_STG_ROW * 4, NO = T / 4;
-  static_assert(TH % 2 == 0 && TW % 2 == 0 && WM * TM * 16 >= T && (WM * TM - 2) * 16 < T && NPW <= 24, "shape");
-  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * BUFB + STGB];
+  constexpr int NW = WM * WN, PW2 = TW + 2, T = TH * TW, RU = PW2 * PU + SK;  // units per patch row
+  constexpr int NPC = ((TH + 2) * RU + 63) / 64, NPW = (NPC + NW - 1) / NW;
+  constexpr int BUFB = NPW * NW * 1024, STGB = NW * TM * 4 * X3_STG_ROW * 4, NO = T / 4, NK = 9 * NCH;
+  static_assert(NW == 4 && PU >= 12 && TH % 2 == 0 && TW % 2 == 0 && WM * TM * 16 >= T && (WM * TM - 2) * 16 < T &&
+                    NPW <= 24 && 2 * NCH * BUFB + STGB + 32 * WN * 16 <= 160 * 1024,
+                "shape");
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * NCH * BUFB + STGB];
   __shared__ f32x4 epl[32 * WN];
 
   const int lane = threadIdx.x & 63;
@@ -1070,8 +1075,8 @@ conv3x3_x3_pp_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __restri
   const int wg = xcd_tile(blockIdx.x, gridDim.x);
   const int lo = (int)((long long)ntiles * wg / gridDim.x), hi = (int)((long long)ntiles * (wg + 1) / gridDim.x);
   const int nmine = (hi - lo - team + 1) / 2;
-  unsigned char* const P = smem + team * BUFB;
-  float* const stg = reinterpret_cast<float*>(smem + 2 * BUFB) + wt * (TM * 4 * X3_STG_ROW);
+  unsigned char* const P = smem + team * NCH * BUFB;
+  float* const stg = reinterpret_cast<float*>(smem + 2 * NCH * BUFB) + wt * (TM * 4 * X3_STG_ROW);
 
   int rowoff[TM];
 #pragma unroll
@@ -1080,7 +1085,7 @@ conv3x3_x3_pp_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __restri
     r = r < T ? r : T - 1;
     const int w = r >> 2, q = r & 3;
     const int ly = 2 * (w / (TW / 2)) + (q >> 1), lx = 2 * (w % (TW / 2)) + (q & 1);
-    rowoff[i] = (ly * PW2 + lx) * LP + 16 * fq;
+    rowoff[i] = (ly * RU + lx * PU) * 16 + 16 * fq;
   }
   auto tile_of = [&](int k, int& b, int& y0, int& x0) {
     const int t = lo + team + 2 * k;
@@ -1090,9 +1095,11 @@ conv3x3_x3_pp_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __restri
     x0 = tx * TW;
   };
 
+  // patch DMA: LDS unit U of a chunk's buffer = patch row U / RU, pixel (U % RU) / PU, unit
+  // (U % RU) % PU; units past 12 of a pixel and the SK skew units read neighbouring bytes (never read)
   const unsigned rowB = 6u * (unsigned)g.C;
   const auto rsA = __builtin_amdgcn_make_buffer_rsrc((void*)in, 0, (int)in_bytes, 0x00020000);
-  auto issue_patch = [&](int k) {  // the team's k-th tile into its buffer
+  auto issue_patch = [&](int k) {  // every chunk of the team's k-th tile into its buffers
     int b, y0, x0;
     tile_of(k, b, y0, x0);
     const unsigned pbase = (unsigned)((b * (g.H + 2) + y0) * Wp + x0);
@@ -1104,19 +1111,21 @@ conv3x3_x3_pp_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __restri
     for (int kk = 0; kk < NPW; ++kk) {
       if (wt + NW * kk >= NPC) break;  // (wave-uniform)
       const unsigned U = 64u * (unsigned)(wt + NW * kk) + ln;
-      unsigned r = U / PU;
-      const unsigned u = U - r * PU;
-      r = r < (unsigned)PR ? r : (unsigned)PR - 1;
-      const unsigned py = r / PW2, px = r - py * PW2;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          rsA, (__attribute__((address_space(3))) void*)(P + 1024 * (wt + NW * kk)), 16,
-          (int)((pbase + py * (unsigned)Wp + px) * rowB + 16u * u), 0, 0, 0);
+      unsigned jr = U / RU;
+      const unsigned rem = U - jr * RU;
+      unsigned px = rem / PU, u = rem - px * PU;
+      if (px >= (unsigned)PW2) px = PW2 - 1, u = PU - 1;
+      jr = jr < (unsigned)(TH + 2) ? jr : TH + 1;
+      const int vo = (int)((pbase + jr * (unsigned)Wp + px) * rowB + 16u * u);
+#pragma unroll
+      for (int c = 0; c < NCH; ++c)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            rsA, (__attribute__((address_space(3))) void*)(P + c * BUFB + 1024 * (wt + NW * kk)), 16, vo, c * 192, 0, 0);
     }
   };
 
-  constexpr int nk = 9;  // one 32-channel chunk (launcher: C == 32)
-  const unsigned bvo = (unsigned)((n0 / 16) * nk * 3072 + lane * 16);
-  const int bjs = nk * 3072;
+  const unsigned bvo = (unsigned)((n0 / 16) * NK * 3072 + lane * 16);
+  const int bjs = NK * 3072;
   const auto rsB = __builtin_amdgcn_make_buffer_rsrc((void*)Bt, 0, (int)b_bytes, 0x00020000);
   bf16x8 bq[3][3][2];
   auto load_b = [&](int s, bf16x8 (&dst)[3][2]) {
@@ -1138,9 +1147,9 @@ conv3x3_x3_pp_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __restri
   __syncthreads();
 
   f32x4 acc[TM][2], accc[TM][2];
-  auto frag = [&](int i, int tap, bf16x8 (&a)[3]) {
-    const int toff = ((tap / 3) * PW2 + (tap % 3)) * LP;
-    const unsigned char* q = P + rowoff[i] + toff;
+  auto frag = [&](const unsigned char* Pc, int i, int tap, bf16x8 (&a)[3]) {
+    const int toff = ((tap / 3) * RU + (tap % 3) * PU) * 16;
+    const unsigned char* q = Pc + rowoff[i] + toff;
 #pragma unroll
     for (int p = 0; p < 3; ++p) a[p] = *reinterpret_cast<const bf16x8*>(q + 64 * p);
   };
@@ -1152,11 +1161,11 @@ conv3x3_x3_pp_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __restri
 #if (X3DIAG & 2048) != 0
   unsigned long long dg[4] = {0, 0, 0, 0}, t_in = __builtin_amdgcn_s_memtime(), t_start = t_in;
   const bool dwave = (threadIdx.x & 255) == 0;
-#define PP_MARK(slot)                                      \
-  {                                                        \
+#define PP_MARK(slot)                                              \
+  {                                                                \
     const unsigned long long t_now = __builtin_amdgcn_s_memtime(); \
-    dg[slot] += t_now - t_in;                              \
-    t_in = t_now;                                          \
+    dg[slot] += t_now - t_in;                                      \
+    t_in = t_now;                                                  \
   }
 #else
 #define PP_MARK(slot)
@@ -1175,28 +1184,34 @@ conv3x3_x3_pp_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __restri
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = accc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-      bf16x8 af[2][3];
-      frag(0, 0, af[0]);
 #pragma unroll
-      for (int tp = 0; tp < 9; ++tp) {
-        __builtin_amdgcn_sched_barrier(0);
-        if (tp + 2 < 9) load_b(tp + 2, bq[(tp + 2) % 3]);
+      for (int c = 0; c < NCH; ++c) {
+        const unsigned char* Pc = P + c * BUFB;
+        bf16x8 af[2][3];
+        frag(Pc, 0, 0, af[0]);
 #pragma unroll
-        for (int i = 0; i < TM; ++i) {
-          const int cur = i & 1, nxt = cur ^ 1;
-          if (i + 1 < TM)
-            frag(i + 1, tp, af[nxt]);
-          else if (tp < 8)
-            frag(0, tp + 1, af[nxt]);
-          const bf16x8(&bb)[3][2] = bq[tp % 3];
-#pragma unroll
-          for (int jb = 0; jb < 2; ++jb) x3_step<true>(acc[i][jb], accc[i][jb], af[cur], bb, jb);
+        for (int tp = 0; tp < 9; ++tp) {
+          const int s = 9 * c + tp;
           __builtin_amdgcn_sched_barrier(0);
-        }
-        if constexpr (TM & 1) {
-          if (tp < 8) {
+          // (X3DIAG 4096, diagnostic: step 0's weights for every step -- no weight loads in the loop)
+          if (s + 2 < NK && (X3DIAG & 4096) == 0) load_b(s + 2, bq[(s + 2) % 3]);
 #pragma unroll
-            for (int p = 0; p < 3; ++p) af[0][p] = af[1][p];
+          for (int i = 0; i < TM; ++i) {
+            const int cur = i & 1, nxt = cur ^ 1;
+            if (i + 1 < TM)
+              frag(Pc, i + 1, tp, af[nxt]);
+            else if (tp < 8)
+              frag(Pc, 0, tp + 1, af[nxt]);
+            const bf16x8(&bb)[3][2] = bq[(X3DIAG & 4096) != 0 ? 0 : s % 3];
+#pragma unroll
+            for (int jb = 0; jb < 2; ++jb) x3_step<true>(acc[i][jb], accc[i][jb], af[cur], bb, jb);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+          if constexpr (TM & 1) {
+            if (tp < 8) {
+#pragma unroll
+              for (int p = 0; p < 3; ++p) af[0][p] = af[1][p];
+            }
           }
         }
       }

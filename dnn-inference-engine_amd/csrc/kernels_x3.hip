@@ -507,21 +507,26 @@ int launch_conv_x3(const bf16_bits* in_split, const bf16_bits* Bt, float* out, b
                      xg, (unsigned)in_bytes, (unsigned)b_bytes)
 #define X3T2(TH_, TW_, WM, WN, NBUF, POOL, FL_) X3T2M(TH_, TW_, WM, WN, X3T_TM, NBUF, POOL, FL_)
     const bool yolo = epi.flags == X3_YOLO_FL;  // YOLO's epilogue set compiled in for the pooled forms
-    // N = 64 from one chunk (conv2), pooled into split planes, a batch grid of >= 4 tiles per CU:
-    // the ping-pong kernel, one workgroup per CU (conv3x3_x3_pp_kernel; same bits as the tile
-    // kernel).  DNN_HIP_X3_PP=0 (read per launch, A/B) keeps the tile kernel.
-    if (kind == 1 && pool && out_split && !small && blocks >= 4LL * device_cu_count() &&
-        !getenv_flag_off("DNN_HIP_X3_PP")) {
+    // N = 64 from one chunk (conv2), pooled into split planes, batch grids of >= 4 tiles per CU:
+    // the ping-pong kernel, one workgroup per CU (conv3x3_x3_pp_kernel; the tile kernel's bits).
+    // DNN_HIP_X3_PP=0 (read per launch, A/B) keeps the tile kernel, DNN_HIP_X3_PP_PRIO=0 its MFMA
+    // steps at the default priority.  (conv3's shape -- N = 128, two chunks, 192-B skewed rows --
+    // measured slower on it, 0.1199 vs 0.1133 ms: its MFMA steps are 3.6x its store steps, so the
+    // two tile-kernel workgroups per CU already keep the MFMA pipes fed, and one workgroup per CU
+    // serialises the CUs' 6.5 tiles.)
+    if (pool && out_split && !small && blocks >= 4LL * device_cu_count() && !getenv_flag_off("DNN_HIP_X3_PP") &&
+        kind == 1 && C == 32 && N == 64) {
       const int G = device_cu_count();
-      const int prio = !getenv_flag_off("DNN_HIP_X3_PP_PRIO");  // (A/B, read per launch)
+      const int prio = !getenv_flag_off("DNN_HIP_X3_PP_PRIO");
+#define X3PP(TH_, WM_, WN_, NCH_, PU_, SK_, FL_)                                                                   \
+  hipLaunchKernelGGL((conv3x3_x3_pp_kernel<TH_, 26, WM_, WN_, X3T_TM, NCH_, PU_, SK_, FL_>), dim3((unsigned)G),     \
+                     dim3(512), 0, stream, in_split, Bt, out_split, N, epi, tilesX, tilesY, (int)blocks, xg,       \
+                     (unsigned)in_bytes, (unsigned)b_bytes, prio)
       if (yolo)
-        hipLaunchKernelGGL((conv3x3_x3_pp_kernel<8, 26, X3T_TM, X3_YOLO_FL>), dim3((unsigned)G), dim3(512), 0, stream,
-                           in_split, Bt, out_split, N, epi, tilesX, tilesY, (int)blocks, xg, (unsigned)in_bytes,
-                           (unsigned)b_bytes, prio);
+        X3PP(8, 2, 2, 1, 14, 0, X3_YOLO_FL);
       else
-        hipLaunchKernelGGL((conv3x3_x3_pp_kernel<8, 26, X3T_TM, -1>), dim3((unsigned)G), dim3(512), 0, stream, in_split,
-                           Bt, out_split, N, epi, tilesX, tilesY, (int)blocks, xg, (unsigned)in_bytes, (unsigned)b_bytes,
-                           prio);
+        X3PP(8, 2, 2, 1, 14, 0, -1);
+#undef X3PP
       return check_x3("conv_x3 (ping-pong)");
     }
     if (small) {
