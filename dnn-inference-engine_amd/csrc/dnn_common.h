@@ -255,6 +255,11 @@ bool conv_x3_ktile_supported(long long batch, int C, int OC, int H, int W, int O
 int launch_conv_x3_ktile(const unsigned short* in_split, const unsigned short* Bt, float* out,
                          unsigned short* out_split, long long M, int N, int Npad, int K, int H, int W, int C,
                          const EpiParams& epi, hipStream_t stream, int pool);
+// batch plans' small-frame x3 conv with its 2x2/s1 SAME pool fused (gemm_x3_img.h: conv5 +
+// pool5), one image x 128 columns per workgroup over the whole K, split planes out
+bool conv_x3_img_supported(int C, int OC, int H, int W);
+int launch_conv_x3_img(const unsigned short* in_split, const unsigned short* Bt, float* out, unsigned short* out_split,
+                       int n, int N, int Npad, int K, int H, int W, int C, const EpiParams& epi, hipStream_t stream);
 bool conv_x3_lat_supported(long long batch, int C, int OC, int H, int W, int OH, int OW, int kh, int kw, int sh,
                            int sw, int pt, int pl);
 int x3_lat_splits(int N, int K);

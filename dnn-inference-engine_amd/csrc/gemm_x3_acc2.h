@@ -32,6 +32,17 @@ namespace dnnhip {
 constexpr int X3_DIAG_WGS = 8192;
 __device__ unsigned long long x3_diag_stamps[X3_DIAG_WGS * 4];  // [workgroup][t0, r0, t1, r1]
 #endif
+#if (X3DIAG & 8192) != 0  // per-layer phase stamps (results unchanged), wave 0:
+// [layer: N = 256 / 512 / other][workgroup][0 s_memrealtime start, 1 s_memtime start, 2 prologue
+// done, 3 loop done, 4 end, 5 s_memrealtime end, 6 HW_ID, 7 XCC_ID]
+constexpr int AC_DIAG_WGS = 512;
+__device__ unsigned long long acc2_diag_stamps[3 * AC_DIAG_WGS * 8];
+#define AC_STAMP(k, v)                                                                                      \
+  if (threadIdx.x == 0 && blockIdx.x < AC_DIAG_WGS)                                                         \
+    acc2_diag_stamps[((N == 256 ? 0 : N == 512 ? 1 : 2) * AC_DIAG_WGS + blockIdx.x) * 8 + (k)] = (v);
+#else
+#define AC_STAMP(k, v)
+#endif
 
 template <int I, int N, class F>
 __device__ __forceinline__ void static_for(F&& f) {
@@ -80,6 +91,10 @@ conv3x3_x3_acc2_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __rest
 
   const int lane = threadIdx.x & 63;
   const int wid = wave_uniform(threadIdx.x >> 6);
+  AC_STAMP(0, __builtin_amdgcn_s_memrealtime())
+  AC_STAMP(1, __builtin_amdgcn_s_memtime())
+  AC_STAMP(6, (unsigned)__builtin_amdgcn_s_getreg(4 | (31 << 11)))
+  AC_STAMP(7, (unsigned)__builtin_amdgcn_s_getreg(20 | (31 << 11)))
   const int tile_s = xcd_tile(blockIdx.x, gridDim.x), ntiles = gridDim.x / g.splits;
   const int split = tile_s / ntiles, tile = tile_s - split * ntiles;
   // tiles N-major inside each XCD's contiguous range (~31 M tiles of one N panel per XCD).
@@ -170,6 +185,7 @@ conv3x3_x3_acc2_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __rest
   load_b(0, bq[0]);
   vm_wait<0>();
   __syncthreads();
+  AC_STAMP(2, __builtin_amdgcn_s_memtime())
 #if (X3DIAG & 16) != 0
   const unsigned long long st0 = __builtin_amdgcn_s_memtime(), sr0 = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -246,6 +262,7 @@ conv3x3_x3_acc2_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __rest
     }
   }
   vm_wait<0>();
+  AC_STAMP(3, __builtin_amdgcn_s_memtime())
 #if (X3DIAG & 16) != 0
   {
     const unsigned long long st1 = __builtin_amdgcn_s_memtime(), sr1 = __builtin_amdgcn_s_memrealtime();
@@ -298,6 +315,8 @@ conv3x3_x3_acc2_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __rest
       pool_epilogue_batch<FL>(accm, pb, pm, ps, pg, epi.flags,
                               [&](int i, int jb, float v) { stg[(4 * i + fq) * X3_STG_ROW + 16 * jb + fr] = v; });
       x3_pool_split_store<TM>(stg, orow, BM / 4, 0, out_split, 3 * (size_t)N, (n0 >> 5) * 96, lane);
+      AC_STAMP(4, __builtin_amdgcn_s_memtime())
+      AC_STAMP(5, __builtin_amdgcn_s_memrealtime())
       return;
     }
     static_for<0, NJ>([&](auto jbc) {
@@ -392,6 +411,9 @@ conv3x3_x3_acc2_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __rest
       }
     }
   });
+  AC_STAMP(4, __builtin_amdgcn_s_memtime())
+  AC_STAMP(5, __builtin_amdgcn_s_memrealtime())
 }
+#undef AC_STAMP
 
 }  // namespace dnnhip

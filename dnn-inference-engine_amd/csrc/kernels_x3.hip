@@ -7,6 +7,7 @@
 #include "gemm_x3_lat.h"
 #include "gemm_x3_1x1.h"
 #include "gemm_x3_ktile.h"
+#include "gemm_x3_img.h"
 
 #include <cfloat>
 #include <cstdlib>
@@ -638,6 +639,36 @@ static int x3_ktile_shape(int C, int OC, int H, int W, int pool) {
   return -1;
 }
 
+// conv3x3_x3_img_kernel (gemm_x3_img.h): whole-image tiles, instantiated for YOLOv2-tiny's 13x13
+// frames.  DNN_HIP_X3_IMG=0 (plan time) keeps the wide kernel's K slices + the pool5 combine.
+bool conv_x3_img_supported(int C, int OC, int H, int W) {
+  return H == 13 && W == 13 && C % 32 == 0 && OC % 128 == 0 && x3_enabled() && !getenv_flag_off("DNN_HIP_X3_IMG");
+}
+
+int launch_conv_x3_img(const bf16_bits* in_split, const bf16_bits* Bt, float* out, bf16_bits* out_split, int n, int N,
+                       int Npad, int K, int H, int W, int C, const EpiParams& epi, hipStream_t stream) {
+  if (n == 0 || N == 0) return 0;
+  const long long in_bytes = (long long)x3_act_bytes(n, H, W, C);
+  const long long b_bytes = (long long)(Npad / 16) * (K / 32) * 3072;
+  if (!conv_x3_img_supported(C, N, H, W) || K != 9 * C || Npad != N || (out_split == nullptr) == (out == nullptr) ||
+      in_bytes >= 0x80000000LL || b_bytes >= 0x80000000LL || x3_act_bytes(n, H, W, N) >= 0x80000000ULL) {
+    set_error("conv_x3_img: unsupported shape n=%d N=%d K=%d %dx%dx%d", n, N, K, H, W, C);
+    return -2;
+  }
+  const long long blocks = (long long)n * (N / 128);
+  if (blocks > 0x7fffffffLL) {
+    set_error("conv_x3_img: grid too large");
+    return -2;
+  }
+  if (epi.flags == X3_YOLO_FL)
+    hipLaunchKernelGGL((conv3x3_x3_img_kernel<13, 13, X3_YOLO_FL>), dim3((unsigned)blocks), dim3(512), 0, stream,
+                       in_split, Bt, out, out_split, N, K, epi, C, (unsigned)in_bytes, (unsigned)b_bytes);
+  else
+    hipLaunchKernelGGL((conv3x3_x3_img_kernel<13, 13, -1>), dim3((unsigned)blocks), dim3(512), 0, stream, in_split, Bt,
+                       out, out_split, N, K, epi, C, (unsigned)in_bytes, (unsigned)b_bytes);
+  return check_x3("conv_x3_img");
+}
+
 bool conv_x3_ktile_supported(long long batch, int C, int OC, int H, int W, int OH, int OW, int kh, int kw, int sh,
                              int sw, int pt, int pl, int pool) {
   if (!(kh == 3 && kw == 3 && sh == 1 && sw == 1 && pt == 1 && pl == 1 && OH == H && OW == W)) return false;
@@ -874,6 +905,18 @@ extern "C" __attribute__((visibility("default"))) int dnn_ktile_diag_stamps(unsi
 extern "C" __attribute__((visibility("default"))) int dnn_tile2_diag_stamps(unsigned long long* host, int n) {
   if (n < 0 || n > 2 * dnnhip::T2_DIAG_WGS * dnnhip::T2_DIAG_SLOTS) return -2;
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(dnnhip::tile2_diag_stamps), (size_t)n * sizeof(unsigned long long), 0,
+                             hipMemcpyDeviceToHost) == hipSuccess
+             ? 0
+             : -1;
+}
+#endif
+
+#if (X3DIAG & 8192) != 0
+// diagnostic builds (X3DIAG bit 8192): conv3x3_x3_acc2_kernel's per-workgroup phase stamps of its
+// last launch per layer class (N = 256 / 512 / other; 8 per workgroup) copied to host[0 .. 8 n)
+extern "C" __attribute__((visibility("default"))) int dnn_acc2_diag_stamps(unsigned long long* host, int n) {
+  if (n < 0 || n > 3 * dnnhip::AC_DIAG_WGS) return -2;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(dnnhip::acc2_diag_stamps), (size_t)n * 8 * sizeof(unsigned long long), 0,
                              hipMemcpyDeviceToHost) == hipSuccess
              ? 0
              : -1;

@@ -106,7 +106,8 @@ struct PlanLayer {
   bool pool = false;  // a 2x2/stride-2 max pool fused into this conv
   bool x3lat = false;  // MODE_X3 on the small-M kernel (latency plans: launch_conv_x3_lat)
   bool x3k = false;    // MODE_X3 with the K split inside the workgroup (latency plans: launch_conv_x3_ktile)
-  bool pool1 = false;  // x3k: a 2x2/stride-1 SAME pool fused (same output frame)
+  bool pool1 = false;  // x3k / x3img: a 2x2/stride-1 SAME pool fused (same output frame)
+  bool x3img = false;  // MODE_X3 on whole-image tiles over all of K (launch_conv_x3_img), pool1 fused
   bool front = false;  // conv0 (MODE_DIRECT) run together with the next layer (the 16-channel x3
                        // conv1) as one kernel (conv_front.hip); the next layer launches nothing
   bool out_padded = false;  // output written zero-bordered (the next layer is MODE_PATCH16 / MODE_X3;
@@ -638,6 +639,15 @@ int dnn_plan_add_max_pool(dnn_plan* p, int kh, int kw, int stride_h, int stride_
       prev.pool1 = true;
       return 0;
     }
+    // ... into a batch-tile x3 conv of a small frame (conv5 + pool5): whole-image tiles over all
+    // of K (gemm_x3_img.h) instead of K slices whose partials the pool combines
+    if (prev.type == 0 && prev.mode == MODE_X3 && !prev.x3k && !prev.x3lat && !prev.pool && !prev.pool1 &&
+        prev.C != 16 && conv_x3_img_supported(prev.C, prev.OC, prev.H, prev.W)) {
+      prev.pool1 = true;
+      prev.x3img = true;
+      prev.splits = 1;
+      return 0;
+    }
   }
   p->layers.push_back(std::move(L));
   p->cur_h = p->layers.back().OH;
@@ -949,7 +959,11 @@ int dnn_plan_run(dnn_plan* p, int n, const float* d_in, float* d_out, void* stre
                                           L.W, L.C, epi, s);
           break;
         case MODE_X3:
-          if (L.x3k) {
+          if (L.x3img) {
+            rc = launch_conv_x3_img(reinterpret_cast<const unsigned short*>(cur),
+                                    reinterpret_cast<const unsigned short*>(wt), dsplit ? nullptr : dst, dsplit, n,
+                                    L.OC, L.Npad, L.K, L.H, L.W, L.C, epi, s);
+          } else if (L.x3k) {
             rc = launch_conv_x3_ktile(reinterpret_cast<const unsigned short*>(cur),
                                       reinterpret_cast<const unsigned short*>(wt), dsplit ? nullptr : dst, dsplit,
                                       L.pool ? 4LL * n * L.PH * L.PW : Mc, L.OC, L.Npad, L.K, L.H, L.W, L.C, epi, s,
@@ -1081,7 +1095,7 @@ int dnn_plan_describe(const dnn_plan* p, char* buf, int buf_len) {
       if (L.splits > 1) snprintf(sk, sizeof(sk), " splitK=%d", L.splits);
       const bool fr = L.front || (i > 0 && p->layers[i - 1].front);
       snprintf(line, sizeof(line), "conv %dx%dx%d -> %dx%dx%d k%dx%d s%d mode=%s cfg=%d K=%d Kpad=%d%s%s%s%s%s%s\n", L.H,
-               L.W, L.C, L.out_h(), L.out_w(), L.OC, L.kh, L.kw, L.sh, L.x3lat ? "x3_lat" : L.x3k ? "x3_ktile" : kModeName[L.mode], L.cfg, L.K, L.Kpad,
+               L.W, L.C, L.out_h(), L.out_w(), L.OC, L.kh, L.kw, L.sh, L.x3lat ? "x3_lat" : L.x3k ? "x3_ktile" : L.x3img ? "x3_img" : kModeName[L.mode], L.cfg, L.K, L.Kpad,
                L.pool ? " +pool2x2s2" : L.pool1 ? " +pool2x2s1" : "", fr ? " front01" : "", sk,
                L.splits > 1 ? (L.mode == MODE_X3 ? " x3-combine" : fused_splitk(p) ? " combine" : "") : "",
                p->fp16 ? " fp16" : "", p->latency ? " latency" : "");

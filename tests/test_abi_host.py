@@ -181,9 +181,10 @@ def test_plan_shape_memory_and_flops_host_only(monkeypatch, fuse, splitk):
 def test_plan_x3_structure_host_only(monkeypatch):
     """Default fp32 batch plan: conv1-conv7 on the x3 conv (exact 3-way bf16 splits; conv1 on the
     16-channel kernel reading conv0's fp32 output, conv2 and conv3 on the 2-D tile kernel, N = 64 /
-    128), conv1-conv4 with their 2x2 pools fused, pool5 writing split planes; conv5 (N = 512) in
-    2 K slices whose partials pool5 combines; conv8 (1x1) on the 1x1 x3 conv reading conv7's split
-    planes; weights of those layers in 3 bf16 pieces."""
+    128), conv1-conv4 with their 2x2 pools fused; conv5 (N = 512) on whole-image tiles over all of
+    K with pool5 fused (x3_img; DNN_HIP_X3_IMG=0: 2 K slices whose partials pool5 combines); conv8
+    (1x1) on the 1x1 x3 conv reading conv7's split planes; weights of those layers in 3 bf16
+    pieces."""
     monkeypatch.delenv("DNN_HIP_X3", raising=False)
     monkeypatch.delenv("DNN_HIP_X3_TILE", raising=False)
     monkeypatch.delenv("DNN_HIP_X3_C16", raising=False)
@@ -196,19 +197,29 @@ def test_plan_x3_structure_host_only(monkeypatch):
     assert wb >= 4 * nparams + 2 * x3params and wb < (4 * nparams + 2 * x3params) * 1.2
     act2 = 2 * 64 * 208 * 208 * 16 * 4
     # one zero-bordered split-plane region per producer: conv1 (pooled 104x104x32), conv2
-    # (pooled 52x52x64), conv3 (pooled 26x26x128), conv4 (pooled 13x13x256), pool5 (13x13x512),
-    # conv6 and conv7 (13x13x1024 each), 6 B per element
+    # (pooled 52x52x64), conv3 (pooled 26x26x128), conv4 (pooled 13x13x256), conv5 + pool5
+    # (13x13x512), conv6 and conv7 (13x13x1024 each), 6 B per element; no split-K slab
     pad = sum(64 * 6 * (h + 2) ** 2 * c
               for h, c in ((104, 32), (52, 64), (26, 128), (13, 256), (13, 512), (13, 1024), (13, 1024)))
-    slab = 2 * 64 * 13 * 13 * 512 * 4  # conv5's two raw K-slice partials
-    assert act2 + pad + slab <= sb < act2 + pad + slab + 16384
+    assert act2 + pad <= sb < act2 + pad + 16384
     lines = _describe_yolo(64, False)
     conv = [ln for ln in lines if ln.startswith("conv")]
-    assert [i for i, ln in enumerate(conv) if "patch_x3" in ln] == [1, 2, 3, 4, 5, 6, 7]
+    assert [i for i, ln in enumerate(conv) if "patch_x3" in ln] == [1, 2, 3, 4, 6, 7]
+    assert "mode=x3_img" in conv[5] and "+pool2x2s1" in conv[5], conv[5]
     assert "mode=x3_1x1" in conv[8]
-    assert "splitK=2 x3-combine" in conv[5] and sum("splitK" in ln for ln in lines) == 1
+    assert sum("splitK" in ln for ln in lines) == 0
     assert all("+pool2x2s2" in conv[i] for i in (1, 2, 3, 4))  # pools fused into the x3 convs
-    assert sum(ln.startswith("pool") for ln in lines) == 1  # pool5 (s1, combines conv5's slices)
+    assert sum(ln.startswith("pool") for ln in lines) == 0  # pool5 fused into conv5
+    # DNN_HIP_X3_IMG=0: conv5 in 2 K slices of the wide kernel, pool5 combining their partials
+    monkeypatch.setenv("DNN_HIP_X3_IMG", "0")
+    wb0, sb0 = dnn_hip.Plan.memory(64, (416, 416, 3), entries)
+    slab = 2 * 64 * 13 * 13 * 512 * 4  # conv5's two raw K-slice partials
+    assert act2 + pad + slab <= sb0 < act2 + pad + slab + 16384
+    lines0 = _describe_yolo(64, False)
+    conv0 = [ln for ln in lines0 if ln.startswith("conv")]
+    assert "splitK=2 x3-combine" in conv0[5] and sum("splitK" in ln for ln in lines0) == 1
+    assert sum(ln.startswith("pool") for ln in lines0) == 1  # pool5 (s1, combines conv5's slices)
+    monkeypatch.delenv("DNN_HIP_X3_IMG")
     # latency plans (one frame): conv1 / conv2 on the narrow x3 kernels (small tiles), conv3-conv5
     # and conv8 on the K-split x3 kernels (pool5 fused into conv5), conv6 / conv7 on the small-M
     # x3 kernel; conv0 stays on its fp32 direct kernel
@@ -222,11 +233,11 @@ def test_plan_x3_structure_host_only(monkeypatch):
     # DNN_HIP_X3_C16=0: conv1 on the fp32 patch kernel (its pooled epilogue splits for conv2)
     monkeypatch.setenv("DNN_HIP_X3_TILE", "0")
     conv = [ln for ln in _describe_yolo(64, False) if ln.startswith("conv")]
-    assert [i for i, ln in enumerate(conv) if "patch_x3" in ln] == [1, 4, 5, 6, 7]
+    assert [i for i, ln in enumerate(conv) if "patch_x3" in ln] == [1, 4, 6, 7] and "mode=x3_img" in conv[5]
     monkeypatch.setenv("DNN_HIP_X3_TILE", "1")
     monkeypatch.setenv("DNN_HIP_X3_C16", "0")
     conv = [ln for ln in _describe_yolo(64, False) if ln.startswith("conv")]
-    assert [i for i, ln in enumerate(conv) if "patch_x3" in ln] == [2, 3, 4, 5, 6, 7] and "mode=patch " in conv[1] + " "
+    assert [i for i, ln in enumerate(conv) if "patch_x3" in ln] == [2, 3, 4, 6, 7] and "mode=patch " in conv[1] + " "
 
 
 def test_plan_errors_are_reported():
@@ -348,9 +359,10 @@ def test_latency_plan_layout():
     for i in (6, 7):
         assert "mode=x3_lat" in conv[i] and " splitK=16 x3-combine latency" in conv[i], conv[i]
     assert "mode=x3_ktile" in conv[8] and " splitK=" not in conv[8], conv[8]
-    # the batch plan at batch 1: conv1-conv7 on the x3 conv, conv5 in the (N, K) rule's 2 K slices
-    assert [l for l in base if " splitK=" in l] == [l for l in base if " splitK=2 x3-combine" in l] and \
-        sum(" splitK=2 " in l for l in base) == 1 and sum("patch_x3" in l for l in base) == 7
+    # the batch plan at batch 1: conv1-conv7 on the x3 conv (conv5 + pool5 on whole-image tiles, as
+    # at batch 64), no K split
+    assert not any(" splitK=" in l for l in base) and sum("patch_x3" in l for l in base) == 6 and \
+        sum("mode=x3_img" in l for l in base) == 1
     assert sum(" splitK=16 " in l for l in conv) == 2  # conv6/conv7 at batch 1: 48 tiles x 16
     # batch 64: latency mode leaves the (N, K)-only rule in charge of every layer that fills the chip
     assert [l.replace(" latency", "") for l in _describe_yolo(64, True)] == _describe_yolo(64, False)

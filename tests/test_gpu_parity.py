@@ -459,8 +459,8 @@ def test_plan_timing_api(yolo_b1):
         plan.run_host(x)
     ms, cnt = plan.timing_end()
     ks = plan.kernels()
-    # 10 plan kernels: conv0-8 + pool5 (combines conv5's K slices; conv4's pool is fused)
-    assert len(ms) == len(ks) == 10
+    # 9 plan kernels: conv0-8 (conv4's pool and pool5 fused: conv5 on whole-image tiles)
+    assert len(ms) == len(ks) == 9
     assert all(c == 3 for c in cnt)
     assert all(m > 0 for m in ms)
     # events around one kernel only (the bench's timed region): the others report no launches
@@ -470,7 +470,7 @@ def test_plan_timing_api(yolo_b1):
             plan.run_host(x)
         ms1, cnt1 = plan.timing_end()
         names = [k["name"] for k in ks]
-        assert [c for n, c in zip(names, cnt1) if n != only] == [0] * 9
+        assert [c for n, c in zip(names, cnt1) if n != only] == [0] * 8
         assert cnt1[names.index(only)] == 3 and ms1[names.index(only)] > 0
 
 
@@ -1455,6 +1455,75 @@ def test_x3_1x1_conv_vs_oracle(monkeypatch, case):
     assert errs["11"] <= 1.25 * errs["01"], errs
 
 
+X3_IMG_CASES = [
+    # B, last: pool 2x2 s1 -> conv3x3 256->512 + pool 2x2 s1 SAME (whole-image x3 tiles, 13x13) ->
+    # conv3x3 512->256 (x3 consumer of its split planes), or with the pool-fused conv the last layer
+    # (fp32 output)
+    (5, False), (3, True), (1, False),
+]
+
+
+@pytest.mark.parametrize("case", X3_IMG_CASES)
+def test_x3_img_conv_pool_vs_oracle(monkeypatch, case):
+    """conv3x3_x3_img_kernel (batch plans' conv5 + pool5: one 13x13 image x 128 columns per
+    workgroup over all of K, the stride-1 pool on the image's raw sums in LDS before the epilogue,
+    split planes or fp32 out): mode as planned, within the fp32 tolerance of the float64 oracle and
+    within 1.25x of the fp32-MFMA plan's error (DNN_HIP_X3=0), negative-gamma channels (the window's
+    minimum), batch rows bit-equal to one-frame runs, repeat runs identical; the K-slice form
+    (DNN_HIP_X3_IMG=0) within the same tolerance."""
+    B, last = case
+    rng = np.random.default_rng(B * 13 + int(last))
+    x = rng.standard_normal((B, 13, 13, 256)).astype(np.float32)
+
+    def layer(c, od):
+        k = (rng.standard_normal((3, 3, c, od)) * np.sqrt(2.0 / (9 * c))).astype(np.float32)
+        b = rng.standard_normal(od).astype(np.float32) * 0.1
+        gam = rng.uniform(0.5, 1.5, od).astype(np.float32)
+        gam[::5] *= -1
+        return k, b, (rng.standard_normal(od).astype(np.float32) * 0.1, rng.uniform(0.5, 1.5, od).astype(np.float32),
+                      gam)
+
+    L = [layer(256, 512)] + ([] if last else [layer(512, 256)])
+
+    def graph(shape):
+        g = dnn_hip.DnnGraphBuilder()
+        y = g.create_input(list(shape))
+        y = g.create_max_pool2d(y, [1, 2, 2, 1], [1, 1, 1, 1], "SAME")  # (an x3 producer)
+        for j, (k, b, n) in enumerate(L):
+            y = g.create_conv2d(y, k, [1, 1, 1, 1], "SAME")
+            y = g.create_bias_add(y, b)
+            y = g.create_batch_norm(y, *n, 1e-5)
+            y = g.create_leaky_relu(y)
+            if j == 0:
+                y = g.create_max_pool2d(y, [1, 2, 2, 1], [1, 1, 1, 1], "SAME")
+        g.set_out_node(y)
+        return g
+
+    ref = R.max_pool2d(x, [1, 2, 2, 1], [1, 1, 1, 1], "SAME")
+    for j, (k, b, n) in enumerate(L):
+        ref = R.leaky_relu(R.batch_norm(R.bias_add(R.conv2d(ref, k), b), *n, 1e-5))
+        if j == 0:
+            ref = R.max_pool2d(ref, [1, 2, 2, 1], [1, 1, 1, 1], "SAME")
+    errs = {}
+    for arm in ("img", "slices", "fp32"):
+        monkeypatch.setenv("DNN_HIP_X3", "0" if arm == "fp32" else "1")
+        monkeypatch.setenv("DNN_HIP_X3_IMG", "0" if arm == "slices" else "1")
+        eng = dnn_hip.DnnInferenceEngine(graph(x.shape), False)
+        conv = [ln for ln in eng.plan().describe().splitlines() if ln.startswith("conv")]
+        if arm == "img":
+            assert "mode=x3_img" in conv[0] and "+pool2x2s1" in conv[0], conv
+        y = eng.run(x)
+        errs[arm] = R.normwise_err(y, ref)
+        if arm == "img":
+            assert np.array_equal(eng.run(x), y)
+            for f in range(B):
+                one = dnn_hip.DnnInferenceEngine(graph((1,) + x.shape[1:]), False).run(x[f:f + 1])
+                assert np.array_equal(one, y[f:f + 1]), f
+    print("x3 img errs", errs)
+    assert all(e < 3 * LAYER_TOL for e in errs.values()), errs
+    assert errs["img"] <= 1.25 * errs["fp32"], errs
+
+
 X3_CHAIN_CASES = [
     # B, H, W, C0: conv3x3 C0->128 + pool 2x2 s2 (fp32 implicit GEMM writing the x3 split planes)
     # -> conv3x3 128->512 (x3, 2 K slices) -> then "pool" (2x2 s1: pool5's combine) or "conv"
@@ -1473,6 +1542,7 @@ def test_x3_split_combine_and_producer_vs_oracle(monkeypatch, case):
     tolerance of the float64 oracle and within 1.25x of the fp32-MFMA plan's error
     (DNN_HIP_X3=0), batch rows bit-equal to batch-1 runs; negative-gamma channels throughout."""
     B, H, W, C0, mid = case
+    monkeypatch.setenv("DNN_HIP_X3_IMG", "0")  # (the K-slice form; whole-image tiles: test_x3_img_*)
     rng = np.random.default_rng(B * 7 + C0)
     x = rng.standard_normal((B, H, W, C0)).astype(np.float32)
 

@@ -5,6 +5,7 @@ order rotated per round; a child pre-heats the batch-64 plan for --preheat secon
 median over rounds of each kernel's mean time and of the forward.
 
   python tools/lib_ab.py --lib libdnn_hip.so --lib diag/libdnn_hip_old.so [--rounds 4] [--precision fp16]
+  python tools/lib_ab.py --env DNN_HIP_X3_IMG=1,0   (plan-time switches: one child per arm)
 """
 import argparse
 import json
@@ -60,6 +61,7 @@ def child(a):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--lib", action="append", default=[])
+    ap.add_argument("--env", default=None, help="VAR=v1,v2,...: arms over an environment variable")
     ap.add_argument("--rounds", type=int, default=4)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--preheat", type=float, default=2.0)
@@ -70,11 +72,17 @@ def main():
     if a.child:
         child(a)
         return
-    res = {lib: [] for lib in a.lib}
+    arms = []  # (name, env overrides)
+    if a.env:
+        var, vals = a.env.split("=", 1)
+        arms = [("%s=%s" % (var, v), {var: v}) for v in vals.split(",")]
+    else:
+        arms = [(lib, {"DNN_HIP_LIB": lib}) for lib in a.lib]
+    res = {name: [] for name, _ in arms}
     for r in range(a.rounds):
-        order = a.lib[r % len(a.lib):] + a.lib[:r % len(a.lib)]
-        for lib in order:
-            env = dict(os.environ, DNN_HIP_LIB=lib)
+        order = arms[r % len(arms):] + arms[:r % len(arms)]
+        for lib, over in order:
+            env = dict(os.environ, **over)
             out = subprocess.run([sys.executable, os.path.abspath(__file__), "--child", "--iters", str(a.iters),
                                   "--preheat", str(a.preheat), "--batch", str(a.batch), "--precision", a.precision],
                                  env=env, capture_output=True, text=True, timeout=600)
@@ -87,7 +95,7 @@ def main():
     for lib, rs in res.items():
         ks = rs[0]["kernels"].keys()
         med = {k: round(statistics.median(x["kernels"][k] for x in rs), 4) for k in ks}
-        print(json.dumps({"lib": lib, "fwd_ms_median": round(statistics.median(x["fwd_ms"] for x in rs), 4),
+        print(json.dumps({"arm": lib, "fwd_ms_median": round(statistics.median(x["fwd_ms"] for x in rs), 4),
                           "kernels_ms_median": med}))
 
 

@@ -22,6 +22,8 @@ from collections import defaultdict
 # convN.reduce kernel after each)
 ORDER = ["conv0.direct", "conv1.gemm", "conv2.gemm", "conv3.gemm", "conv4.gemm", "conv5.gemm", "pool5",
          "conv6.gemm", "conv7.gemm", "conv8.gemm"]
+# (round 5: pool5 fused into conv5's whole-image x3 kernel -- the same list without "pool5";
+# dispatch_sequence picks the variant whose length matches the trace's forward period)
 # (the same kernel list with DNN_HIP_X3=0: conv5-7 split-K combined in the GEMM)
 # ... the fp16 plan (dnn_plan_set_precision 1): conv1 patch kernel, f16->f32 output conversion
 ORDER_FP16 = ["conv0.direct", "conv1.patch", "conv2.gemm", "conv3.gemm", "conv4.gemm", "conv5.gemm", "pool5",
@@ -68,6 +70,9 @@ def dispatch_sequence(rows, key_start="Start_Timestamp", key_end="End_Timestamp"
             first = name  # the first dispatch of the first forward defines the start marker
             if "conv01_front" in name:  # conv0 + conv1 as one kernel (conv_front.hip)
                 order = ["conv0+1.gemm"] + [k for k in ORDER if k not in ("conv0.direct", "conv1.gemm")]
+            starts = [j for j in range(i, len(seq)) if seq[j]["Kernel_Name"] == first]
+            if len(starts) > 1 and starts[1] - starts[0] == len(order) - 1 and "pool5" in order:
+                order = [k for k in order if k != "pool5"]  # pool5 fused into conv5 (x3_img)
         if name == first and i + len(order) <= len(seq):
             for j, pk in enumerate(order):
                 out.append((pk, seq[i + j]))

@@ -116,6 +116,28 @@ def main():
                       ("team B MFMA steps", 3), ("team B store steps", 4), ("team B barrier waits", 5),
                       ("total (wave 0)", 6)):
             print("  %-22s %10.0f" % (nm, statistics.median(r[i] for r in rows)))
+    fa = getattr(plan.lib, "dnn_acc2_diag_stamps", None)
+    if fa is not None:  # X3DIAG 8192: the wide kernel's phases per layer class
+        fa.restype = ctypes.c_int
+        fa.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        ab = (ctypes.c_ulonglong * (3 * 512 * 8))()
+        assert fa(ab, 3 * 512) == 0
+        for li, name in enumerate(("conv4 (N = 256)", "conv5 (N = 512)", "conv6/7 (N = 1024, last)")):
+            rows = [list(ab[(li * 512 + w) * 8:(li * 512 + w) * 8 + 8]) for w in range(512)]
+            rows = [r for r in rows if r[5] > 0 and r[4] > 0]
+            if not rows:
+                continue
+            print("%s: %d workgroups, median cycles" % (name, len(rows)))
+            for nm, a, b in (("prologue", 1, 2), ("main loop", 2, 3), ("epilogue", 3, 4), ("total", 1, 4)):
+                v = sorted(r[b] - r[a] for r in rows)
+                print("  %-10s %8.0f  (p10 %6.0f, p90 %6.0f)" % (nm, statistics.median(v), v[len(v) // 10], v[len(v) * 9 // 10]))
+            t0 = min(r[0] for r in rows)
+            t1 = max(r[5] for r in rows)
+            st = sorted((r[0] - t0) * 10e-3 for r in rows)
+            en = sorted((r[5] - t0) * 10e-3 for r in rows)
+            cyc = statistics.median([(r[4] - r[1]) / max(r[5] - r[0], 1) for r in rows]) * 100
+            print("  span %.1f us, clock ~%.0f MHz; starts p50 %.1f max %.1f us; ends p10 %.1f p50 %.1f max %.1f us" %
+                  ((t1 - t0) * 10e-3, cyc, st[len(st) // 2], st[-1], en[len(en) // 10], en[len(en) // 2], en[-1]))
     fn = getattr(plan.lib, "dnn_tile2_diag_stamps", None)
     if fn is None:
         print("no dnn_tile2_diag_stamps: not an X3DIAG 1024 build")
