@@ -911,6 +911,18 @@ extern "C" __attribute__((visibility("default"))) int dnn_tile2_diag_stamps(unsi
 }
 #endif
 
+#if (X3DIAG & 16384) != 0
+// diagnostic builds (X3DIAG bit 16384): conv3x3_x3_img_kernel's per-workgroup phase stamps of its
+// last launch (8 per workgroup) copied to host[0 .. 8 n)
+extern "C" __attribute__((visibility("default"))) int dnn_img_diag_stamps(unsigned long long* host, int n) {
+  if (n < 0 || n > dnnhip::IMG_DIAG_WGS) return -2;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(dnnhip::img_diag_stamps), (size_t)n * 8 * sizeof(unsigned long long), 0,
+                             hipMemcpyDeviceToHost) == hipSuccess
+             ? 0
+             : -1;
+}
+#endif
+
 #if (X3DIAG & 8192) != 0
 // diagnostic builds (X3DIAG bit 8192): conv3x3_x3_acc2_kernel's per-workgroup phase stamps of its
 // last launch per layer class (N = 256 / 512 / other; 8 per workgroup) copied to host[0 .. 8 n)

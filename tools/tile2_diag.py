@@ -116,6 +116,20 @@ def main():
                       ("team B MFMA steps", 3), ("team B store steps", 4), ("team B barrier waits", 5),
                       ("total (wave 0)", 6)):
             print("  %-22s %10.0f" % (nm, statistics.median(r[i] for r in rows)))
+    fi = getattr(plan.lib, "dnn_img_diag_stamps", None)
+    if fi is not None:  # X3DIAG 16384: the whole-image kernel's phases (conv5 + pool5)
+        fi.restype = ctypes.c_int
+        fi.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        ib = (ctypes.c_ulonglong * (512 * 8))()
+        assert fi(ib, 512) == 0
+        rows = [list(ib[8 * w:8 * w + 8]) for w in range(512) if ib[8 * w + 7] > 0]
+        print("conv5 + pool5 (whole-image tiles): %d workgroups, median cycles" % len(rows))
+        for nm, a, b in (("prologue", 1, 2), ("loop (wave 0)", 2, 3), ("loop (wave 7)", 2, 4),
+                         ("fold + stage", 3, 5), ("pool/epilogue/stores", 5, 6), ("total", 1, 6)):
+            v = sorted(r[b] - r[a] for r in rows)
+            print("  %-24s %8.0f  (p10 %6.0f, p90 %6.0f)" % (nm, statistics.median(v), v[len(v) // 10], v[len(v) * 9 // 10]))
+        t0 = min(r[0] for r in rows)
+        print("  span %.1f us" % ((max(r[7] for r in rows) - t0) * 10e-3))
     fa = getattr(plan.lib, "dnn_acc2_diag_stamps", None)
     if fa is not None:  # X3DIAG 8192: the wide kernel's phases per layer class
         fa.restype = ctypes.c_int
