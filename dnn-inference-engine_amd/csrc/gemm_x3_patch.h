@@ -1049,7 +1049,7 @@ conv3x3_x3_tile2_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __res
 // that four buffers fit: 0.92 modelled extra cycles per fragment read either way); one stage area
 // (the teams' store steps never overlap) and the epilogue parameters.  The row table is computed
 // per window (no team-wide barrier inside a step).
-template <int TH, int TW, int WM, int WN, int TM, int NCH, int PU, int SK, int FL = -1>
+template <int TH, int TW, int WM, int WN, int TM, int NCH, int PU, int SK, int FL = -1, int PPLEAD = 1>
 __global__ void __launch_bounds__(512, 1)
 conv3x3_x3_pp_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __restrict__ Bt,
                      bf16_bits* __restrict__ out_split, int N, EpiParams epi, int tilesX, int tilesY, int ntiles,
@@ -1187,8 +1187,13 @@ conv3x3_x3_pp_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __restri
 #pragma unroll
       for (int c = 0; c < NCH; ++c) {
         const unsigned char* Pc = P + c * BUFB;
-        bf16x8 af[2][3];
-        frag(Pc, 0, 0, af[0]);
+        // fragments PPLEAD row blocks ahead through a ring of PPLEAD + 1 sets (9 TM a multiple of
+        // the ring: every chunk starts at slot 0)
+        constexpr int RING = PPLEAD + 1, NBC = 9 * TM;
+        static_assert(NCH == 1 || NBC % RING == 0, "fragment ring phase per chunk");
+        bf16x8 af[RING][3];
+#pragma unroll
+        for (int l = 0; l < PPLEAD; ++l) frag(Pc, l % TM, l / TM, af[l]);
 #pragma unroll
         for (int tp = 0; tp < 9; ++tp) {
           const int s = 9 * c + tp;
@@ -1197,21 +1202,12 @@ conv3x3_x3_pp_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __restri
           if (s + 2 < NK && (X3DIAG & 4096) == 0) load_b(s + 2, bq[(s + 2) % 3]);
 #pragma unroll
           for (int i = 0; i < TM; ++i) {
-            const int cur = i & 1, nxt = cur ^ 1;
-            if (i + 1 < TM)
-              frag(Pc, i + 1, tp, af[nxt]);
-            else if (tp < 8)
-              frag(Pc, 0, tp + 1, af[nxt]);
+            const int bi = TM * tp + i;
+            if (bi + PPLEAD < NBC) frag(Pc, (bi + PPLEAD) % TM, (bi + PPLEAD) / TM, af[(bi + PPLEAD) % RING]);
             const bf16x8(&bb)[3][2] = bq[(X3DIAG & 4096) != 0 ? 0 : s % 3];
 #pragma unroll
-            for (int jb = 0; jb < 2; ++jb) x3_step<true>(acc[i][jb], accc[i][jb], af[cur], bb, jb);
+            for (int jb = 0; jb < 2; ++jb) x3_step<true>(acc[i][jb], accc[i][jb], af[bi % RING], bb, jb);
             __builtin_amdgcn_sched_barrier(0);
-          }
-          if constexpr (TM & 1) {
-            if (tp < 8) {
-#pragma unroll
-              for (int p = 0; p < 3; ++p) af[0][p] = af[1][p];
-            }
           }
         }
       }

@@ -519,14 +519,15 @@ int launch_conv_x3(const bf16_bits* in_split, const bf16_bits* Bt, float* out, b
         kind == 1 && C == 32 && N == 64) {
       const int G = device_cu_count();
       const int prio = !getenv_flag_off("DNN_HIP_X3_PP_PRIO");
-#define X3PP(TH_, WM_, WN_, NCH_, PU_, SK_, FL_)                                                                   \
-  hipLaunchKernelGGL((conv3x3_x3_pp_kernel<TH_, 26, WM_, WN_, X3T_TM, NCH_, PU_, SK_, FL_>), dim3((unsigned)G),     \
-                     dim3(512), 0, stream, in_split, Bt, out_split, N, epi, tilesX, tilesY, (int)blocks, xg,       \
+#define X3PP(TH_, WM_, WN_, NCH_, PU_, SK_, FL_, LEAD_)                                                             \
+  hipLaunchKernelGGL((conv3x3_x3_pp_kernel<TH_, 26, WM_, WN_, X3T_TM, NCH_, PU_, SK_, FL_, LEAD_>), dim3((unsigned)G), \
+                     dim3(512), 0, stream, in_split, Bt, out_split, N, epi, tilesX, tilesY, (int)blocks, xg,         \
                      (unsigned)in_bytes, (unsigned)b_bytes, prio)
+      // (fragments two row blocks ahead: conv2 0.1130 -> 0.1118 ms against one, same call)
       if (yolo)
-        X3PP(8, 2, 2, 1, 14, 0, X3_YOLO_FL);
+        X3PP(8, 2, 2, 1, 14, 0, X3_YOLO_FL, 2);
       else
-        X3PP(8, 2, 2, 1, 14, 0, -1);
+        X3PP(8, 2, 2, 1, 14, 0, -1, 2);
 #undef X3PP
       return check_x3("conv_x3 (ping-pong)");
     }
