@@ -30,6 +30,26 @@ cp $D/fused_trace/fused_trace_kernel_stats.csv $P/${R}_rocprof_kernel_stats.csv
 cp $D/unf_trace/unf_trace_kernel_stats.csv $P/${R}_rocprof_kernel_stats_unfused.csv
 cp $D/f16_trace/f16_trace_kernel_stats.csv $P/${R}_rocprof_kernel_stats_fp16.csv
 cp $B/bench.json $P/${R}_bench.json
+# the committed bench line's rocprof fields from THIS call's trace and PMC passes (bench.py read the
+# previous round's summary when it ran): same box, same build
+python3 - "$P/${R}_bench.json" "$P/pmc_summary.json" <<'PYEOF'
+import json, sys
+b = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
+p = json.load(open(sys.argv[2]))
+r = b["roofline"]
+k = p["kernels"].get(r["kernel"], {})
+if k.get("avg_us"):
+    mult = r["achieved"] * r["avg_launch_ms"] / 1e3 / (r["flops_per_launch"] / 1e12) if r.get("flops_per_launch") else 6.0
+    r["rocprof_avg_launch_ms"] = round(k["avg_us"] / 1e3, 4)
+    r["rocprof_frac"] = round(mult * r["flops_per_launch"] / (k["avg_us"] / 1e6) / 1e12 / r["peak"], 4)
+    r["rocprof_same_box"] = p.get("same_box")
+    r["rocprof_source"] = "profiles/pmc_summary.json: rocprofv3 --kernel-trace of bench.py in the same gpurun call (same box) as this line"
+if k.get("hbm_bytes_per_launch"):
+    r["traffic"] = k["hbm_bytes_per_launch"]
+    if r.get("algorithmic_bytes"):
+        r["traffic_over_algorithmic"] = round(k["hbm_bytes_per_launch"] / r["algorithmic_bytes"], 2)
+open(sys.argv[1], "w").write(json.dumps(b) + "\n")
+PYEOF
 python3 tools/pmc_table.py $D/pmc_sqa/*counter_collection.csv $D/pmc_sqb/*counter_collection.csv \
   --out $P/${R}_sq_counters_fp32.json > /dev/null
 echo done
