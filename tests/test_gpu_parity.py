@@ -1603,7 +1603,8 @@ def test_x3_split_combine_and_producer_vs_oracle(monkeypatch, case):
 
 X3_POOL_CASES = [
     # B, H, W, C: pool (2x2 s1) -> conv3x3 C->256 + pool 2x2 s2 fused into the x3 conv (rows
-    # pool-window-major) -> conv3x3 256->512 (x3, 2 K slices) -> pool 2x2 s1 (combine)
+    # pool-window-major) -> conv3x3 256->512 + pool 2x2 s1 (13x13: whole-image x3 tiles with the
+    # pool fused; else x3 in 2 K slices + the pool's combine)
     (8, 26, 26, 128),   # conv4-like
     (3, 13, 13, 64),    # odd: ragged windows (cells past the edge repeat cell (0, 0))
 ]
@@ -1653,7 +1654,10 @@ def test_x3_pool_fused_vs_oracle(monkeypatch, case):
         if x3 == "1":
             conv = [ln for ln in eng.plan().describe().splitlines() if ln.startswith("conv")]
             assert "mode=patch_x3" in conv[0] and "+pool2x2s2" in conv[0], conv
-            assert "mode=patch_x3" in conv[1] and "splitK=2 x3-combine" in conv[1], conv
+            if H // 2 == 13:  # 13x13 frames: whole-image tiles with the stride-1 pool fused
+                assert "mode=x3_img" in conv[1] and "+pool2x2s1" in conv[1], conv
+            else:
+                assert "mode=patch_x3" in conv[1] and "splitK=2 x3-combine" in conv[1], conv
         y = eng.run(x)
         errs[x3] = R.normwise_err(y, ref)
         print("x3=%s pool-fused chain normwise err %.3e" % (x3, errs[x3]))
