@@ -459,11 +459,12 @@ int launch_conv0_mfma_f16(const float* in, const float* w, half_t* out, const Di
 
 // ------------------------------------------------------------------------------ conv1 fp16
 // in: fp16 NHWC [B][H][W][16]; Bt: packed fp16 weights [32][ldb] (k = tap*16 + c, ldb >= 144);
-// out: fp16 pooled [B][PH][PW][32].  SAME 3x3 stride 1, even OH/OW.
+// out: fp16 pooled [B][PH][PW][32] (opad: the interior of a zero-bordered [B][PH+2][PW+2][32]
+// buffer, the tile kernel's input).  SAME 3x3 stride 1, even OH/OW.
 __global__ void __launch_bounds__(256)
 conv1_patch_f16_kernel(const half_t* __restrict__ in, const half_t* __restrict__ Bt, int ldb,
                        half_t* __restrict__ out, DirectGeom g, int tilesX, int tilesY, const float* __restrict__ zero,
-                       EpiParams epi) {
+                       EpiParams epi, int opad) {
   constexpr int C = 16;
   constexpr int PATCH = SC_P * SC_P * C;      // halves
   constexpr int PATCH_CH = (PATCH * 2 + 1023) / 1024;  // 1-KiB DMA chunks
@@ -541,7 +542,7 @@ conv1_patch_f16_kernel(const half_t* __restrict__ in, const half_t* __restrict__
     for (int i = 0; i < 4; ++i) {
       const int wy = (y0 >> 1) + 2 * wid + (i >> 1), wx = (x0 >> 1) + 4 * (i & 1) + fp;
       if (wy < g.PH && wx < g.PW)
-        store_out(out + (((size_t)b * g.PH + wy) * g.PW + wx) * 32 + n,
+        store_out(out + (((size_t)b * (g.PH + 2 * opad) + wy + opad) * (g.PW + 2 * opad) + wx + opad) * 32 + n,
                   pool_then_epilogue(acc[i][j], pb, pm, ps, pg, epi.flags));
     }
   }
@@ -554,7 +555,7 @@ bool conv1_patch_f16_supported(int C, int OC, int H, int W, int OH, int OW, int 
 }
 
 int launch_conv1_patch_f16(const half_t* in, const half_t* Bt, int ldb, half_t* out, const DirectGeom& g,
-                           const float* zero, const EpiParams& epi, hipStream_t s) {
+                           const float* zero, const EpiParams& epi, hipStream_t s, int opad) {
   if (g.B == 0) return 0;
   if (ldb < 144 || ldb % 8 || g.OH % 2 || g.OW % 2 || g.PH != g.OH / 2 || g.PW != g.OW / 2 || g.pt != 1 ||
       g.pl != 1 || !zero) {
@@ -564,7 +565,7 @@ int launch_conv1_patch_f16(const half_t* in, const half_t* Bt, int ldb, half_t* 
   const int tilesX = (g.OW + SC_T - 1) / SC_T, tilesY = (g.OH + SC_T - 1) / SC_T;
   const long long blocks = (long long)g.B * tilesX * tilesY;
   hipLaunchKernelGGL(conv1_patch_f16_kernel, dim3((unsigned)blocks), dim3(256), 0, s, in, Bt, ldb, out, g, tilesX,
-                     tilesY, zero, epi);
+                     tilesY, zero, epi, opad);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
     set_error("launch conv1_patch_f16: %s", hipGetErrorString(e));

@@ -272,6 +272,13 @@ int launch_conv_x3_lat(const unsigned short* in_split, const unsigned short* Bt,
 int launch_x3_combine(const float* part, int splits, long long slab, const EpiParams& epi, const PoolGeom& g,
                       float* out, unsigned short* out_split, hipStream_t s);
 int patch16_pack_order();  // launch_pack_weights order of the patch kernel's MFMA shape (3 or 4)
+// fp16 3x3/s1/SAME conv + 2x2/s2 pool on 2-D tiles (gemm_f16_tile.h: conv2-conv4 of the fp16 path),
+// zero-bordered input [B][H+2][W+2][C] (C % 32 == 0, N % 64 == 0, H, W even), weights packed
+// by launch_pack_weights order 5; out_padded: the pooled output zero-bordered too
+bool conv_tile16_supported(int C, int OC, int H, int W, int OH, int OW, int kh, int kw, int sh, int sw, int pt,
+                           int pl);
+int launch_conv_tile16(const half_t* in_padded, const half_t* Bt, int ldb, half_t* out, int out_padded, int n, int N,
+                       int K, int H, int W, int C, const EpiParams& epi, hipStream_t stream);
 int launch_conv_patch16(const half_t* in_padded, const half_t* Bt, int ldb, half_t* out, int out_padded, long long M,
                         int N, int K, int H, int W, int C, const EpiParams& epi, hipStream_t stream);
 // conv0 direct kernel with an fp16 output (fp32 input frames)
@@ -294,7 +301,7 @@ int launch_conv01_front(const float* in, const float* w0, const EpiParams& epi0,
 bool conv1_patch_f16_supported(int C, int OC, int H, int W, int OH, int OW, int kh, int kw, int sh, int sw, int pt,
                                int pl);
 int launch_conv1_patch_f16(const half_t* in, const half_t* Bt, int ldb, half_t* out, const DirectGeom& g,
-                           const float* zero, const EpiParams& epi, hipStream_t s);
+                           const float* zero, const EpiParams& epi, hipStream_t s, int opad = 0);
 
 // element-wise ops of the per-op ABI
 int launch_bias_add(const float* in, const float* b, float* out, long long n, int C, hipStream_t s);

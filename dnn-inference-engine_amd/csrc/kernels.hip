@@ -806,7 +806,7 @@ __global__ void pack_weights_kernel(const float* __restrict__ w, float* __restri
       const long long e = i & 7, lane = (i >> 3) & 63, kq = (i >> 9) % (Kpad / 16), nb = (i >> 9) / (Kpad / 16);
       n = (int)(nb * 32 + (lane & 31));
       k = (int)(kq * 16 + 8 * (lane >> 5) + e);
-    } else if (order == 4) {  // ... for 16x16x32: [n/16][k/32][lane][8]
+    } else if (order == 4 || order == 5) {  // ... for 16x16x32: [n/16][k/32][lane][8]
       const long long e = i & 7, lane = (i >> 3) & 63, kq = (i >> 9) % (Kpad / 32), nb = (i >> 9) / (Kpad / 32);
       n = (int)(nb * 16 + (lane & 15));
       k = (int)(kq * 32 + 8 * (lane >> 4) + e);
@@ -818,10 +818,12 @@ __global__ void pack_weights_kernel(const float* __restrict__ w, float* __restri
         int tap = k / C, c = k - tap * C;
         int dy = tap / kw, dx = tap - dy * kw;
         src = (c * kh + dy) * kw + dx;
-      } else if (order >= 2) {  // k = (chunk * taps + tap) * 64 + cc, c = 64 * chunk + cc (conv_patch16)
-        const int taps = kh * kw, blk = k / 64, cc = k - blk * 64;
+      } else if (order >= 2) {  // k = (chunk * taps + tap) * cw + cc, c = cw * chunk + cc (conv_patch16: cw
+        // 64; order 5, conv_tile16: 32-channel chunks)
+        const int cw = order == 5 ? 32 : 64;
+        const int taps = kh * kw, blk = k / cw, cc = k - blk * cw;
         const int chunk = blk / taps, tap = blk - chunk * taps;
-        src = tap * C + 64 * chunk + cc;
+        src = tap * C + cw * chunk + cc;
       }
       v = w[(long long)src * N + n];
     }

@@ -2,10 +2,12 @@
 // small fp16 kernels around it (weight / activation conversion, 2x2 max pool, split-K
 // reduce).  Activations are NHWC fp16 between layers, accumulation and epilogue fp32.
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <cfloat>
 #include "dnn_common.h"
 #include "gemm_f16.h"
 #include "gemm_f16_acc.h"
+#include "gemm_f16_tile.h"
 
 namespace dnnhip {
 
@@ -352,4 +354,111 @@ int launch_conv_patch16(const half_t* in_padded, const half_t* Bt, int ldb, half
   return check16("conv_patch16");
 }
 
+// ---- conv3x3_f16_tile_kernel (gemm_f16_tile.h): conv2-conv4 of the fp16 path, 2-D tiles with the
+// 2x2/s2 pool fused; weights packed in order 5 ([n/16][k/32][lane][8], 32-channel chunks)
+struct Tile16Shape {
+  int th, tw, wm, tm;
+};
+static constexpr Tile16Shape kTile16[] = {{8, 52, 4, 7}, {4, 52, 2, 7}, {8, 26, 2, 7}};
+
+// DNN_HIP_TILE16=0 keeps these layers on the implicit fp16 GEMM (A/B experiments)
+static bool tile16_enabled() {
+  const char* e = getenv("DNN_HIP_TILE16");
+  return !(e && e[0] == '0');
+}
+
+// the tile shape computing the fewest rows for the frame (ties: the first, the widest workgroup)
+static int tile16_shape(int H, int W) {
+  int best = 0;
+  long long bw = -1;
+  for (int i = 0; i < 3; ++i) {
+    const Tile16Shape& t = kTile16[i];
+    const long long rows = (long long)((H + t.th - 1) / t.th) * ((W + t.tw - 1) / t.tw) * t.wm * t.tm * 16;
+    if (bw < 0 || rows < bw) best = i, bw = rows;
+  }
+  return best;
+}
+
+bool conv_tile16_supported(int C, int OC, int H, int W, int OH, int OW, int kh, int kw, int sh, int sw, int pt,
+                           int pl) {
+  return kh == 3 && kw == 3 && sh == 1 && sw == 1 && pt == 1 && pl == 1 && OH == H && OW == W && C % 32 == 0 &&
+         OC % 64 == 0 && H % 2 == 0 && W % 2 == 0 && H >= 2 && W >= 2 && tile16_enabled() &&
+         (long long)(H + 2) * (W + 2) * C * 2 < 0x40000000LL && (long long)OC * 9 * C * 2 < 0x80000000LL;
+}
+
+template <int SH, int WN, int FL>
+static void tile16_launch(dim3 grid, hipStream_t s, const half_t* in, const half_t* Bt, int ldb, half_t* out, int N,
+                          const EpiParams& epi, int tilesX, int tilesY, int tilesN, int nsp, const Tile16Geom& g,
+                          unsigned in_bytes, unsigned b_bytes) {
+  constexpr Tile16Shape t = kTile16[SH];
+  hipLaunchKernelGGL((conv3x3_f16_tile_kernel<t.th, t.tw, t.wm, WN, t.tm, FL>), grid, dim3(64 * t.wm * WN), 0, s, in,
+                     Bt, ldb, out, N, epi, tilesX, tilesY, tilesN, nsp, g, in_bytes, b_bytes);
+}
+
+// persistent workgroups per CU (two: the kernel's registers allow two waves per SIMD);
+// DNN_HIP_TILE16_WGS=n overrides it, 0 = one tile per workgroup
+static int tile16_wgs_per_cu() {
+  const char* e = getenv("DNN_HIP_TILE16_WGS");
+  return e ? atoi(e) : 2;
+}
+
+int launch_conv_tile16(const half_t* in_padded, const half_t* Bt, int ldb, half_t* out, int out_padded, int n, int N,
+                       int K, int H, int W, int C, const EpiParams& epi, hipStream_t stream) {
+  if (n == 0 || N == 0) return 0;
+  if (!conv_tile16_supported(C, N, H, W, H, W, 3, 3, 1, 1, 1, 1) || K != 9 * C || ldb < K || ldb % 32 != 0) {
+    set_error("conv_tile16: unsupported shape N=%d K=%d %dx%dx%d ldb=%d", N, K, H, W, C, ldb);
+    return -2;
+  }
+  const int sh = tile16_shape(H, W);
+  const Tile16Shape& t = kTile16[sh];
+  const int wn = (sh != 0 && N % 128 == 0) ? 2 : 1;
+  const int tilesX = (W + t.tw - 1) / t.tw, tilesY = (H + t.th - 1) / t.th, tilesN = N / (64 * wn);
+  const Tile16Geom g{H, W, C, H / 2, W / 2, out_padded};
+  const long long img_in = (long long)(H + 2) * (W + 2) * C * 2;
+  const long long img_out = (long long)(H / 2 + 2 * out_padded) * (W / 2 + 2 * out_padded) * N;  // halves
+  const unsigned b_bytes = (unsigned)((long long)N * ldb * 2);
+  constexpr int F16YOLO = EPI_BN_AB | EPI_LEAKY_F32;  // the fp16 path's folded epilogue, compiled in
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  const int wpc = tile16_wgs_per_cu();
+  // frames per launch: the input's byte offsets stay 32-bit
+  const int per = (int)std::min<long long>(n, 0x7fffffffLL / img_in);
+  for (int f0 = 0; f0 < n; f0 += per) {
+    const int nf = std::min(per, n - f0);
+    const half_t* in = in_padded + (size_t)f0 * (img_in / 2);
+    half_t* o = out + (size_t)f0 * img_out;
+    const int nsp = nf * tilesY * tilesX;
+    const int G = wpc > 0 ? std::max(1, std::min(nsp, wpc * cus / tilesN)) : nsp;  // workgroups per column group
+    const dim3 grid((unsigned)(G * tilesN));
+    const unsigned ib = (unsigned)(nf * img_in);
+#define T16_GO(SH, WN, FL) \
+  tile16_launch<SH, WN, FL>(grid, stream, in, Bt, ldb, o, N, epi, tilesX, tilesY, tilesN, nsp, g, ib, b_bytes)
+    const bool y = epi.flags == F16YOLO;
+    if (sh == 0)
+      y ? T16_GO(0, 1, F16YOLO) : T16_GO(0, 1, -1);
+    else if (sh == 1)
+      wn == 2 ? (y ? T16_GO(1, 2, F16YOLO) : T16_GO(1, 2, -1)) : (y ? T16_GO(1, 1, F16YOLO) : T16_GO(1, 1, -1));
+    else
+      wn == 2 ? (y ? T16_GO(2, 2, F16YOLO) : T16_GO(2, 2, -1)) : (y ? T16_GO(2, 1, F16YOLO) : T16_GO(2, 1, -1));
+#undef T16_GO
+    const int rc = check16("conv_tile16");
+    if (rc) return rc;
+  }
+  return 0;
+}
+
 }  // namespace dnnhip
+
+#if T16DIAG
+// diagnostic builds: conv3x3_f16_tile_kernel's phase stamps (gemm_f16_tile.h), class k (0: C 32,
+// 1: C 64, 2: other) of the last launch, n workgroups x 32 slots
+extern "C" __attribute__((visibility("default"))) int dnn_t16_diag_stamps(unsigned long long* host, int k, int n) {
+  if (k < 0 || k > 2 || n < 0 || n > dnnhip::T16_DIAG_WGS) return -2;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(dnnhip::t16_diag_stamps), (size_t)n * 32 * sizeof(unsigned long long),
+                             (size_t)k * dnnhip::T16_DIAG_WGS * 32 * sizeof(unsigned long long),
+                             hipMemcpyDeviceToHost) == hipSuccess
+             ? 0
+             : -1;
+}
+#endif
+

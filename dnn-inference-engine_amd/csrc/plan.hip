@@ -86,13 +86,16 @@ static size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 using namespace dnnhip;
 
 // MODE_PATCH16: fp16 3x3 conv on a zero-bordered input (conv3x3_f16_acc_kernel; conv6/conv7)
+// MODE_TILE16: fp16 3x3 conv + 2x2/s2 pool on 2-D tiles of a zero-bordered input
+//   (conv3x3_f16_tile_kernel; conv2-conv4)
 // MODE_X3: fp32 3x3 conv on the bf16 MFMA with exact 3-way splits, split zero-bordered input
 // (conv3x3_x3_patch_kernel; conv6/conv7 of the fp32 path)
 // MODE_X3_1X1: fp32 1x1 conv with the same arithmetic on its producer's split planes
 // (conv1x1_x3_kernel; conv8 of the fp32 path)
 enum ConvMode : int { MODE_GEMM = 0, MODE_DIRECT_A = 1, MODE_IMPLICIT = 2, MODE_DIRECT = 3, MODE_PATCH = 4,
-                      MODE_PATCH16 = 5, MODE_X3 = 6, MODE_X3_1X1 = 7 };
-static const char* kModeName[] = {"gemm", "direct_a", "implicit", "direct", "patch", "patch16", "patch_x3", "x3_1x1"};
+                      MODE_PATCH16 = 5, MODE_X3 = 6, MODE_X3_1X1 = 7, MODE_TILE16 = 8 };
+static const char* kModeName[] = {"gemm", "direct_a", "implicit", "direct", "patch", "patch16", "patch_x3", "x3_1x1",
+                                  "tile16"};
 
 struct PlanLayer {
   int type = 0;  // 0 conv, 1 pool
@@ -608,6 +611,25 @@ int dnn_plan_add_max_pool(dnn_plan* p, int kh, int kw, int stride_h, int stride_
             conv1_patch_f16_supported(prev.C, prev.OC, prev.H, prev.W, prev.OH, prev.OW, prev.kh, prev.kw, prev.sh,
                                       prev.sw, prev.pt, prev.pl))
           prev.mode = MODE_PATCH;  // fp16 patch kernel on the same fp16 Bt
+        // fp16 3x3 layers whose producer can write a zero-bordered output (a separate pool, the
+        // conv1 patch kernel, another tile or patch16 conv): the 2-D tile kernel (its weights
+        // packed in order 5 into the same Npad x Kpad slot)
+        if (p->fp16 && prev.mode == MODE_IMPLICIT && prev.splits == 1 && p->layers.size() >= 2 &&
+            conv_tile16_supported(prev.C, prev.OC, prev.H, prev.W, prev.OH, prev.OW, prev.kh, prev.kw, prev.sh,
+                                  prev.sw, prev.pt, prev.pl) &&
+            prev.Kpad % 32 == 0) {
+          PlanLayer& q = p->layers[p->layers.size() - 2];
+          if (q.type == 1 || (q.type == 0 && (q.mode == MODE_PATCH16 || q.mode == MODE_TILE16 ||
+                                              (q.mode == MODE_PATCH && q.pool)))) {
+            prev.mode = MODE_TILE16;
+            q.out_padded = true;
+          }
+        }
+      } else if (p->fp16 && prev.mode == MODE_PATCH16 &&
+                 conv_tile16_supported(prev.C, prev.OC, prev.H, prev.W, prev.OH, prev.OW, prev.kh, prev.kw, prev.sh,
+                                       prev.sw, prev.pt, prev.pl)) {
+        prev.mode = MODE_TILE16;  // (its producer already writes the zero-bordered input) the pool fused
+        ok = true;
       } else if (prev.mode == MODE_GEMM && direct_conv_pool_supported(prev.C, prev.OC, prev.kh, prev.kw, prev.sh,
                                                                       prev.sw)) {
         prev.mode = MODE_DIRECT;
@@ -693,7 +715,7 @@ static int upload_weights(dnn_plan* p) {
       if (hipMemcpy(tmp, L.w.data(), wb, hipMemcpyHostToDevice) != hipSuccess) rc = -1;
       if (p->fp16) {
         if (!rc)
-          rc = launch_pack_weights(tmp, packed32, L.K, L.OC, L.Kpad, L.Npad, L.mode == MODE_PATCH16 ? patch16_pack_order() : 0, L.kh,
+          rc = launch_pack_weights(tmp, packed32, L.K, L.OC, L.Kpad, L.Npad, L.mode == MODE_PATCH16 ? patch16_pack_order() : L.mode == MODE_TILE16 ? 5 : 0, L.kh,
                                    L.kw, L.C, 0);
         if (!rc)
           rc = launch_f32_to_f16(packed32, reinterpret_cast<half_t*>(p->weights + L.w_off),
@@ -826,7 +848,7 @@ static int run_fp16(dnn_plan* p, int n, const float* d_in, float* d_out, hipStre
         }
         case MODE_PATCH: {
           DirectGeom g{n, L.H, L.W, L.OH, L.OW, L.PH, L.PW, L.pt, L.pl};
-          rc = launch_conv1_patch_f16(cur, wt, L.Kpad, dst, g, zero, epi, s);
+          rc = launch_conv1_patch_f16(cur, wt, L.Kpad, dst, g, zero, epi, s, L.out_padded ? 1 : 0);
           break;
         }
         case MODE_DIRECT_A:
@@ -835,6 +857,9 @@ static int run_fp16(dnn_plan* p, int n, const float* d_in, float* d_out, hipStre
           break;
         case MODE_PATCH16:
           rc = launch_conv_patch16(cur, wt, L.Kpad, dst, L.out_padded ? 1 : 0, Mc, L.OC, L.K, L.H, L.W, L.C, epi, s);
+          break;
+        case MODE_TILE16:
+          rc = launch_conv_tile16(cur, wt, L.Kpad, dst, L.out_padded ? 1 : 0, n, L.OC, L.K, L.H, L.W, L.C, epi, s);
           break;
         case MODE_IMPLICIT: {
           ImplicitConv ic{zero, L.H, L.W, L.C, L.OH, L.OW, L.PH, L.PW, L.kh, L.kw, L.sh, L.sw, L.pt, L.pl,

@@ -1333,6 +1333,65 @@ def test_fp16_patch_conv_vs_oracle(monkeypatch, case):
     assert np.array_equal(eng.run(x), y)
 
 
+TILE16_CASES = [
+    # B, H, W, C, od1, od2, tile16 layers: pool (2x2 s1) -> conv3x3 C->od1 + pool 2x2/s2 ->
+    # conv3x3 od1->od2 + pool 2x2/s2, on the fp16 tile kernel where the frame allows it
+    (4, 104, 104, 32, 64, 128, 2),   # conv2 -> conv3 shapes (8x52 then 4x52 tiles, zero-bordered hand-off)
+    (3, 52, 52, 64, 128, 256, 2),    # conv3 -> conv4 shapes (4x52 then 8x26 tiles, 2 column groups)
+    (2, 26, 26, 128, 256, 64, 1),    # conv4 shape (over patch16); its 13x13 pooled output feeds the implicit GEMM
+    (2, 20, 36, 32, 64, 64, 2),      # ragged frames: edge tiles past the frame
+    (2, 20, 18, 32, 64, 64, 1),      # ... then a 10x9 frame (odd: the implicit GEMM)
+]
+
+
+@pytest.mark.parametrize("case", TILE16_CASES)
+def test_fp16_tile_conv_pool_vs_oracle(monkeypatch, case):
+    """conv3x3_f16_tile_kernel (2-D tiles, 32-channel patches LDS-DMA'd as skewed 64-B rows,
+    64-column waves, 2x2/s2 pool fused, persistent workgroups streaming (tile, chunk) pairs):
+    whole chain within the fp16 layer tolerance of the fp32 oracle; batch rows independent of the
+    batch (row 0 alone == row 0 of the batch, bit for bit); one tile per workgroup and one
+    persistent workgroup per CU give the same bits as the default two."""
+    B, H, W, C, od1, od2, ntile = case
+    rng = np.random.default_rng(B + C + od1 + H)
+    x = rng.standard_normal((B, H, W, C)).astype(np.float32)
+    k1 = (rng.standard_normal((3, 3, C, od1)) * np.sqrt(2.0 / (9 * C))).astype(np.float32)
+    k2 = (rng.standard_normal((3, 3, od1, od2)) * np.sqrt(2.0 / (9 * od1))).astype(np.float32)
+    bn = lambda n: (rng.standard_normal(n).astype(np.float32) * 0.1, rng.uniform(0.5, 1.5, n).astype(np.float32),
+                    rng.uniform(0.5, 1.5, n).astype(np.float32))
+    b1, bn1 = rng.standard_normal(od1).astype(np.float32) * 0.1, bn(od1)
+    b2, bn2 = rng.standard_normal(od2).astype(np.float32) * 0.1, bn(od2)
+
+    def graph(shape):
+        g = dnn_hip.DnnGraphBuilder()
+        y = g.create_input(list(shape))
+        y = g.create_max_pool2d(y, [1, 2, 2, 1], [1, 1, 1, 1], "SAME")
+        for k, b, n in ((k1, b1, bn1), (k2, b2, bn2)):
+            y = g.create_conv2d(y, k, [1, 1, 1, 1], "SAME")
+            y = g.create_bias_add(y, b)
+            y = g.create_batch_norm(y, *n, 1e-5)
+            y = g.create_leaky_relu(y)
+            y = g.create_max_pool2d(y, [1, 2, 2, 1], [1, 2, 2, 1], "SAME")
+        g.set_out_node(y)
+        return g
+
+    monkeypatch.delenv("DNN_HIP_TILE16_WGS", raising=False)
+    eng = dnn_hip.DnnInferenceEngine(graph(x.shape), False, precision="fp16")
+    assert eng.plan().describe().count("mode=tile16") == ntile, eng.plan().describe()
+    y = eng.run(x)
+    ref = R.max_pool2d(x, [1, 2, 2, 1], [1, 1, 1, 1], "SAME")
+    for k, b, n in ((k1, b1, bn1), (k2, b2, bn2)):
+        ref = R.leaky_relu(R.batch_norm(R.bias_add(R.conv2d(ref, k), b), *n, 1e-5))
+        ref = R.max_pool2d(ref, [1, 2, 2, 1], [1, 2, 2, 1], "SAME")
+    err = R.normwise_err(y, ref)
+    print("fp16 tile", case, "err %.3g" % err)
+    assert err < 2 * FP16_LAYER_TOL
+    y0 = dnn_hip.DnnInferenceEngine(graph((1,) + x.shape[1:]), False, precision="fp16").run(x[:1])
+    assert np.array_equal(y0, y[:1])
+    for wgs in ("0", "1"):  # launch-time switch
+        monkeypatch.setenv("DNN_HIP_TILE16_WGS", wgs)
+        assert np.array_equal(eng.run(x), y), wgs
+
+
 X3_CASES = [
     # B, H, W, C, od1, od2: pool (2x2 s1) -> conv3x3 C->od1 -> conv3x3 od1->od2, both on the fp32
     # x3 conv (exact 3-way bf16 splits; split planes written by the pool and by the first conv)
