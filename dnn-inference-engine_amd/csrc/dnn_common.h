@@ -277,8 +277,10 @@ int patch16_pack_order();  // launch_pack_weights order of the patch kernel's MF
 // by launch_pack_weights order 5; out_padded: the pooled output zero-bordered too
 bool conv_tile16_supported(int C, int OC, int H, int W, int OH, int OW, int kh, int kw, int sh, int sw, int pt,
                            int pl);
+// pool: 1 = 2x2/s2 (2-D tiles), 2 = 2x2/s1 SAME (whole 13 x 13 frames, conv_img16_supported)
+bool conv_img16_supported(int C, int OC, int H, int W);
 int launch_conv_tile16(const half_t* in_padded, const half_t* Bt, int ldb, half_t* out, int out_padded, int n, int N,
-                       int K, int H, int W, int C, const EpiParams& epi, hipStream_t stream);
+                       int K, int H, int W, int C, const EpiParams& epi, hipStream_t stream, int pool);
 int launch_conv_patch16(const half_t* in_padded, const half_t* Bt, int ldb, half_t* out, int out_padded, long long M,
                         int N, int K, int H, int W, int C, const EpiParams& epi, hipStream_t stream);
 // conv0 direct kernel with an fp16 output (fp32 input frames)

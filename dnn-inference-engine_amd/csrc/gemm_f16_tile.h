@@ -36,15 +36,15 @@ namespace dnnhip {
 #endif
 #if T16DIAG
 // diagnostic builds (-DT16DIAG=1, tools/build_diag.sh): per-workgroup phase stamps of the last
-// launch per input width class (C 32 / 64 / other), wave 0: [0] realtime start, [1] memtime
+// launch per input width class (C 32 / 64 / 128 / other), wave 0: [0] realtime start, [1] memtime
 // start, [2] prologue done, per pair q < 8: [3 + 3q] MFMA end, [4 + 3q] barrier passed, [5 + 3q]
 // epilogue done; [27] memtime end, [28] realtime end, [29] HW_ID, [30] XCC_ID, [31] tiles
 constexpr int T16_DIAG_WGS = 1024;
-__device__ unsigned long long t16_diag_stamps[3 * T16_DIAG_WGS * 32];
+__device__ unsigned long long t16_diag_stamps[4 * T16_DIAG_WGS * 32];
 #define T16_STAMP(k, v)                                                                              \
   {                                                                                                  \
     if (threadIdx.x == 0 && blockIdx.x < T16_DIAG_WGS)                                               \
-      t16_diag_stamps[((g.C == 32 ? 0 : g.C == 64 ? 1 : 2) * T16_DIAG_WGS + blockIdx.x) * 32 + (k)] = (v); \
+      t16_diag_stamps[((g.C == 32 ? 0 : g.C == 64 ? 1 : g.C == 128 ? 2 : 3) * T16_DIAG_WGS + blockIdx.x) * 32 + (k)] = (v); \
   }
 #else
 #define T16_STAMP(k, v) {}
@@ -56,18 +56,23 @@ struct Tile16Geom {
   int out_padded;  // 1: pooled output into a zero-bordered [B][PH+2][PW+2][N] buffer
 };
 
-template <int TH, int TW, int WM, int WN, int TM, int FL = -1>
+// MODE 0: 2-D tiles, pool-window-major rows, 2x2/s2 pool (above).  MODE 1 (conv5 + pool5): the
+// whole TH x TW frame per tile in raster rows, the epilogue's fp16 values staged for the whole
+// frame and the 2x2/s1 SAME pool taken from the stage (pool of the rounded values == rounding of
+// the pooled value: rounding is monotone); PU-unit pixel rows (13 x 13 frames: 96-B rows skewed by
+// 4 units per image row, 1.45 extra conflict cycles per fragment read; 64-B rows 4.7).
+template <int TH, int TW, int WM, int WN, int TM, int FL = -1, int MODE = 0, int PU = 4, int SK = 2, int BR = 3>
 __global__ void __launch_bounds__(64 * WM * WN, 2)
 conv3x3_f16_tile_kernel(const half_t* __restrict__ in, const half_t* __restrict__ Bt, int ldb, half_t* __restrict__ out,
                         int N, EpiParams epi, int tilesX, int tilesY, int tilesN, int nspatial, Tile16Geom g,
                         unsigned in_bytes, unsigned b_bytes) {
-  constexpr int NW = WM * WN, PU = 4, SK = 2, PW2 = TW + 2, RU = PU * PW2 + SK, T = TH * TW, NJ = 4;
+  constexpr int NW = WM * WN, PW2 = TW + 2, RU = PU * PW2 + SK, T = TH * TW, NJ = 4;
   constexpr int NU = (TH + 2) * RU, NP = (NU + 63) / 64, NPW = (NP + NW - 1) / NW;  // units / pieces per chunk
   constexpr int BUFB = NP * 1024;
   constexpr int SROW = 72;  // stage row pitch (halves): 64 columns + 8 (144-B rows)
   constexpr int STGB = TM * 4 * SROW * 2;  // per wave
-  static_assert(TH % 2 == 0 && TW % 2 == 0 && WM * TM * 16 >= T && (WM - 1) * TM * 16 < T && NPW <= 16 &&
-                    NW * STGB <= BUFB,
+  static_assert(WM * TM * 16 >= T && (WM - 1) * TM * 16 < T && NPW <= 16 && PU >= 4 && (MODE == 0 || MODE == 1) &&
+                    (MODE == 0 ? TH % 2 == 0 && TW % 2 == 0 && NW * STGB <= BUFB : T * 64 * WN * 2 <= BUFB),
                 "shape");
   __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * BUFB + WN * 64 * 16];
   f32x4* const epl = reinterpret_cast<f32x4*>(smem + 2 * BUFB);
@@ -104,8 +109,15 @@ conv3x3_f16_tile_kernel(const half_t* __restrict__ in, const half_t* __restrict_
   for (int i = 0; i < TM; ++i) {
     int r = (wm * TM + i) * 16 + fr;
     r = r < T ? r : T - 1;
-    const int w = r >> 2, q = r & 3;
-    const int ly = 2 * (w / (TW / 2)) + (q >> 1), lx = 2 * (w % (TW / 2)) + (q & 1);
+    int ly, lx;
+    if constexpr (MODE == 0) {
+      const int w = r >> 2, q = r & 3;
+      ly = 2 * (w / (TW / 2)) + (q >> 1);
+      lx = 2 * (w % (TW / 2)) + (q & 1);
+    } else {
+      ly = r / TW;
+      lx = r % TW;
+    }
     rowoff[i] = (RU * ly + PU * lx) * 16 + 16 * fq;
   }
   auto rowoff_of = [&](int i) {
@@ -150,7 +162,11 @@ conv3x3_f16_tile_kernel(const half_t* __restrict__ in, const half_t* __restrict_
   const unsigned bvo = (unsigned)((n0 / 16) * ldb * 32 + lane * 16);
   const int bjs = ldb * 32;
   const auto rsB = __builtin_amdgcn_make_buffer_rsrc((void*)Bt, 0, (int)b_bytes, 0x00020000);
-  f16x8 bq[3][NJ];
+  // weight ring of BR K-steps, loads BR - 1 steps ahead (9 % BR == 0: the same slots every pair).
+  // A vector-memory load waits for every older one, the next pair's patch DMA included: the
+  // DMA has BR - 1 steps to land before the loop stalls on a weight issued after it.
+  static_assert(9 % BR == 0 && BR >= 3, "weight ring");
+  f16x8 bq[BR][NJ];
   auto load_b = [&](int s, f16x8 (&dst)[NJ]) {
 #pragma unroll
     for (int j = 0; j < NJ; ++j)
@@ -166,8 +182,8 @@ conv3x3_f16_tile_kernel(const half_t* __restrict__ in, const half_t* __restrict_
 
   const int eflags = FL < 0 ? epi.flags : FL;
   issue(0, 0);
-  load_b(0, bq[0]);
-  load_b(1 % S, bq[1]);
+#pragma unroll
+  for (int l = 0; l < BR - 1; ++l) load_b(l, bq[l]);
   if (threadIdx.x < 64 * WN) {  // the workgroup's epilogue parameters
     const int n = tn * (64 * WN) + threadIdx.x;
     epl[threadIdx.x] = f32x4{(eflags & EPI_BIAS) ? epi.bias[n] : 0.f,
@@ -198,8 +214,9 @@ conv3x3_f16_tile_kernel(const half_t* __restrict__ in, const half_t* __restrict_
       const int s = 9 * c + tp;
       __builtin_amdgcn_sched_barrier(0);
       {
-        const int s2 = s + 2 < S ? s + 2 : s + 2 - S;  // (the next tile's first steps)
-        load_b(s2, bq[(tp + 2) % 3]);
+        int s2 = s + BR - 1;  // (past the tile's last step: the next tile's first steps; BR - 1 < 9 <= S)
+        s2 = s2 < S ? s2 : s2 - S;
+        load_b(s2, bq[(tp + BR - 1) % BR]);
       }
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
@@ -207,17 +224,58 @@ conv3x3_f16_tile_kernel(const half_t* __restrict__ in, const half_t* __restrict_
         const f16x8 a = af[bi % RING];
         if (bi + LEAD < 9 * TM) af[(bi + LEAD) % RING] = *reinterpret_cast<const f16x8*>(blk(P, bi + LEAD));
 #pragma unroll
-        for (int jb = 0; jb < NJ; ++jb) acc[i][jb] = mfma16_f16(a, bq[tp % 3][jb], acc[i][jb]);
+        for (int jb = 0; jb < NJ; ++jb) acc[i][jb] = mfma16_f16(a, bq[tp % BR][jb], acc[i][jb]);
         __builtin_amdgcn_sched_barrier(0);
       }
     }
-    // the ring holds steps s + 1, s + 2 in slots 0, 1 for the next pair (9 % 3 == 0)
+    // the ring holds the next pair's first BR - 1 steps in slots 0 .. BR - 2 (9 % BR == 0)
     if (q < 8) T16_STAMP(3 + 3 * q, __builtin_amdgcn_s_memtime())
     vm_wait<0>();  // this wave's DMA pieces of pair q + 1 landed
     wait_lgkm0();
     __syncthreads();  // every wave's pieces landed; pair q's buffer read by every wave
     if (q < 8) T16_STAMP(4 + 3 * q, __builtin_amdgcn_s_memtime())
-    if (c == nch - 1) {
+    if (MODE == 1 && c == nch - 1) {
+      // epilogue of frame q / nch: fp16 values of every pixel x the workgroup's 64 WN columns
+      // into the just-read buffer, then the 2x2/s1 SAME pool from it, 8 columns per thread
+      int b, y0, x0;
+      tile_xyb(q / nch, b, y0, x0);
+      half_t* const st = reinterpret_cast<half_t*>(smem + (q & 1) * BUFB);
+      constexpr int SW = 64 * WN;
+#pragma unroll
+      for (int jb = 0; jb < NJ; ++jb) {
+        const f32x4 e = epl[wn * 64 + 16 * jb + fr];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = (wm * TM + i) * 16 + 4 * fq + r;
+            if (row < T)
+              st[row * SW + wn * 64 + 16 * jb + fr] =
+                  (half_t)apply_epilogue_t<FL>(acc[i][jb][r], e[0], e[1], e[2], e[3], epi.flags);
+          }
+          acc[i][jb] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+      }
+      wait_lgkm0();
+      __syncthreads();
+      const int ncol0 = tn * (64 * WN);
+      for (int idx = threadIdx.x; idx < T * (SW / 8); idx += 64 * NW) {
+        const int p = idx / (SW / 8), gq = idx - p * (SW / 8);
+        const int y = p / TW, x = p - y * TW;
+        const h8v* sp = reinterpret_cast<const h8v*>(st + p * SW + 8 * gq);
+        h8v v = sp[0];
+        if (x + 1 < TW) v = __builtin_elementwise_max(v, sp[SW / 8]);
+        if (y + 1 < TH) {
+          v = __builtin_elementwise_max(v, sp[TW * (SW / 8)]);
+          if (x + 1 < TW) v = __builtin_elementwise_max(v, sp[(TW + 1) * (SW / 8)]);
+        }
+        const size_t o = g.out_padded ? (size_t)(b * (TH + 2) + y + 1) * (TW + 2) + x + 1 : (size_t)(b * TH + y) * TW + x;
+        *reinterpret_cast<h8v*>(out + o * N + ncol0 + 8 * gq) = v;
+      }
+      wait_lgkm0();
+      __syncthreads();  // the stage read before pair q + 2's DMA reuses the buffer
+    }
+    if (MODE == 0 && c == nch - 1) {
       // epilogue of tile q / nch through the just-read buffer: window (block i, fq) of column
       // 16 jb + fr -> the wave's stage row 4 i + fq, then 16-B stores of 8 halves
       int b, y0, x0;

@@ -402,10 +402,57 @@ static int tile16_wgs_per_cu() {
   return e ? atoi(e) : 2;
 }
 
+#ifndef IMG16_BR
+#define IMG16_BR 3
+#endif
+// whole-frame form (MODE 1) with the 2x2/s1 SAME pool fused: 13 x 13 frames (conv5 + pool5)
+bool conv_img16_supported(int C, int OC, int H, int W) {
+  const char* e = getenv("DNN_HIP_IMG16");
+  return H == 13 && W == 13 && C % 32 == 0 && OC % 64 == 0 && tile16_enabled() && !(e && e[0] == '0') &&
+         (long long)OC * 9 * C * 2 < 0x80000000LL;
+}
+
+static int launch_img16(const half_t* in_padded, const half_t* Bt, int ldb, half_t* out, int out_padded, int n, int N,
+                        int K, int H, int W, int C, const EpiParams& epi, hipStream_t stream) {
+  if (!conv_img16_supported(C, N, H, W) || K != 9 * C || ldb < K || ldb % 32 != 0) {
+    set_error("conv_img16: unsupported shape N=%d K=%d %dx%dx%d ldb=%d", N, K, H, W, C, ldb);
+    return -2;
+  }
+  const int tilesN = N / 64;
+  const Tile16Geom g{H, W, C, H, W, out_padded};
+  const long long img_in = (long long)(H + 2) * (W + 2) * C * 2;
+  const long long img_out = (long long)(H + 2 * out_padded) * (W + 2 * out_padded) * N;  // halves
+  const unsigned b_bytes = (unsigned)((long long)N * ldb * 2);
+  constexpr int F16YOLO = EPI_BN_AB | EPI_LEAKY_F32;
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  const int wpc = tile16_wgs_per_cu();
+  const int per = (int)std::min<long long>(n, 0x7fffffffLL / img_in);
+  for (int f0 = 0; f0 < n; f0 += per) {
+    const int nf = std::min(per, n - f0);
+    const int G = wpc > 0 ? std::max(1, std::min(nf, wpc * cus / tilesN)) : nf;
+    const dim3 grid((unsigned)(G * tilesN));
+    const half_t* in = in_padded + (size_t)f0 * (img_in / 2);
+    half_t* o = out + (size_t)f0 * img_out;
+    const unsigned ib = (unsigned)(nf * img_in);
+    if (epi.flags == F16YOLO)
+      hipLaunchKernelGGL((conv3x3_f16_tile_kernel<13, 13, 4, 1, 3, F16YOLO, 1, 6, 4, IMG16_BR>), grid, dim3(256), 0, stream, in,
+                         Bt, ldb, o, N, epi, 1, 1, tilesN, nf, g, ib, b_bytes);
+    else
+      hipLaunchKernelGGL((conv3x3_f16_tile_kernel<13, 13, 4, 1, 3, -1, 1, 6, 4, IMG16_BR>), grid, dim3(256), 0, stream, in, Bt,
+                         ldb, o, N, epi, 1, 1, tilesN, nf, g, ib, b_bytes);
+    const int rc = check16("conv_img16");
+    if (rc) return rc;
+  }
+  return 0;
+}
+
 int launch_conv_tile16(const half_t* in_padded, const half_t* Bt, int ldb, half_t* out, int out_padded, int n, int N,
-                       int K, int H, int W, int C, const EpiParams& epi, hipStream_t stream) {
+                       int K, int H, int W, int C, const EpiParams& epi, hipStream_t stream, int pool) {
   if (n == 0 || N == 0) return 0;
-  if (!conv_tile16_supported(C, N, H, W, H, W, 3, 3, 1, 1, 1, 1) || K != 9 * C || ldb < K || ldb % 32 != 0) {
+  if (pool == 2) return launch_img16(in_padded, Bt, ldb, out, out_padded, n, N, K, H, W, C, epi, stream);
+  if (pool != 1 || !conv_tile16_supported(C, N, H, W, H, W, 3, 3, 1, 1, 1, 1) || K != 9 * C || ldb < K ||
+      ldb % 32 != 0) {
     set_error("conv_tile16: unsupported shape N=%d K=%d %dx%dx%d ldb=%d", N, K, H, W, C, ldb);
     return -2;
   }
@@ -451,9 +498,9 @@ int launch_conv_tile16(const half_t* in_padded, const half_t* Bt, int ldb, half_
 
 #if T16DIAG
 // diagnostic builds: conv3x3_f16_tile_kernel's phase stamps (gemm_f16_tile.h), class k (0: C 32,
-// 1: C 64, 2: other) of the last launch, n workgroups x 32 slots
+// 1: C 64, 2: C 128, 3: other) of the last launch, n workgroups x 32 slots
 extern "C" __attribute__((visibility("default"))) int dnn_t16_diag_stamps(unsigned long long* host, int k, int n) {
-  if (k < 0 || k > 2 || n < 0 || n > dnnhip::T16_DIAG_WGS) return -2;
+  if (k < 0 || k > 3 || n < 0 || n > dnnhip::T16_DIAG_WGS) return -2;
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(dnnhip::t16_diag_stamps), (size_t)n * 32 * sizeof(unsigned long long),
                              (size_t)k * dnnhip::T16_DIAG_WGS * 32 * sizeof(unsigned long long),
                              hipMemcpyDeviceToHost) == hipSuccess

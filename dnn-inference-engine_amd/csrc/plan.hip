@@ -458,7 +458,7 @@ int dnn_plan_add_conv(dnn_plan* p, int kh, int kw, int od, int stride_h, int str
     if (L.mode == MODE_IMPLICIT && !p->layers.empty() &&
         conv_patch16_supported(L.C, od, L.H, L.W, L.OH, L.OW, kh, kw, stride_h, stride_w, L.pt, L.pl)) {
       PlanLayer& prev = p->layers.back();
-      if (prev.type == 1 || (prev.mode == MODE_PATCH16 && !prev.pool)) {
+      if (prev.type == 1 || (prev.mode == MODE_PATCH16 && !prev.pool) || prev.mode == MODE_TILE16) {
         L.mode = MODE_PATCH16;
         prev.out_padded = true;
       }
@@ -661,6 +661,23 @@ int dnn_plan_add_max_pool(dnn_plan* p, int kh, int kw, int stride_h, int stride_
       prev.pool1 = true;
       return 0;
     }
+    // ... into an fp16 conv of a 13 x 13 frame fed by a zero-bordered producer (conv5 + pool5 of
+    // the fp16 path): the tile kernel's whole-frame form, pool taken from its fp16 stage
+    if (p->fp16 && prev.type == 0 && (prev.mode == MODE_IMPLICIT || prev.mode == MODE_PATCH16) && !prev.pool &&
+        !prev.pool1 && p->layers.size() >= 2 &&
+        prev.kh == 3 && prev.kw == 3 && prev.sh == 1 && prev.sw == 1 && prev.pt == 1 && prev.pl == 1 &&
+        prev.OH == prev.H && prev.OW == prev.W && prev.Kpad % 32 == 0 &&
+        conv_img16_supported(prev.C, prev.OC, prev.H, prev.W)) {
+      PlanLayer& q = p->layers[p->layers.size() - 2];
+      if (q.type == 1 || (q.type == 0 && (q.mode == MODE_PATCH16 || q.mode == MODE_TILE16 ||
+                                          (q.mode == MODE_PATCH && q.pool)))) {
+        prev.mode = MODE_TILE16;
+        prev.pool1 = true;
+        prev.splits = 1;
+        q.out_padded = true;
+        return 0;
+      }
+    }
     // ... into a batch-tile x3 conv of a small frame (conv5 + pool5): whole-image tiles over all
     // of K (gemm_x3_img.h) instead of K slices whose partials the pool combines
     if (prev.type == 0 && prev.mode == MODE_X3 && !prev.x3k && !prev.x3lat && !prev.pool && !prev.pool1 &&
@@ -715,7 +732,7 @@ static int upload_weights(dnn_plan* p) {
       if (hipMemcpy(tmp, L.w.data(), wb, hipMemcpyHostToDevice) != hipSuccess) rc = -1;
       if (p->fp16) {
         if (!rc)
-          rc = launch_pack_weights(tmp, packed32, L.K, L.OC, L.Kpad, L.Npad, L.mode == MODE_PATCH16 ? patch16_pack_order() : L.mode == MODE_TILE16 ? 5 : 0, L.kh,
+          rc = launch_pack_weights(tmp, packed32, L.K, L.OC, L.Kpad, L.Npad, L.mode == MODE_TILE16 ? 5 : L.mode == MODE_PATCH16 ? patch16_pack_order() : 0, L.kh,
                                    L.kw, L.C, 0);
         if (!rc)
           rc = launch_f32_to_f16(packed32, reinterpret_cast<half_t*>(p->weights + L.w_off),
@@ -859,7 +876,8 @@ static int run_fp16(dnn_plan* p, int n, const float* d_in, float* d_out, hipStre
           rc = launch_conv_patch16(cur, wt, L.Kpad, dst, L.out_padded ? 1 : 0, Mc, L.OC, L.K, L.H, L.W, L.C, epi, s);
           break;
         case MODE_TILE16:
-          rc = launch_conv_tile16(cur, wt, L.Kpad, dst, L.out_padded ? 1 : 0, n, L.OC, L.K, L.H, L.W, L.C, epi, s);
+          rc = launch_conv_tile16(cur, wt, L.Kpad, dst, L.out_padded ? 1 : 0, n, L.OC, L.K, L.H, L.W, L.C, epi, s,
+                                  L.pool1 ? 2 : 1);
           break;
         case MODE_IMPLICIT: {
           ImplicitConv ic{zero, L.H, L.W, L.C, L.OH, L.OW, L.PH, L.PW, L.kh, L.kw, L.sh, L.sw, L.pt, L.pl,

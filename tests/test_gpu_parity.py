@@ -1392,6 +1392,66 @@ def test_fp16_tile_conv_pool_vs_oracle(monkeypatch, case):
         assert np.array_equal(eng.run(x), y), wgs
 
 
+IMG16_CASES = [
+    # B, C, od1, od2: 13x13 frames: pool (2x2 s1) -> conv3x3 C->od1 + pool 2x2/s1 SAME (the tile
+    # kernel's whole-frame form) -> conv3x3 od1->od2 (patch16: the zero-bordered hand-off)
+    (64, 256, 512, 256),   # conv5 + pool5 -> conv6 shapes at batch 64 (8 column groups)
+    (3, 64, 192, 256),     # 3 column groups, few frames
+    (1, 32, 64, 64),       # one frame; od2 = 64: the implicit GEMM reads a plain output
+]
+
+
+@pytest.mark.parametrize("case", IMG16_CASES)
+def test_fp16_img_conv_pool1_vs_oracle(monkeypatch, case):
+    """conv3x3_f16_tile_kernel MODE 1 (whole 13x13 frame per tile, raster rows in skewed 96-B
+    LDS rows, epilogue staged in fp16 for the frame, the 2x2/s1 SAME pool taken from the stage):
+    chain within the fp16 tolerance of the fp32 oracle; batch rows independent of the batch;
+    the same bits with one frame per workgroup (DNN_HIP_TILE16_WGS=0)."""
+    B, C, od1, od2 = case
+    H = W = 13
+    rng = np.random.default_rng(B + C + od1)
+    x = rng.standard_normal((B, H, W, C)).astype(np.float32)
+    k1 = (rng.standard_normal((3, 3, C, od1)) * np.sqrt(2.0 / (9 * C))).astype(np.float32)
+    k2 = (rng.standard_normal((3, 3, od1, od2)) * np.sqrt(2.0 / (9 * od1))).astype(np.float32)
+    bn = lambda n: (rng.standard_normal(n).astype(np.float32) * 0.1, rng.uniform(0.5, 1.5, n).astype(np.float32),
+                    rng.uniform(0.5, 1.5, n).astype(np.float32))
+    b1, bn1 = rng.standard_normal(od1).astype(np.float32) * 0.1, bn(od1)
+    b2, bn2 = rng.standard_normal(od2).astype(np.float32) * 0.1, bn(od2)
+
+    def graph(shape):
+        g = dnn_hip.DnnGraphBuilder()
+        y = g.create_input(list(shape))
+        y = g.create_max_pool2d(y, [1, 2, 2, 1], [1, 1, 1, 1], "SAME")
+        for i, (k, b, n) in enumerate(((k1, b1, bn1), (k2, b2, bn2))):
+            y = g.create_conv2d(y, k, [1, 1, 1, 1], "SAME")
+            y = g.create_bias_add(y, b)
+            y = g.create_batch_norm(y, *n, 1e-5)
+            y = g.create_leaky_relu(y)
+            if i == 0:
+                y = g.create_max_pool2d(y, [1, 2, 2, 1], [1, 1, 1, 1], "SAME")
+        g.set_out_node(y)
+        return g
+
+    monkeypatch.delenv("DNN_HIP_TILE16_WGS", raising=False)
+    eng = dnn_hip.DnnInferenceEngine(graph(x.shape), False, precision="fp16")
+    d = eng.plan().describe()
+    assert d.count("mode=tile16") == 1 and "+pool2x2s1" in d, d
+    assert ("mode=patch16" in d) == (od2 % 256 == 0), d
+    y = eng.run(x)
+    ref = R.max_pool2d(x, [1, 2, 2, 1], [1, 1, 1, 1], "SAME")
+    for i, (k, b, n) in enumerate(((k1, b1, bn1), (k2, b2, bn2))):
+        ref = R.leaky_relu(R.batch_norm(R.bias_add(R.conv2d(ref, k), b), *n, 1e-5))
+        if i == 0:
+            ref = R.max_pool2d(ref, [1, 2, 2, 1], [1, 1, 1, 1], "SAME")
+    err = R.normwise_err(y, ref)
+    print("fp16 img", case, "err %.3g" % err)
+    assert err < 2 * FP16_LAYER_TOL
+    y0 = dnn_hip.DnnInferenceEngine(graph((1,) + x.shape[1:]), False, precision="fp16").run(x[:1])
+    assert np.array_equal(y0, y[:1])
+    monkeypatch.setenv("DNN_HIP_TILE16_WGS", "0")
+    assert np.array_equal(eng.run(x), y)
+
+
 X3_CASES = [
     # B, H, W, C, od1, od2: pool (2x2 s1) -> conv3x3 C->od1 -> conv3x3 od1->od2, both on the fp32
     # x3 conv (exact 3-way bf16 splits; split planes written by the pool and by the first conv)

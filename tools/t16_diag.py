@@ -60,14 +60,14 @@ def main():
     f = plan.lib.dnn_t16_diag_stamps
     f.restype = ctypes.c_int
     f.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
-    for k, name in enumerate(("conv2 (C 32)", "conv3 (C 64)", "conv4 (C 128)")):
+    for k, name in enumerate(("conv2 (C 32)", "conv3 (C 64)", "conv4 (C 128)", "conv5 + pool5 (C 256)")):
         buf = (ctypes.c_ulonglong * (WGS * 32))()
         assert f(buf, k, WGS) == 0
         rows = [list(buf[32 * w:32 * w + 32]) for w in range(WGS) if buf[32 * w + 27] > 0]
         if not rows:
             print(name, ": no stamps")
             continue
-        nch = {0: 1, 1: 2, 2: 4}[k]
+        nch = {0: 1, 1: 2, 2: 4, 3: 8}[k]
         print("%s: %d workgroups, tiles/workgroup %s" % (name, len(rows), sorted(set(r[31] for r in rows))))
         print("  prologue              ", med([r[2] - r[1] for r in rows]))
         for q in range(8):
