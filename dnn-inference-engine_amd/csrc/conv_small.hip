@@ -17,6 +17,7 @@
 //   of v_mfma_f32_16x16x32_f16 covers two taps (lane part p: tap 2s + p/2, channels
 //   8(p&1)..+7), tap 9 being zero.
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <cfloat>
 #include <type_traits>
 #include "dnn_common.h"
@@ -461,36 +462,35 @@ int launch_conv0_mfma_f16(const float* in, const float* w, half_t* out, const Di
 // in: fp16 NHWC [B][H][W][16]; Bt: packed fp16 weights [32][ldb] (k = tap*16 + c, ldb >= 144);
 // out: fp16 pooled [B][PH][PW][32] (opad: the interior of a zero-bordered [B][PH+2][PW+2][32]
 // buffer, the tile kernel's input).  SAME 3x3 stride 1, even OH/OW.
+// Round 5: persistent workgroups (conv1 is memory-bound: 16 x 16 tiles of 40 MFMAs per wave, so
+// a one-tile workgroup spent most of its life waiting for its patch and loading its weights):
+// weights loaded once per workgroup, tile t + 1's patch DMA'd into the other buffer while tile t
+// computes.  Same products, same order: same bits as the one-tile form (DNN_HIP_C1F16_WGS=0).
 __global__ void __launch_bounds__(256)
 conv1_patch_f16_kernel(const half_t* __restrict__ in, const half_t* __restrict__ Bt, int ldb,
                        half_t* __restrict__ out, DirectGeom g, int tilesX, int tilesY, const float* __restrict__ zero,
-                       EpiParams epi, int opad) {
+                       EpiParams epi, int opad, int ntiles) {
   constexpr int C = 16;
   constexpr int PATCH = SC_P * SC_P * C;      // halves
   constexpr int PATCH_CH = (PATCH * 2 + 1023) / 1024;  // 1-KiB DMA chunks
-  __shared__ __attribute__((aligned(1024))) float smem[PATCH_CH * 256];
-  const half_t* P = reinterpret_cast<const half_t*>(smem);
+  __shared__ __attribute__((aligned(1024))) float smem[2 * PATCH_CH * 256];
 
-  int t = xcd_tile(blockIdx.x, gridDim.x);
-  const int tx = t % tilesX;
-  t /= tilesX;
-  const int ty = t % tilesY;
-  const int b = t / tilesY;
-  const int y0 = ty * SC_T, x0 = tx * SC_T;
   const int lane = threadIdx.x & 63;
   const int wid = wave_uniform(threadIdx.x >> 6);
-
-  // patch: 16-B chunks = 8 channels; pixel pp = chunk / 2
-  const half_t* inb = in + (size_t)b * g.H * g.W * C;
-  for (int c = wid; c < PATCH_CH; c += 4) {
-    const int q = c * 64 + lane;  // 16-B chunk index
-    const int pp = q >> 1, half8 = (q & 1) * 8;
-    const int py = pp / SC_P, px = pp - py * SC_P;
-    const int iy = y0 - 1 + py, ix = x0 - 1 + px;
-    const bool ok = pp < SC_P * SC_P && (unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W;
-    lds_dma16(ok ? reinterpret_cast<const float*>(inb + ((size_t)iy * g.W + ix) * C + half8) : zero,
-              smem + c * 256);
-  }
+  auto issue = [&](int t, int buf) {  // tile t's patch: 16-B chunks = 8 channels; pixel pp = chunk / 2
+    const int tx = t % tilesX, ty = (t / tilesX) % tilesY, b = t / (tilesX * tilesY);
+    const int y0 = ty * SC_T, x0 = tx * SC_T;
+    const half_t* inb = in + (size_t)b * g.H * g.W * C;
+    for (int c = wid; c < PATCH_CH; c += 4) {
+      const int q = c * 64 + lane;  // 16-B chunk index
+      const int pp = q >> 1, half8 = (q & 1) * 8;
+      const int py = pp / SC_P, px = pp - py * SC_P;
+      const int iy = y0 - 1 + py, ix = x0 - 1 + px;
+      const bool ok = pp < SC_P * SC_P && (unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W;
+      lds_dma16(ok ? reinterpret_cast<const float*>(inb + ((size_t)iy * g.W + ix) * C + half8) : zero,
+                smem + buf * (PATCH_CH * 256) + c * 256);
+    }
+  };
 
   // B fragments in registers: K-step s (0..4) covers taps 2s, 2s+1; lane part p -> tap 2s + p/2,
   // channels 8(p&1)..+7; N-tile j -> output channel 16j + (lane&15)
@@ -507,44 +507,59 @@ conv1_patch_f16_kernel(const half_t* __restrict__ in, const half_t* __restrict__
         bw[s][j] = h8_t{0, 0, 0, 0, 0, 0, 0, 0};
     }
   }
-  wait_vmcnt<0>();
-  raw_barrier();
-
-  f32x4 acc[4][2];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int wi = fr >> 2, pos = fr & 3;
-    const int y = 4 * wid + 2 * (i >> 1) + (pos >> 1);
-    const int x = 2 * (4 * (i & 1) + wi) + (pos & 1);
-    const int base = (y * SC_P + x) * C + 8 * (fp & 1);
-#pragma unroll
-    for (int s = 0; s < 5; ++s) {
-      const int tap = 2 * s + (fp >> 1);
-      h8_t a = h8_t{0, 0, 0, 0, 0, 0, 0, 0};
-      if (tap < 9) a = *reinterpret_cast<const h8_t*>(P + base + ((tap / 3) * SC_P + tap % 3) * C);
-#pragma unroll
-      for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, bw[s][j], acc[i][j], 0, 0, 0);
-    }
-  }
-
+  float pb[2], pm[2], ps[2], pg[2];
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int n = 16 * j + fr;
-    const float pb = (epi.flags & EPI_BIAS) ? epi.bias[n] : 0.f;
-    const float pm = (epi.flags & (EPI_BN | EPI_BN_AB)) ? epi.mean[n] : 0.f;
-    const float ps = (epi.flags & (EPI_BN | EPI_BN_AB)) ? epi.sq[n] : 1.f;
-    const float pg = (epi.flags & EPI_BN) ? epi.gamma[n] : 1.f;
+    pb[j] = (epi.flags & EPI_BIAS) ? epi.bias[n] : 0.f;
+    pm[j] = (epi.flags & (EPI_BN | EPI_BN_AB)) ? epi.mean[n] : 0.f;
+    ps[j] = (epi.flags & (EPI_BN | EPI_BN_AB)) ? epi.sq[n] : 1.f;
+    pg[j] = (epi.flags & EPI_BN) ? epi.gamma[n] : 1.f;
+  }
+
+  int t = blockIdx.x;
+  if (t < ntiles) issue(t, 0);
+  for (int k = 0; t < ntiles; ++k, t += gridDim.x) {
+    wait_vmcnt<0>();  // this wave's pieces of tile t (and its previous tile's stores)
+    raw_barrier();    // every wave's pieces landed; the other buffer's tile read by every wave
+    if (t + (int)gridDim.x < ntiles) issue(t + gridDim.x, (k + 1) & 1);
+    const half_t* P = reinterpret_cast<const half_t*>(smem + (k & 1) * (PATCH_CH * 256));
+    const int tx = t % tilesX, ty = (t / tilesX) % tilesY, b = t / (tilesX * tilesY);
+    const int y0 = ty * SC_T, x0 = tx * SC_T;
+
+    f32x4 acc[4][2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int wy = (y0 >> 1) + 2 * wid + (i >> 1), wx = (x0 >> 1) + 4 * (i & 1) + fp;
-      if (wy < g.PH && wx < g.PW)
-        store_out(out + (((size_t)b * (g.PH + 2 * opad) + wy + opad) * (g.PW + 2 * opad) + wx + opad) * 32 + n,
-                  pool_then_epilogue(acc[i][j], pb, pm, ps, pg, epi.flags));
+      const int wi = fr >> 2, pos = fr & 3;
+      const int y = 4 * wid + 2 * (i >> 1) + (pos >> 1);
+      const int x = 2 * (4 * (i & 1) + wi) + (pos & 1);
+      const int base = (y * SC_P + x) * C + 8 * (fp & 1);
+#pragma unroll
+      for (int s = 0; s < 5; ++s) {
+        const int tap = 2 * s + (fp >> 1);
+        h8_t a = h8_t{0, 0, 0, 0, 0, 0, 0, 0};
+        if (tap < 9) a = *reinterpret_cast<const h8_t*>(P + base + ((tap / 3) * SC_P + tap % 3) * C);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, bw[s][j], acc[i][j], 0, 0, 0);
+      }
     }
+
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int n = 16 * j + fr;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int wy = (y0 >> 1) + 2 * wid + (i >> 1), wx = (x0 >> 1) + 4 * (i & 1) + fp;
+        if (wy < g.PH && wx < g.PW)
+          store_out(out + (((size_t)b * (g.PH + 2 * opad) + wy + opad) * (g.PW + 2 * opad) + wx + opad) * 32 + n,
+                    pool_then_epilogue(acc[i][j], pb[j], pm[j], ps[j], pg[j], epi.flags));
+      }
+    }
+    wait_lgkm0();  // (this tile's patch reads done before the barrier that frees its buffer)
   }
 }
 
@@ -563,9 +578,20 @@ int launch_conv1_patch_f16(const half_t* in, const half_t* Bt, int ldb, half_t* 
     return -2;
   }
   const int tilesX = (g.OW + SC_T - 1) / SC_T, tilesY = (g.OH + SC_T - 1) / SC_T;
-  const long long blocks = (long long)g.B * tilesX * tilesY;
+  const long long tiles = (long long)g.B * tilesX * tilesY;
+  if (tiles > 0x7fffffffLL) {
+    set_error("conv1_patch_f16: too many tiles");
+    return -2;
+  }
+  // persistent workgroups per CU (DNN_HIP_C1F16_WGS; 0: one tile per workgroup)
+  const char* ev = getenv("DNN_HIP_C1F16_WGS");
+  const int wpc = ev ? atoi(ev) : 8;  // (batch 64: one-tile 73.9 us, 4 per CU 59.9, 8 per CU 56.0)
+  int dev = 0, cus = 256;
+  if (wpc > 0 && hipGetDevice(&dev) == hipSuccess)
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  const long long blocks = wpc > 0 ? std::min<long long>(tiles, (long long)wpc * cus) : tiles;
   hipLaunchKernelGGL(conv1_patch_f16_kernel, dim3((unsigned)blocks), dim3(256), 0, s, in, Bt, ldb, out, g, tilesX,
-                     tilesY, zero, epi, opad);
+                     tilesY, zero, epi, opad, (int)tiles);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
     set_error("launch conv1_patch_f16: %s", hipGetErrorString(e));
