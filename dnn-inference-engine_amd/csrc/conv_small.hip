@@ -378,7 +378,9 @@ static int launch_conv0(const float* in, const float* w, OutT* out, const Direct
   // persistent: 8 workgroups per CU loop over the tiles (weights loaded once per workgroup,
   // the next tile's patch prefetched into registers during the current tile's MFMAs)
   const int nt = (int)blocks;
-  const dim3 grid((unsigned)(nt < 2048 ? nt : 2048));
+  const char* eg = getenv("DNN_HIP_C0_GRID");  // (tuning experiments: workgroups of the launch)
+  const int gmax = eg && atoi(eg) > 0 ? atoi(eg) : 4096;  // (fp16 conv0 at batch 64: 2048 89.4 us, 4096 85.1, 8192 87.2)
+  const dim3 grid((unsigned)(nt < gmax ? nt : gmax));
   switch (cin) {
     case 1: hipLaunchKernelGGL((conv0_mfma_pool_kernel<1, F16, OutT>), grid, dim3(256), 0, s, in, w, out, g, tilesX, tilesY, nt, epi); break;
     case 2: hipLaunchKernelGGL((conv0_mfma_pool_kernel<2, F16, OutT>), grid, dim3(256), 0, s, in, w, out, g, tilesX, tilesY, nt, epi); break;
