@@ -461,6 +461,9 @@ int launch_conv0_mfma_f16(const float* in, const float* w, half_t* out, const Di
 }
 
 // ------------------------------------------------------------------------------ conv1 fp16
+#ifndef C1F16_STAGE
+#define C1F16_STAGE 1
+#endif
 // in: fp16 NHWC [B][H][W][16]; Bt: packed fp16 weights [32][ldb] (k = tap*16 + c, ldb >= 144);
 // out: fp16 pooled [B][PH][PW][32] (opad: the interior of a zero-bordered [B][PH+2][PW+2][32]
 // buffer, the tile kernel's input).  SAME 3x3 stride 1, even OH/OW.
@@ -475,7 +478,9 @@ conv1_patch_f16_kernel(const half_t* __restrict__ in, const half_t* __restrict__
   constexpr int C = 16;
   constexpr int PATCH = SC_P * SC_P * C;      // halves
   constexpr int PATCH_CH = (PATCH * 2 + 1023) / 1024;  // 1-KiB DMA chunks
-  __shared__ __attribute__((aligned(1024))) float smem[2 * PATCH_CH * 256];
+  constexpr int SP = 40;  // output stage row pitch (halves): 32 columns + 8
+  __shared__ __attribute__((aligned(1024))) float smem[2 * PATCH_CH * 256 + 4 * 16 * SP / 2];
+  half_t* const stg = reinterpret_cast<half_t*>(smem + 2 * PATCH_CH * 256);
 
   const int lane = threadIdx.x & 63;
   const int wid = wave_uniform(threadIdx.x >> 6);
@@ -550,6 +555,26 @@ conv1_patch_f16_kernel(const half_t* __restrict__ in, const half_t* __restrict__
       }
     }
 
+#if C1F16_STAGE
+    // the wave's 2 x 8 windows x 32 columns through its LDS stage: one 16-B store per lane
+    half_t* const st = stg + wid * (16 * SP);
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        st[((i >> 1) * 8 + 4 * (i & 1) + fp) * SP + 16 * j + fr] =
+            (half_t)pool_then_epilogue(acc[i][j], pb[j], pm[j], ps[j], pg[j], epi.flags);
+    wait_lgkm0();
+    {
+      typedef half_t h8v __attribute__((ext_vector_type(8)));
+      const int wl = lane >> 2, cg = lane & 3;
+      const int wy = (y0 >> 1) + 2 * wid + (wl >> 3), wx = (x0 >> 1) + (wl & 7);
+      const h8v v = *reinterpret_cast<const h8v*>(st + wl * SP + 8 * cg);
+      if (wy < g.PH && wx < g.PW)
+        *reinterpret_cast<h8v*>(out + (((size_t)b * (g.PH + 2 * opad) + wy + opad) * (g.PW + 2 * opad) + wx + opad) * 32 +
+                                8 * cg) = v;
+    }
+#else
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int n = 16 * j + fr;
@@ -561,7 +586,8 @@ conv1_patch_f16_kernel(const half_t* __restrict__ in, const half_t* __restrict__
                     pool_then_epilogue(acc[i][j], pb[j], pm[j], ps[j], pg[j], epi.flags));
       }
     }
-    wait_lgkm0();  // (this tile's patch reads done before the barrier that frees its buffer)
+#endif
+    wait_lgkm0();  // (this tile's patch and stage reads done before the barrier that frees its buffer)
   }
 }
 
