@@ -211,6 +211,9 @@ int gemm16_cfg_bn(int cfg);
 // mode: GEMM_DENSE (A = [M][lda] fp16), GEMM_IMPLICIT / GEMM_IMPLICIT_POOL (A = NHWC fp16 input
 // described by ic; C % 8 == 0).  Kpad % 64 == 0; C is fp16 [M][ldc]; split-K partials in slab.
 // `tickets`: in-GEMM split-K combine as for launch_gemm (slab: splitk16_fused_slab_floats).
+bool gemm16_f32out_supported(int splits);
+int launch_gemm16_f32out(const half_t* A, int lda, const half_t* Bt, int ldb, float* C, int ldc, long long M, int N,
+                         int Kpad, const EpiParams& epi, hipStream_t stream);
 int launch_gemm16(int cfg, int mode, const half_t* A, int lda, const ImplicitConv& ic, const half_t* Bt, int ldb,
                   half_t* C, int ldc, long long M, int N, int Kpad, const EpiParams& epi, hipStream_t stream,
                   int splits = 1, float* slab = nullptr, unsigned* tickets = nullptr);

@@ -176,6 +176,31 @@ int launch_gemm16(int cfg, int mode, const half_t* A, int lda, const ImplicitCon
   }
 }
 
+// the fp16 plan's last layer when it is a dense GEMM without split-K (conv8): 32 x 128 tiles at
+// every M (the tile shape changes no sum), the epilogue's fp32 values stored as fp32 into the
+// plan's output (no fp16 rounding, no separate conversion kernel)
+bool gemm16_f32out_supported(int splits) { return splits == 1; }
+
+int launch_gemm16_f32out(const half_t* A, int lda, const half_t* Bt, int ldb, float* C, int ldc, long long M, int N,
+                         int Kpad, const EpiParams& epi, hipStream_t stream) {
+  if (M == 0 || N == 0) return 0;
+  const long long a_bytes = M * (long long)lda * 2;
+  const long long b_bytes = (long long)((N + 511) / 512) * 512 * ldb * 2;
+  if (Kpad % 64 != 0 || ldb % 8 != 0 || lda % 8 != 0 || M > 0x7fffffffLL ||
+      a_bytes >= 0x80000000LL || b_bytes >= 0x80000000LL) {
+    set_error("gemm16_f32out: unsupported shape M=%lld N=%d Kpad=%d", M, N, Kpad);
+    return -2;
+  }
+  const int tilesM = (int)((M + 31) / 32), tilesN = (N + 127) / 128;
+  SplitK sk{0, tilesM * tilesN, 0};
+  sk.nmajor = nmajor_order(N, tilesN);
+  const BufDesc bd{reinterpret_cast<const float*>(A), (unsigned)a_bytes, (unsigned)b_bytes};
+  hipLaunchKernelGGL((gemm_f16_glds_kernel<32, 128, 1, 4, 4, GEMM_DENSE, float, true>), dim3(tilesM * tilesN),
+                     dim3(256), 0, stream, A, lda, Bt, ldb, C, nullptr, ldc, (int)M, N, Kpad, epi, tilesN,
+                     ImplicitConv{}, sk, bd);
+  return check16("gemm16_f32out");
+}
+
 int launch_splitk_reduce16(const float* slab, int splits, long long M, int N, half_t* C, int ldc,
                            const EpiParams& epi, hipStream_t stream) {
   if (M == 0 || N == 0) return 0;

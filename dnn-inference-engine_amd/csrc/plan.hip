@@ -139,6 +139,7 @@ struct dnn_plan {
   bool patch = true;
   bool splitk_fused = true;  // fp32 split-K layers combine in the GEMM (no reduce kernel)
   int fp16 = 0;  // 1: fp16 activations/weights, fp16 MFMA, fp32 accumulate + epilogue
+  bool direct_out = false;  // fp16: the last layer writes the fp32 output itself (fp16_direct_out)
   bool latency = false;  // split K by M too (dnn_plan_set_latency_mode): batch-1 latency plans
   std::vector<PlanLayer> layers;
   std::vector<KernelDesc> kernels;
@@ -202,8 +203,17 @@ static void mark_front(dnn_plan* p) {
   }
 }
 
+// fp16 plans whose last layer is a dense GEMM the fp32-output launcher covers (conv8): it writes
+// the plan's fp32 output itself, no output conversion kernel.  DNN_HIP_F16_DIRECT_OUT=0: off.
+static bool fp16_direct_out(const dnn_plan* p) {
+  if (!p->fp16 || p->layers.empty() || getenv_flag_off("DNN_HIP_F16_DIRECT_OUT")) return false;
+  const PlanLayer& L = p->layers.back();
+  return L.type == 0 && L.mode == MODE_DIRECT_A && gemm16_f32out_supported(L.splits) && !L.out_padded;
+}
+
 static void layout(dnn_plan* p) {
   mark_front(p);
+  p->direct_out = fp16_direct_out(p);
   size_t off = 0, act = (size_t)p->in_h * p->in_w * p->in_c, col = 0, slab = 0, slab_fused = 0, tickets = 0;
   int nconv = 0, npool = 0;  // kernel names use conv / pool ordinals: "conv7.gemm" is YOLO's conv7
   p->kernels.clear();
@@ -290,7 +300,8 @@ static void layout(dnn_plan* p) {
   if (p->fp16) {  // fp16 plans convert at the edges: fp32 frames in (unless conv0 is direct), fp32 out
     if (p->layers.empty() || p->layers[0].mode != MODE_DIRECT)
       p->kernels.insert(p->kernels.begin(), {"input.cvt", -1, 4, 0.0, 6.0 * B * p->in_h * p->in_w * p->in_c});
-    p->kernels.push_back({"output.cvt", -1, 4, 0.0, 6.0 * B * p->cur_h * p->cur_w * p->cur_c});
+    if (!p->direct_out)
+      p->kernels.push_back({"output.cvt", -1, 4, 0.0, 6.0 * B * p->cur_h * p->cur_w * p->cur_c});
     for (auto& L : p->layers) L.kernel_idx += (p->layers.empty() || p->layers[0].mode != MODE_DIRECT) ? 1 : 0;
   }
   p->weight_floats = align_up(off, 64);
@@ -869,6 +880,11 @@ static int run_fp16(dnn_plan* p, int n, const float* d_in, float* d_out, hipStre
           break;
         }
         case MODE_DIRECT_A:
+          if (i == nl - 1 && p->direct_out) {
+            rc = launch_gemm16_f32out(cur, L.C, wt, L.Kpad, d_out, L.OC, Mc, L.OC, L.Kpad, epi, s);
+            if (rc) return rc;
+            return record(p, -1, s);
+          }
           rc = launch_gemm16(L.cfg, GEMM_DENSE, cur, L.C, ImplicitConv{}, wt, L.Kpad, dst, L.OC, Mc, L.OC, L.Kpad,
                              epi, s, L.splits, slab, tickets);
           break;

@@ -73,6 +73,9 @@ def dispatch_sequence(rows, key_start="Start_Timestamp", key_end="End_Timestamp"
             starts = [j for j in range(i, len(seq)) if seq[j]["Kernel_Name"] == first]
             if len(starts) > 1 and starts[1] - starts[0] == len(order) - 1 and "pool5" in order:
                 order = [k for k in order if k != "pool5"]  # pool5 fused into conv5 (x3_img)
+            elif len(starts) > 1 and starts[1] - starts[0] == len(order) - 2 and "output.cvt" in order:
+                # fp16, round 5: pool5 fused into conv5, conv8 writes the fp32 output itself
+                order = [k for k in order if k not in ("pool5", "output.cvt")]
         if name == first and i + len(order) <= len(seq):
             for j, pk in enumerate(order):
                 out.append((pk, seq[i + j]))
