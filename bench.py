@@ -51,6 +51,8 @@ BF16_MFMA_PEAK_TFLOPS = FP16_MFMA_PEAK_TFLOPS  # the bf16 forms take the F16 for
 X3_PRODUCTS = 6  # x3 conv: bf16 MFMA products per fp32 product (gemm_x3_patch.h)
 HBM_PEAK_GBS = 8000.0
 DOMINANT = "conv7.gemm"
+NOMINAL_SCLK_GHZ = 2.4  # the clock the MFMA peaks above are quoted at (MI355X_MICROARCH.md)
+CLOCK_WGS = 256  # clock-stamp workgroups per launch (one per CU: every XCD sampled)
 
 
 def parse():
@@ -593,16 +595,20 @@ def main():
         runner.reset_stats()
 
     # HIP events around the dominant kernel only (an event packet between every kernel costs
-    # the step ~1 %); --kernels: around every kernel, for the per-kernel table
+    # the step ~1 %); --kernels: around every kernel, for the per-kernel table.  Two clock-stamp
+    # launches on the run stream bracket the timed forwards (the shader clock over the region)
+    clk = torch.zeros((2, CLOCK_WGS, 4), dtype=torch.int64, device=dev)
     plan.timing_begin(args.steps, only=None if args.kernels else DOMINANT)
     torch.cuda.synchronize()
     if distributed:
         tdist.barrier()
     t0 = time.perf_counter()
+    dnn_hip.clock_stamp(clk[0].data_ptr(), CLOCK_WGS, stream)
     full = None
     for _ in range(args.steps):
         r = one_step()
         full = r if r is not None else full
+    dnn_hip.clock_stamp(clk[1].data_ptr(), CLOCK_WGS, stream)
     r = drain()
     full = r if r is not None else full
     torch.cuda.synchronize()
@@ -661,6 +667,30 @@ def main():
                      "dominant_kernel": DOMINANT,
                      "dominant_avg_launch_ms": round(ms_sus[kidx] / max(cnt_sus[kidx], 1), 4),
                      "preheat_steps": n_pre, "preheat_seconds": round(preheat_s, 3)}
+
+    # the dominant kernel's own shader clock: clock stamps right before and after it in each of
+    # a few further steps (outside its HIP-event window; a separate window, so the stamp launches
+    # never touch the timed or sustained steps)
+    clk_region = dnn_hip.sclk_from_stamps(clk[0].cpu().numpy(), clk[1].cpu().numpy())
+    n_clk = 20
+    kbuf = torch.zeros((n_clk, 2, CLOCK_WGS, 4), dtype=torch.int64, device=dev)
+    plan.clock_begin(DOMINANT, kbuf.data_ptr(), n_clk, CLOCK_WGS)
+    for _ in range(n_clk):
+        one_step()
+    drain()
+    torch.cuda.synchronize()
+    runs_clk = plan.clock_end()
+    kb = kbuf.cpu().numpy()
+    per_run = [dnn_hip.sclk_from_stamps(kb[i, 0], kb[i, 1]) for i in range(runs_clk)]
+    per_run = [c for c in per_run if c]
+    clk_kernel = None
+    if per_run:
+        med = lambda v: sorted(v)[len(v) // 2]
+        clk_kernel = {"mean": med([c["mean"] for c in per_run]), "min": med([c["min"] for c in per_run]),
+                      "max": med([c["max"] for c in per_run]), "runs": len(per_run),
+                      "window_us": med([c["window_us"] for c in per_run]),
+                      "per_xcd": {str(x): round(med([c["per_xcd"][x] for c in per_run if x in c["per_xcd"]]), 4)
+                                  for x in per_run[0]["per_xcd"]}}
 
     post_ms = None
     if args.gather == "detections":  # the postprocess kernel alone, for the per-kernel table
@@ -762,7 +792,21 @@ def main():
                                             "clock, so this frac and `frac` come from different boxes"),
                          "rocprof_same_box": prof.get("same_box"),
                          "with_reduce_achieved": round(mult * k["flops"] / (avg_s + red_s) / 1e12, 2),
-                         "reduce_ms": round(red_s * 1e3, 4)},
+                         "reduce_ms": round(red_s * 1e3, 4),
+                         # the measured shader clock (clock.hip stamps) and the fraction against
+                         # the peak at that clock: peak x sclk / 2.4 GHz
+                         "sclk_ghz": round(clk_kernel["mean"], 4) if clk_kernel else None,
+                         "sclk_ghz_xcd_min": round(clk_kernel["min"], 4) if clk_kernel else None,
+                         "sclk_ghz_xcd_max": round(clk_kernel["max"], 4) if clk_kernel else None,
+                         "sclk_ghz_per_xcd": clk_kernel["per_xcd"] if clk_kernel else None,
+                         "sclk_ghz_timed_region": round(clk_region["mean"], 4) if clk_region else None,
+                         "frac_at_measured_clock": round(achieved / (peak * clk_kernel["mean"] / NOMINAL_SCLK_GHZ), 4)
+                         if clk_kernel else None,
+                         "sclk_source": (f"s_memtime / s_memrealtime stamps (one workgroup per CU) right before "
+                                         f"and after {DOMINANT} in {clk_kernel['runs'] if clk_kernel else 0} "
+                                         "steps after the sustained window, per XCD, median over steps; "
+                                         "sclk_ghz = the mean over XCDs; sclk_ghz_timed_region: stamps "
+                                         "bracketing the timed steps; nominal 2.4 GHz")},
             # ALGORITHMIC fp32 flops over the fp32 MFMA peak: the x3 layers exceed 100 % by running on
             # the bf16 MFMA, so this is a speed figure, not an MFMA utilisation (that is `roofline`
             # for the dominant kernel, and `fp32_mfma` for the fp32-MFMA-only plan)

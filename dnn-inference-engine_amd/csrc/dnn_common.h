@@ -211,9 +211,9 @@ int gemm16_cfg_bn(int cfg);
 // mode: GEMM_DENSE (A = [M][lda] fp16), GEMM_IMPLICIT / GEMM_IMPLICIT_POOL (A = NHWC fp16 input
 // described by ic; C % 8 == 0).  Kpad % 64 == 0; C is fp16 [M][ldc]; split-K partials in slab.
 // `tickets`: in-GEMM split-K combine as for launch_gemm (slab: splitk16_fused_slab_floats).
-bool gemm16_f32out_supported(int splits);
-int launch_gemm16_f32out(const half_t* A, int lda, const half_t* Bt, int ldb, float* C, int ldc, long long M, int N,
-                         int Kpad, const EpiParams& epi, hipStream_t stream);
+bool gemm16_f32out_supported(int splits, int Npad);
+int launch_gemm16_f32out(const half_t* A, int lda, const half_t* Bt, int ldb, int Npad, float* C, int ldc, long long M,
+                         int N, int Kpad, const EpiParams& epi, hipStream_t stream);
 int launch_gemm16(int cfg, int mode, const half_t* A, int lda, const ImplicitConv& ic, const half_t* Bt, int ldb,
                   half_t* C, int ldc, long long M, int N, int Kpad, const EpiParams& epi, hipStream_t stream,
                   int splits = 1, float* slab = nullptr, unsigned* tickets = nullptr);
@@ -297,12 +297,8 @@ int launch_conv0_mfma(const float* in, const float* w, float* out, const DirectG
                       const EpiParams& epi, hipStream_t s);
 int launch_conv0_mfma_f16(const float* in, const float* w, half_t* out, const DirectGeom& g, int cin,
                           const EpiParams& epi, hipStream_t s);
-// conv_front.hip: conv0 (3 -> 16, pool) + conv1 (16 -> 32 on the x3 arithmetic, pool) as one kernel,
-// fp32 frames [B][H][W][3] in, conv1's pooled output as split planes of a zero-bordered
-// [B][H/4+2][W/4+2][32] buffer out; w0 HWIO [27][16], Bt1 packed by launch_pack_weights_x3 (C = 16)
-bool conv01_front_supported(int B, int H, int W);
-int launch_conv01_front(const float* in, const float* w0, const EpiParams& epi0, const unsigned short* Bt1,
-                        const EpiParams& epi1, unsigned short* out_split, int B, int H, int W, hipStream_t s);
+// clock.hip: nwg one-wave workgroups each storing {s_memtime, s_memrealtime, XCC_ID, HW_ID}
+int launch_clock_stamp(hipStream_t s, unsigned long long* out, int nwg);
 bool conv1_patch_f16_supported(int C, int OC, int H, int W, int OH, int OW, int kh, int kw, int sh, int sw, int pt,
                                int pl);
 int launch_conv1_patch_f16(const half_t* in, const half_t* Bt, int ldb, half_t* out, const DirectGeom& g,

@@ -74,6 +74,20 @@ conv3x3_f16_tile_kernel(const half_t* __restrict__ in, const half_t* __restrict_
   static_assert(WM * TM * 16 >= T && (WM - 1) * TM * 16 < T && NPW <= 16 && PU >= 4 && (MODE == 0 || MODE == 1) &&
                     (MODE == 0 ? TH % 2 == 0 && TW % 2 == 0 && NW * STGB <= BUFB : T * 64 * WN * 2 <= BUFB),
                 "shape");
+  // LDS regions (round 6 audit, DESIGN.md §2 "fp16 tile-kernel race"): two patch buffers of BUFB
+  // bytes, then the epilogue parameters (epl, WN x 64 f32x4).  Every access is bounded here:
+  //  * the DMA writes pieces 0 .. NP - 1 of a buffer, 1 KiB each: NP * 1024 == BUFB;
+  //  * the farthest fragment read (row T - 1 at tap (2, 2), lane quarter 3, 16 B) ends inside the
+  //    patch's NU units: (RU (TH + 1) + PU (TW + 1)) 16 + 64 <= 16 NU <= BUFB;
+  //  * the MODE 0 stage (NW waves x STGB) and the MODE 1 stage (T rows x 64 WN halves) fit one
+  //    buffer, so the stage never reaches the other buffer (the next pair's patch) or epl;
+  //  * epl reads are epl[wn 64 + 16 jb + fr] < 64 WN;
+  //  * two workgroups per CU (__launch_bounds__) fit the 160 KiB of LDS.
+  static_assert(NP * 1024 == BUFB && NP * 64 >= NU, "patch pieces");
+  static_assert((RU * (TH + 1) + PU * (TW + 1)) * 16 + 64 <= NU * 16, "fragment reads inside the patch");
+  static_assert(MODE == 0 ? (NW * STGB <= BUFB && 4 * TM * SROW * 2 == STGB) : (T * 64 * WN * 2 <= BUFB), "stage");
+  static_assert(WN * 64 == 16 * NJ * WN, "epl covers the workgroup's columns");
+  static_assert(2 * (2 * BUFB + WN * 64 * 16) <= 160 * 1024, "two workgroups per CU");
   __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * BUFB + WN * 64 * 16];
   f32x4* const epl = reinterpret_cast<f32x4*>(smem + 2 * BUFB);
 

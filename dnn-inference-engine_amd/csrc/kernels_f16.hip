@@ -178,16 +178,19 @@ int launch_gemm16(int cfg, int mode, const half_t* A, int lda, const ImplicitCon
 
 // the fp16 plan's last layer when it is a dense GEMM without split-K (conv8): 32 x 128 tiles at
 // every M (the tile shape changes no sum), the epilogue's fp32 values stored as fp32 into the
-// plan's output (no fp16 rounding, no separate conversion kernel)
-bool gemm16_f32out_supported(int splits) { return splits == 1; }
+// plan's output (no fp16 rounding, no separate conversion kernel).  The tiles are 128 columns wide
+// and their epilogue reads the parameters of every column of the tile, so the layer's packed
+// weights and epilogue vectors must cover whole 128-column tiles (Npad % 128 == 0): a narrower head
+// (OC <= 64, Npad 32 / 64) stays on the general launcher, whose tile width divides its Npad.
+bool gemm16_f32out_supported(int splits, int Npad) { return splits == 1 && Npad > 0 && Npad % 128 == 0; }
 
-int launch_gemm16_f32out(const half_t* A, int lda, const half_t* Bt, int ldb, float* C, int ldc, long long M, int N,
-                         int Kpad, const EpiParams& epi, hipStream_t stream) {
+int launch_gemm16_f32out(const half_t* A, int lda, const half_t* Bt, int ldb, int Npad, float* C, int ldc, long long M,
+                         int N, int Kpad, const EpiParams& epi, hipStream_t stream) {
   if (M == 0 || N == 0) return 0;
   const long long a_bytes = M * (long long)lda * 2;
-  const long long b_bytes = (long long)((N + 511) / 512) * 512 * ldb * 2;
-  if (Kpad % 64 != 0 || ldb % 8 != 0 || lda % 8 != 0 || M > 0x7fffffffLL ||
-      a_bytes >= 0x80000000LL || b_bytes >= 0x80000000LL) {
+  const long long b_bytes = (long long)Npad * ldb * 2;  // the layer's own rows only
+  if (!gemm16_f32out_supported(1, Npad) || N > Npad || Kpad % 64 != 0 || ldb % 8 != 0 || lda % 8 != 0 ||
+      M > 0x7fffffffLL || a_bytes >= 0x80000000LL || b_bytes >= 0x80000000LL) {
     set_error("gemm16_f32out: unsupported shape M=%lld N=%d Kpad=%d", M, N, Kpad);
     return -2;
   }
@@ -404,11 +407,16 @@ static int tile16_shape(int H, int W) {
   return best;
 }
 
+// shape limits only (the launcher's check); the plan also applies the DNN_HIP_TILE16 switch
+static bool tile16_shape_ok(int C, int OC, int H, int W) {
+  return C % 32 == 0 && OC % 64 == 0 && H % 2 == 0 && W % 2 == 0 && H >= 2 && W >= 2 &&
+         (long long)(H + 2) * (W + 2) * C * 2 < 0x40000000LL && (long long)OC * 9 * C * 2 < 0x80000000LL;
+}
+
 bool conv_tile16_supported(int C, int OC, int H, int W, int OH, int OW, int kh, int kw, int sh, int sw, int pt,
                            int pl) {
-  return kh == 3 && kw == 3 && sh == 1 && sw == 1 && pt == 1 && pl == 1 && OH == H && OW == W && C % 32 == 0 &&
-         OC % 64 == 0 && H % 2 == 0 && W % 2 == 0 && H >= 2 && W >= 2 && tile16_enabled() &&
-         (long long)(H + 2) * (W + 2) * C * 2 < 0x40000000LL && (long long)OC * 9 * C * 2 < 0x80000000LL;
+  return kh == 3 && kw == 3 && sh == 1 && sw == 1 && pt == 1 && pl == 1 && OH == H && OW == W &&
+         tile16_shape_ok(C, OC, H, W) && tile16_enabled();
 }
 
 template <int SH, int WN, int FL>
@@ -431,15 +439,17 @@ static int tile16_wgs_per_cu() {
 #define IMG16_BR 3
 #endif
 // whole-frame form (MODE 1) with the 2x2/s1 SAME pool fused: 13 x 13 frames (conv5 + pool5)
+static bool img16_shape_ok(int C, int OC, int H, int W) {
+  return H == 13 && W == 13 && C % 32 == 0 && OC % 64 == 0 && (long long)OC * 9 * C * 2 < 0x80000000LL;
+}
 bool conv_img16_supported(int C, int OC, int H, int W) {
   const char* e = getenv("DNN_HIP_IMG16");
-  return H == 13 && W == 13 && C % 32 == 0 && OC % 64 == 0 && tile16_enabled() && !(e && e[0] == '0') &&
-         (long long)OC * 9 * C * 2 < 0x80000000LL;
+  return img16_shape_ok(C, OC, H, W) && tile16_enabled() && !(e && e[0] == '0');
 }
 
 static int launch_img16(const half_t* in_padded, const half_t* Bt, int ldb, half_t* out, int out_padded, int n, int N,
                         int K, int H, int W, int C, const EpiParams& epi, hipStream_t stream) {
-  if (!conv_img16_supported(C, N, H, W) || K != 9 * C || ldb < K || ldb % 32 != 0) {
+  if (!img16_shape_ok(C, N, H, W) || K != 9 * C || ldb < K || ldb % 32 != 0) {
     set_error("conv_img16: unsupported shape N=%d K=%d %dx%dx%d ldb=%d", N, K, H, W, C, ldb);
     return -2;
   }
@@ -476,7 +486,7 @@ int launch_conv_tile16(const half_t* in_padded, const half_t* Bt, int ldb, half_
                        int K, int H, int W, int C, const EpiParams& epi, hipStream_t stream, int pool) {
   if (n == 0 || N == 0) return 0;
   if (pool == 2) return launch_img16(in_padded, Bt, ldb, out, out_padded, n, N, K, H, W, C, epi, stream);
-  if (pool != 1 || !conv_tile16_supported(C, N, H, W, H, W, 3, 3, 1, 1, 1, 1) || K != 9 * C || ldb < K ||
+  if (pool != 1 || !tile16_shape_ok(C, N, H, W) || K != 9 * C || ldb < K ||
       ldb % 32 != 0) {
     set_error("conv_tile16: unsupported shape N=%d K=%d %dx%dx%d ldb=%d", N, K, H, W, C, ldb);
     return -2;

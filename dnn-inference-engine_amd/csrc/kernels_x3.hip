@@ -333,7 +333,9 @@ int launch_pack_weights_x3(const float* w, bf16_bits* out, int K, int N, int Npa
 // ---- the conv
 constexpr int X3_BM = 176, X3_NPR = 320;
 
-// DNN_HIP_X3=0 keeps these layers on the fp32 MFMA (implicit GEMM)
+// DNN_HIP_X3=0 keeps these layers on the fp32 MFMA (implicit GEMM).  The DNN_HIP_* switches are
+// read by the *_supported functions the plan calls when it chooses a layer's kernel; launchers
+// check shape limits only, so a plan keeps running what it chose if the environment changes later.
 static bool x3_enabled() {
   const char* e = getenv("DNN_HIP_X3");
   return !(e && e[0] == '0');
@@ -369,9 +371,10 @@ constexpr int X3T_TM = 7;  // row blocks of 16 per wave
 
 // which kernel runs an x3 layer: 0 the row-run kernel (N % 256 == 0), 1 tile kernel N = 64 from
 // one 32-channel chunk, 2 tile kernel N % 128 == 0 (double-buffered chunks), 3 the 16-channel
-// kernel (fp32 input, split while staged); -1 none (the layer stays on the fp32 MFMA)
+// kernel (fp32 input, split while staged); -1 none (the layer stays on the fp32 MFMA).  Shape
+// only: DNN_HIP_X3_C16=0 is applied by conv_x3_supported at plan time.
 static int x3_kind(int N, int C) {
-  if (C == 16) return N == 32 && !getenv_flag_off("DNN_HIP_X3_C16") ? 3 : -1;
+  if (C == 16) return N == 32 ? 3 : -1;
   if (N % 256 == 0) return 0;
   if (N == 64 && C == 32) return 1;
   if (N % 128 == 0) return 2;
@@ -385,7 +388,9 @@ bool conv_x3_supported(int C, int OC, int H, int W, int OH, int OW, int kh, int 
         (C % 32 == 0 || C == 16) && x3_enabled()))
     return false;
   const int kind = x3_kind(OC, C);
-  if (kind < 0 || ((kind == 1 || kind == 2) && getenv_flag_off("DNN_HIP_X3_TILE"))) return false;
+  if (kind < 0 || ((kind == 1 || kind == 2) && getenv_flag_off("DNN_HIP_X3_TILE")) ||
+      (kind == 3 && getenv_flag_off("DNN_HIP_X3_C16")))
+    return false;
   // a tile must fit the patch for any batch: spans grow with M only until a tile crosses whole
   // images, so two images' worth of rows decides it (tile kernel: fixed patch)
   return kind > 0 || x3_span(2LL * H * W + X3_BM, H, W) <= X3_NPR;
@@ -632,7 +637,7 @@ bool conv_x3_lat_supported(long long batch, int C, int OC, int H, int W, int OH,
 // (conv5: 13 x 13 x 256; one-row tiles, one row block, two chunks per group).
 // pool: 0 none, 1 a fused 2x2/s2 pool, 2 a fused 2x2/s1 SAME pool (YOLO's pool5; 13-wide shape)
 static int x3_ktile_shape(int C, int OC, int H, int W, int pool) {
-  if (OC % 64 != 0 || !x3_enabled()) return -1;
+  if (OC % 64 != 0) return -1;
   if (C == 128 && W > 13 && W <= 26 && (pool == 0 || (pool == 1 && H % 2 == 0 && W % 2 == 0))) return 0;
   if (C == 256 && W <= 13 && pool != 1) return 1;
   if (C == 64 && OC == 128 && W > 26 && W <= 52 && (pool == 0 || (pool == 1 && H % 2 == 0 && W % 2 == 0)))
@@ -642,8 +647,11 @@ static int x3_ktile_shape(int C, int OC, int H, int W, int pool) {
 
 // conv3x3_x3_img_kernel (gemm_x3_img.h): whole-image tiles, instantiated for YOLOv2-tiny's 13x13
 // frames.  DNN_HIP_X3_IMG=0 (plan time) keeps the wide kernel's K slices + the pool5 combine.
+static bool x3_img_shape_ok(int C, int OC, int H, int W) {
+  return H == 13 && W == 13 && C % 32 == 0 && OC % 128 == 0;
+}
 bool conv_x3_img_supported(int C, int OC, int H, int W) {
-  return H == 13 && W == 13 && C % 32 == 0 && OC % 128 == 0 && x3_enabled() && !getenv_flag_off("DNN_HIP_X3_IMG");
+  return x3_img_shape_ok(C, OC, H, W) && x3_enabled() && !getenv_flag_off("DNN_HIP_X3_IMG");
 }
 
 int launch_conv_x3_img(const bf16_bits* in_split, const bf16_bits* Bt, float* out, bf16_bits* out_split, int n, int N,
@@ -651,7 +659,7 @@ int launch_conv_x3_img(const bf16_bits* in_split, const bf16_bits* Bt, float* ou
   if (n == 0 || N == 0) return 0;
   const long long in_bytes = (long long)x3_act_bytes(n, H, W, C);
   const long long b_bytes = (long long)(Npad / 16) * (K / 32) * 3072;
-  if (!conv_x3_img_supported(C, N, H, W) || K != 9 * C || Npad != N || (out_split == nullptr) == (out == nullptr) ||
+  if (!x3_img_shape_ok(C, N, H, W) || K != 9 * C || Npad != N || (out_split == nullptr) == (out == nullptr) ||
       in_bytes >= 0x80000000LL || b_bytes >= 0x80000000LL || x3_act_bytes(n, H, W, N) >= 0x80000000ULL) {
     set_error("conv_x3_img: unsupported shape n=%d N=%d K=%d %dx%dx%d", n, N, K, H, W, C);
     return -2;
@@ -673,7 +681,7 @@ int launch_conv_x3_img(const bf16_bits* in_split, const bf16_bits* Bt, float* ou
 bool conv_x3_ktile_supported(long long batch, int C, int OC, int H, int W, int OH, int OW, int kh, int kw, int sh,
                              int sw, int pt, int pl, int pool) {
   if (!(kh == 3 && kw == 3 && sh == 1 && sw == 1 && pt == 1 && pl == 1 && OH == H && OW == W)) return false;
-  if (x3_ktile_shape(C, OC, H, W, pool) < 0) return false;
+  if (!x3_enabled() || x3_ktile_shape(C, OC, H, W, pool) < 0) return false;
   return (long long)x3_act_bytes(batch, H, W, C) < 0x80000000LL &&
          (long long)(OC / 16) * (9 * C / 32) * 3072 < 0x80000000LL;
 }
@@ -739,12 +747,14 @@ int launch_conv_x3_ktile(const bf16_bits* in_split, const bf16_bits* Bt, float* 
 
 // 1x1 form (latency plans' conv8): 16 rows x 32 columns, K groups of one wave (4; at K = 1024: 16
 // groups, 16 columns)
-bool conv_x3_1x1_ktile_supported(int C, int OC, int H, int W) {
+static bool x3_1x1_ktile_shape_ok(int C, int OC, int H, int W) {
   // the launcher's instantiations: K / 128 = 1, 2, 4 or 8 chunk quads (other widths, e.g. C = 384
   // after a kind-2 tile conv, stay on the fp32 GEMM)
   const int nq = C / 128;
-  return C % 128 == 0 && (nq == 1 || nq == 2 || nq == 4 || nq == 8) && OC >= 1 && H >= 1 && W >= 1 && x3_enabled() &&
-         !getenv_flag_off("DNN_HIP_X3_1X1");
+  return C % 128 == 0 && (nq == 1 || nq == 2 || nq == 4 || nq == 8) && OC >= 1 && H >= 1 && W >= 1;
+}
+bool conv_x3_1x1_ktile_supported(int C, int OC, int H, int W) {
+  return x3_1x1_ktile_shape_ok(C, OC, H, W) && x3_enabled() && !getenv_flag_off("DNN_HIP_X3_1X1");
 }
 
 int launch_conv_x3_1x1_ktile(const bf16_bits* in_split, const bf16_bits* Bt, float* out, long long M, int N, int Npad,
@@ -754,7 +764,7 @@ int launch_conv_x3_1x1_ktile(const bf16_bits* in_split, const bf16_bits* Bt, flo
   const long long in_bytes = (long long)x3_act_bytes(nimg, H, W, C);
   const long long b_bytes = (long long)(Npad / 16) * (K / 32) * 3072;
   const int cpk = K / 128;
-  if (M % per_img != 0 || K != C || !conv_x3_1x1_ktile_supported(C, N, H, W) || Npad % 32 != 0 || Npad < N ||
+  if (M % per_img != 0 || K != C || !x3_1x1_ktile_shape_ok(C, N, H, W) || Npad % 32 != 0 || Npad < N ||
       in_bytes >= 0x80000000LL || b_bytes >= 0x80000000LL || M > 0x7fffffffLL ||
       (cpk != 1 && cpk != 2 && cpk != 4 && cpk != 8)) {
     set_error("conv_x3_1x1_ktile: unsupported shape M=%lld N=%d K=%d %dx%dx%d", M, N, K, H, W, C);

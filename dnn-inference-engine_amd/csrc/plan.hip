@@ -111,8 +111,6 @@ struct PlanLayer {
   bool x3k = false;    // MODE_X3 with the K split inside the workgroup (latency plans: launch_conv_x3_ktile)
   bool pool1 = false;  // x3k / x3img: a 2x2/stride-1 SAME pool fused (same output frame)
   bool x3img = false;  // MODE_X3 on whole-image tiles over all of K (launch_conv_x3_img), pool1 fused
-  bool front = false;  // conv0 (MODE_DIRECT) run together with the next layer (the 16-channel x3
-                       // conv1) as one kernel (conv_front.hip); the next layer launches nothing
   bool out_padded = false;  // output written zero-bordered (the next layer is MODE_PATCH16 / MODE_X3;
                             // fp32 plans: as x3 split planes)
   size_t pad_off = 0;       // its zero-bordered output region: float offset inside the pad area
@@ -162,6 +160,11 @@ struct dnn_plan {
   int timing_only = -1;  // >= 0: events only around that kernel (dnn_plan_timing_begin_only)
   std::vector<hipEvent_t> ev;
   std::vector<int> ev_kernel;
+  // shader-clock stamps around one kernel (dnn_plan_clock_begin): run r's stamps of the opening
+  // launch at clk_buf + 2 r nwg 4, of the closing launch 4 nwg further (clock.hip)
+  int clk_kernel = -1, clk_cap = 0, clk_used = 0, clk_nwg = 0;
+  bool clk_open = false;
+  unsigned long long* clk_buf = nullptr;
   // captured forward (dnn_plan_run_graph)
   hipGraph_t graph = nullptr;
   hipGraphExec_t gexec = nullptr;
@@ -180,39 +183,15 @@ static void drop_graph(dnn_plan* p) {
 
 static bool fused_splitk(const dnn_plan* p) { return p->splitk_fused; }
 
-// conv0 -> conv1 as one kernel (conv_front.hip) where the plan has YOLO's front: a 3-channel 3x3
-// SAME conv to 16 channels with its 2x2/s2 pool on the direct kernel, then the 16-channel x3 conv
-// to 32 channels with its pool, writing the next x3 layer's split planes.  Batch plans only (the
-// latency plans keep their single-frame conv1 shape); DNN_HIP_FRONT=0 keeps two kernels.
-static void mark_front(dnn_plan* p) {
-  for (auto& L : p->layers) L.front = false;
-  if (p->fp16 || p->latency || !p->fuse) return;
-  for (size_t i = 0; i + 1 < p->layers.size(); ++i) {
-    const PlanLayer& a = p->layers[i];
-    const PlanLayer& c = p->layers[i + 1];
-    const bool conv0 = a.type == 0 && a.mode == MODE_DIRECT && a.pool && a.C == 3 && a.OC == 16 && a.kh == 3 &&
-                       a.kw == 3 && a.sh == 1 && a.sw == 1 && a.pt == 1 && a.pl == 1 && a.OH == a.H && a.OW == a.W &&
-                       a.PH * 2 == a.OH && a.PW * 2 == a.OW;
-    const bool conv1 = c.type == 0 && c.mode == MODE_X3 && c.C == 16 && c.OC == 32 && c.pool && !c.x3k && !c.x3lat &&
-                       c.splits == 1 && c.out_padded && c.H == a.PH && c.W == a.PW && c.kh == 3 && c.kw == 3 &&
-                       c.pt == 1 && c.pl == 1 && c.OH == c.H && c.OW == c.W;
-    if (conv0 && conv1 && conv01_front_supported(p->batch, a.H, a.W)) {
-      p->layers[i].front = true;
-      ++i;
-    }
-  }
-}
-
 // fp16 plans whose last layer is a dense GEMM the fp32-output launcher covers (conv8): it writes
 // the plan's fp32 output itself, no output conversion kernel.  DNN_HIP_F16_DIRECT_OUT=0: off.
 static bool fp16_direct_out(const dnn_plan* p) {
   if (!p->fp16 || p->layers.empty() || getenv_flag_off("DNN_HIP_F16_DIRECT_OUT")) return false;
   const PlanLayer& L = p->layers.back();
-  return L.type == 0 && L.mode == MODE_DIRECT_A && gemm16_f32out_supported(L.splits) && !L.out_padded;
+  return L.type == 0 && L.mode == MODE_DIRECT_A && gemm16_f32out_supported(L.splits, L.Npad) && !L.out_padded;
 }
 
 static void layout(dnn_plan* p) {
-  mark_front(p);
   p->direct_out = fp16_direct_out(p);
   size_t off = 0, act = (size_t)p->in_h * p->in_w * p->in_c, col = 0, slab = 0, slab_fused = 0, tickets = 0;
   int nconv = 0, npool = 0;  // kernel names use conv / pool ordinals: "conv7.gemm" is YOLO's conv7
@@ -225,19 +204,6 @@ static void layout(dnn_plan* p) {
     const double in_b = 4.0 * B * L.H * L.W * L.C, out_b = 4.0 * B * L.out_h() * L.out_w() * L.OC;
     L.kernel_idx = (int)p->kernels.size();
     char nm[64];
-    if (i > 0 && p->layers[i - 1].front) {  // conv1 inside the front kernel: its weights, no kernel
-      L.kernel_idx = p->layers[i - 1].kernel_idx;
-      L.w_off = off;
-      off = align_up(off + (size_t)L.Npad * L.Kpad * 3 / 2, 64);
-      L.epi_off = off;
-      off = align_up(off + 4 * (size_t)L.Npad, 64);
-      KernelDesc& f = p->kernels.back();
-      f.flops += 2.0 * M * L.OC * L.K;
-      f.bytes += 6.0 * B * (L.out_h() + 2) * (L.out_w() + 2) * L.OC + 4.0 * L.K * L.OC;  // split planes out
-      if (L.pool) npool++;
-      ++nconv;
-      continue;
-    }
     if (L.type == 0) {
       L.w_off = off;
       // fp16 GEMM layers hold Bt in halves (2 per float slot); conv0's direct kernel reads fp32
@@ -256,10 +222,6 @@ static void layout(dnn_plan* p) {
         p->kernels.push_back({nm, (int)i, 0, 0.0, 4.0 * M * L.K + in_b});
         snprintf(nm, sizeof(nm), "conv%d.gemm", nconv++);
         p->kernels.push_back({nm, (int)i, 1, flops, 4.0 * M * L.K + w_b + out_b});
-      } else if (L.front) {  // frames in (conv1's output bytes added with conv1)
-        snprintf(nm, sizeof(nm), "conv%d+%d.gemm", nconv, nconv + 1);
-        ++nconv;
-        p->kernels.push_back({nm, (int)i, 1, flops, in_b + w_b});
       } else if (L.mode == MODE_DIRECT || L.mode == MODE_PATCH) {
         snprintf(nm, sizeof(nm), L.mode == MODE_DIRECT ? "conv%d.direct" : "conv%d.patch", nconv++);
         p->kernels.push_back({nm, (int)i, 1, flops, in_b + w_b + out_b});
@@ -826,7 +788,28 @@ int dnn_plan_weight_buffer(const dnn_plan* p, void** ptr, size_t* bytes) {
   return 0;
 }
 
+static int record_events(dnn_plan* p, int kernel, hipStream_t s);
+
+// before each kernel (its plan index) and after the last one (-1): HIP events (timing) and the
+// clock stamps around the stamped kernel — the opening stamp before its opening event, the closing
+// stamp after the event that closes it, so an event-timed kernel never contains a stamp launch
 static int record(dnn_plan* p, int kernel, hipStream_t s) {
+  int rc;
+  const bool close_now = p->clk_open;
+  if (!close_now && p->clk_kernel >= 0 && kernel == p->clk_kernel && p->clk_used < p->clk_cap) {
+    if ((rc = launch_clock_stamp(s, p->clk_buf + (size_t)p->clk_used * 8 * p->clk_nwg, p->clk_nwg))) return rc;
+    p->clk_open = true;
+  }
+  if ((rc = record_events(p, kernel, s))) return rc;
+  if (close_now) {
+    if ((rc = launch_clock_stamp(s, p->clk_buf + ((size_t)p->clk_used * 8 + 4) * p->clk_nwg, p->clk_nwg))) return rc;
+    p->clk_open = false;
+    p->clk_used++;
+  }
+  return 0;
+}
+
+static int record_events(dnn_plan* p, int kernel, hipStream_t s) {
   if (!p->timing) return 0;
   if (p->timing_only >= 0) {  // one kernel: its opening event and the next one (which closes it)
     const bool closes = p->ev_used > 0 && p->ev_kernel[p->ev_used - 1] == p->timing_only;
@@ -881,7 +864,7 @@ static int run_fp16(dnn_plan* p, int n, const float* d_in, float* d_out, hipStre
         }
         case MODE_DIRECT_A:
           if (i == nl - 1 && p->direct_out) {
-            rc = launch_gemm16_f32out(cur, L.C, wt, L.Kpad, d_out, L.OC, Mc, L.OC, L.Kpad, epi, s);
+            rc = launch_gemm16_f32out(cur, L.C, wt, L.Kpad, L.Npad, d_out, L.OC, Mc, L.OC, L.Kpad, epi, s);
             if (rc) return rc;
             return record(p, -1, s);
           }
@@ -986,18 +969,6 @@ int dnn_plan_run(dnn_plan* p, int n, const float* d_in, float* d_out, void* stre
           break;
         }
         case MODE_DIRECT: {
-          if (L.front) {  // conv0 + conv1 (conv_front.hip) into conv1's split planes
-            PlanLayer& L1 = p->layers[i + 1];
-            const float* e1 = p->weights + L1.epi_off;
-            const EpiParams epi1{e1, e1 + L1.Npad, e1 + 2 * L1.Npad, e1 + 3 * L1.Npad, L1.epi_flags};
-            unsigned short* ds1 = padr + L1.pad_off * 2;
-            rc = launch_conv01_front(cur, wt, epi, reinterpret_cast<const unsigned short*>(p->weights + L1.w_off),
-                                     epi1, ds1, n, L.H, L.W, s);
-            if (rc) return rc;
-            ++i;
-            cur = reinterpret_cast<const float*>(ds1);
-            continue;
-          }
           DirectGeom g{n, L.H, L.W, L.OH, L.OW, L.PH, L.PW, L.pt, L.pl};
           rc = conv0_mfma_supported(L.C, L.OC, L.kh, L.kw, L.sh, L.sw)
                    ? launch_conv0_mfma(cur, wt, dst, g, L.C, zero, epi, s)
@@ -1100,6 +1071,7 @@ int dnn_plan_run_graph(dnn_plan* p, int n, const float* d_in, float* d_out, void
   DNN_REQUIRE(p && p->finalized, "dnn_plan_run_graph: plan not finalized");
   DNN_REQUIRE(stream != nullptr, "dnn_plan_run_graph: needs a created stream (NULL cannot be captured)");
   DNN_REQUIRE(!p->timing, "dnn_plan_run_graph: per-kernel timing is active");
+  DNN_REQUIRE(p->clk_kernel < 0, "dnn_plan_run_graph: clock stamping is active");
   DNN_REQUIRE(n >= 0 && n <= p->batch, "dnn_plan_run_graph: n=%d outside [0, %d]", n, p->batch);
   if (n == 0) return 0;
   hipStream_t s = static_cast<hipStream_t>(stream);
@@ -1152,10 +1124,9 @@ int dnn_plan_describe(const dnn_plan* p, char* buf, int buf_len) {
     if (L.type == 0) {
       char sk[32] = "";
       if (L.splits > 1) snprintf(sk, sizeof(sk), " splitK=%d", L.splits);
-      const bool fr = L.front || (i > 0 && p->layers[i - 1].front);
-      snprintf(line, sizeof(line), "conv %dx%dx%d -> %dx%dx%d k%dx%d s%d mode=%s cfg=%d K=%d Kpad=%d%s%s%s%s%s%s\n", L.H,
+      snprintf(line, sizeof(line), "conv %dx%dx%d -> %dx%dx%d k%dx%d s%d mode=%s cfg=%d K=%d Kpad=%d%s%s%s%s%s\n", L.H,
                L.W, L.C, L.out_h(), L.out_w(), L.OC, L.kh, L.kw, L.sh, L.x3lat ? "x3_lat" : L.x3k ? "x3_ktile" : L.x3img ? "x3_img" : kModeName[L.mode], L.cfg, L.K, L.Kpad,
-               L.pool ? " +pool2x2s2" : L.pool1 ? " +pool2x2s1" : "", fr ? " front01" : "", sk,
+               L.pool ? " +pool2x2s2" : L.pool1 ? " +pool2x2s1" : "", sk,
                L.splits > 1 ? (L.mode == MODE_X3 ? " x3-combine" : fused_splitk(p) ? " combine" : "") : "",
                p->fp16 ? " fp16" : "", p->latency ? " latency" : "");
     } else
@@ -1191,6 +1162,30 @@ int dnn_plan_timing_begin_only(dnn_plan* p, int max_runs, int kernel_idx) {
   int rc = dnn_plan_timing_begin(p, max_runs);
   if (rc) return rc;
   p->timing_only = kernel_idx;
+  return 0;
+}
+
+int dnn_plan_clock_begin(dnn_plan* p, int kernel_idx, unsigned long long* dev_buf, int max_runs, int nwg) {
+  DNN_REQUIRE(p && p->finalized, "dnn_plan_clock_begin: plan not finalized");
+  DNN_REQUIRE(kernel_idx >= 0 && kernel_idx < (int)p->kernels.size(), "dnn_plan_clock_begin: bad kernel index %d",
+              kernel_idx);
+  DNN_REQUIRE(dev_buf && max_runs > 0 && nwg > 0 && nwg <= 65536, "dnn_plan_clock_begin: bad buffer / runs / nwg");
+  p->clk_kernel = kernel_idx;
+  p->clk_buf = dev_buf;
+  p->clk_cap = max_runs;
+  p->clk_nwg = nwg;
+  p->clk_used = 0;
+  p->clk_open = false;
+  return 0;
+}
+
+int dnn_plan_clock_end(dnn_plan* p, int* runs) {
+  DNN_REQUIRE(p && p->clk_kernel >= 0, "dnn_plan_clock_end: clock stamping not active");
+  DNN_REQUIRE(!p->clk_open, "dnn_plan_clock_end: a stamped kernel was not closed");
+  if (runs) *runs = p->clk_used;
+  p->clk_kernel = -1;
+  p->clk_buf = nullptr;
+  p->clk_used = p->clk_cap = 0;
   return 0;
 }
 

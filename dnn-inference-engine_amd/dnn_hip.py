@@ -71,6 +71,9 @@ def _bind_plan_api(lib):
         "dnn_plan_timing_begin": (i, [vp, i]),
         "dnn_plan_timing_begin_only": (i, [vp, i, i]),
         "dnn_plan_timing_end": (i, [vp, P(ctypes.c_double), P(ctypes.c_longlong)]),
+        "dnn_clock_stamp": (i, [vp, vp, i]),
+        "dnn_plan_clock_begin": (i, [vp, i, vp, i, i]),
+        "dnn_plan_clock_end": (i, [vp, P(i)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -507,6 +510,35 @@ def lower_graph(g):
     return entries
 
 
+def clock_stamp(dev_ptr, nwg, stream_ptr, lib=None):
+    """Launch the clock-stamp kernel (dnn_clock_stamp): nwg workgroups, 4 uint64 each at dev_ptr."""
+    lib = lib or load_library()
+    _check(lib.dnn_clock_stamp(ctypes.c_void_p(stream_ptr), ctypes.c_void_p(dev_ptr), int(nwg)), "clock_stamp", lib)
+
+
+def sclk_from_stamps(start, end):
+    """Mean shader clock per XCD between two stamp launches (arrays [nwg][4] of uint64:
+    s_memtime, s_memrealtime (100 MHz), XCC_ID, HW_ID): per XCD the median of each counter over
+    its workgroups, then d(memtime) / d(memrealtime) x 100 MHz.  Returns {"mean", "min", "max",
+    "per_xcd": {xcd: GHz}, "window_us"} (GHz, the mean over XCDs)."""
+    import numpy as np
+    a, b = np.asarray(start, dtype=np.uint64), np.asarray(end, dtype=np.uint64)
+    per = {}
+    win = []
+    for x in sorted(set(int(v) for v in a[:, 2]) & set(int(v) for v in b[:, 2])):
+        sa, sb = a[a[:, 2] == x], b[b[:, 2] == x]
+        dt = float(np.median(sb[:, 0].astype(np.float64))) - float(np.median(sa[:, 0].astype(np.float64)))
+        dr = float(np.median(sb[:, 1].astype(np.float64))) - float(np.median(sa[:, 1].astype(np.float64)))
+        if dr > 0 and dt > 0:
+            per[x] = dt / dr * 0.1  # memrealtime ticks at 100 MHz: GHz = (dt / dr) x 0.1
+            win.append(dr * 0.01)   # microseconds
+    if not per:
+        return None
+    v = list(per.values())
+    return {"mean": sum(v) / len(v), "min": min(v), "max": max(v), "per_xcd": per,
+            "window_us": sum(win) / len(win)}
+
+
 def _pad_code(padding):
     return 1 if padding == 'SAME' else 0
 
@@ -649,6 +681,18 @@ class Plan(object):
         cnt = (ctypes.c_longlong * nk)()
         _check(self.lib.dnn_plan_timing_end(self.h, ms, cnt), "timing_end", self.lib)
         return list(ms), list(cnt)
+
+    def clock_begin(self, kernel, dev_buf_ptr, max_runs, nwg):
+        """Shader-clock stamps around `kernel` (a kernel name) in the next runs, into a device
+        buffer of max_runs x 8 x nwg uint64 (dnn_plan_clock_begin; sclk_from_stamps reads them)."""
+        idx = [k["name"] for k in self.kernels()].index(kernel)
+        _check(self.lib.dnn_plan_clock_begin(self.h, idx, ctypes.c_void_p(dev_buf_ptr), int(max_runs), int(nwg)),
+               "clock_begin", self.lib)
+
+    def clock_end(self):
+        runs = ctypes.c_int()
+        _check(self.lib.dnn_plan_clock_end(self.h, ctypes.byref(runs)), "clock_end", self.lib)
+        return runs.value
 
     def close(self):
         if getattr(self, "h", None):

@@ -119,6 +119,19 @@ int dnn_plan_timing_begin(dnn_plan* plan, int max_runs);
 int dnn_plan_timing_begin_only(dnn_plan* plan, int max_runs, int kernel_idx);
 int dnn_plan_timing_end(dnn_plan* plan, double* ms_sum, long long* launches);
 
+/* Shader-clock measurement (rooflines against the measured clock).
+ * dnn_clock_stamp: launches `nwg` one-wave workgroups on `stream`; workgroup w stores four
+ * uint64 at dev_out[4 w ..]: s_memtime (shader clock counter), s_memrealtime (100 MHz), XCC_ID,
+ * HW_ID.  Two stamps bracketing a region give, per XCD, the mean shader clock over it:
+ * d(memtime) / d(memrealtime) x 100 MHz.
+ * dnn_plan_clock_begin: the next runs (up to max_runs) bracket kernel `kernel_idx` with two such
+ * launches each — run r's opening stamps at dev_buf[8 r nwg], closing ones at [(8 r + 4) nwg];
+ * dev_buf holds max_runs x 8 x nwg uint64.  The stamps sit outside the kernel's HIP-event window.
+ * dnn_plan_clock_end: stops stamping and returns the number of stamped runs. */
+int dnn_clock_stamp(void* stream, unsigned long long* dev_out, int nwg);
+int dnn_plan_clock_begin(dnn_plan* plan, int kernel_idx, unsigned long long* dev_buf, int max_runs, int nwg);
+int dnn_plan_clock_end(dnn_plan* plan, int* runs);
+
 #pragma GCC visibility pop
 #ifdef __cplusplus
 }

@@ -110,16 +110,17 @@ EOF2
     ;;
   profiles)
     P="--gather outputs"
-    prof fused_trace --kernel-trace --stats -- --steps 10 --warmup 3 $FAST || exit 1
+    # (the traces run with --gather outputs too: no postprocess kernel beside conv0 / conv1)
+    prof fused_trace --kernel-trace --stats -- --steps 10 --warmup 3 $FAST $P || exit 1
     prof fused_fetch --pmc FETCH_SIZE -- --steps 3 --warmup 1 $FAST $NOHEAT $P || exit 1
     prof fused_write --pmc WRITE_SIZE -- --steps 3 --warmup 1 $FAST $NOHEAT $P || exit 1
     for g in sqa sqb; do bash "$0" pmc $g || exit 1; done
     export DNN_HIP_FUSE=0
-    prof unf_trace --kernel-trace --stats -- --steps 10 --warmup 3 $FAST || exit 1
+    prof unf_trace --kernel-trace --stats -- --steps 10 --warmup 3 $FAST $P || exit 1
     prof unf_fetch --pmc FETCH_SIZE -- --steps 3 --warmup 1 $FAST $NOHEAT $P || exit 1
     prof unf_write --pmc WRITE_SIZE -- --steps 3 --warmup 1 $FAST $NOHEAT $P || exit 1
     unset DNN_HIP_FUSE
-    prof f16_trace --kernel-trace --stats -- --steps 10 --warmup 3 $FAST --precision fp16 || exit 1
+    prof f16_trace --kernel-trace --stats -- --steps 10 --warmup 3 $FAST $P --precision fp16 || exit 1
     prof f16_fetch --pmc FETCH_SIZE -- --steps 3 --warmup 1 $FAST $NOHEAT $P --precision fp16 || exit 1
     prof f16_write --pmc WRITE_SIZE -- --steps 3 --warmup 1 $FAST $NOHEAT $P --precision fp16 || exit 1
     echo PROFILESOK

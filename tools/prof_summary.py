@@ -49,7 +49,7 @@ def with_reduces(order):
 
 # every kernel of the plan lives in namespace dnnhip; weight packing (finalize) and the
 # postprocessing kernels (after the forward) are not plan kernels
-_NOT_PLAN = ("pack_weights", "yolo_", "f32_to_f16_kernel", "preprocess_kernel")
+_NOT_PLAN = ("pack_weights", "yolo_", "f32_to_f16_kernel", "preprocess_kernel", "clock_stamp")
 
 
 def _ours(name):
@@ -68,8 +68,6 @@ def dispatch_sequence(rows, key_start="Start_Timestamp", key_end="End_Timestamp"
         name = seq[i]["Kernel_Name"]
         if first is None:
             first = name  # the first dispatch of the first forward defines the start marker
-            if "conv01_front" in name:  # conv0 + conv1 as one kernel (conv_front.hip)
-                order = ["conv0+1.gemm"] + [k for k in ORDER if k not in ("conv0.direct", "conv1.gemm")]
             starts = [j for j in range(i, len(seq)) if seq[j]["Kernel_Name"] == first]
             if len(starts) > 1 and starts[1] - starts[0] == len(order) - 1 and "pool5" in order:
                 order = [k for k in order if k != "pool5"]  # pool5 fused into conv5 (x3_img)

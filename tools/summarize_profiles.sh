@@ -23,6 +23,8 @@ p = json.load(open(sys.argv[2]))
 r = b["roofline"]
 p["same_box"] = {"images_per_s": b["value"], "ms_per_step": b["ms_per_step"], "dominant_kernel": r["kernel"],
                  "dominant_event_ms": r["avg_launch_ms"], "event_frac": r["frac"],
+                 "sclk_ghz": r.get("sclk_ghz"), "sclk_ghz_timed_region": r.get("sclk_ghz_timed_region"),
+                 "event_frac_at_measured_clock": r.get("frac_at_measured_clock"),
                  "note": "bench.py line of the same gpurun call (same box) as this trace"}
 json.dump(p, open(sys.argv[2], "w"), indent=1)
 EOF
