@@ -72,6 +72,14 @@ constexpr int PP_DIAG_WGS = 512;
 __device__ unsigned long long pp_diag_stamps[PP_DIAG_WGS * 8];
 #endif
 
+#if (X3DIAG & 32768) != 0  // conv3x3_x3_c16pp_kernel step cycles
+constexpr int C16PP_DIAG_WGS = 512;
+// [workgroup][slot]: s_memtime sums of wave 0 (team A) in 0-3 and wave 4 (team B) in 4-7: MFMA steps,
+// store steps' wait + split + next loads, their fold + epilogue + stores, barrier waits; 8 total
+// cycles of wave 0; 9 tiles of team A
+__device__ unsigned long long c16pp_diag_stamps[C16PP_DIAG_WGS * 16];
+#endif
+
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 struct X3Geom {
@@ -757,6 +765,280 @@ conv3x3_x3_c16p_kernel(const float* __restrict__ in, const bf16_bits* __restrict
   }
 #endif
 #undef C16_STAMP
+}
+
+
+// Ping-pong form of the persistent 16-channel kernel (round 6: conv1 at batch grids).  The c16p
+// stamps (round 4): per tile the split of the staged fp32 patch (~4.7 k cycles), the MFMAs (~9.6 k,
+// ~6 k of them the wave's own) and the pool / epilogue / split-plane stores (~6 k) run one after
+// the other in each workgroup, and two independent workgroups per CU line them up at random (MFMA
+// pipes ~57 % busy).  Here ONE workgroup per CU runs two teams of 4 waves (one wave of each team
+// per SIMD) over a contiguous range of the CU's tiles (team A the even ones, team B the odd ones)
+// in lock step, as conv3x3_x3_pp_kernel: every step ends at a workgroup barrier; in each step one
+// team runs its MFMAs (at issue priority 1) while the other runs its store step -- wait for its
+// next tile's fp32 patch (loaded into registers one step earlier), split it into the team's patch
+// area, issue the loads of the tile after it, then fold, pool + epilogue through the stage and
+// store the pooled split planes of the tile it just computed.  LDS: the 30 KB of weights once (both
+// teams), one split patch per team (48 KB each), one stage area (the store steps never overlap),
+// 150 KB in all.  Products, order and epilogue per output are conv3x3_x3_c16p_kernel<true, true>'s:
+// the same bits (tested).
+template <int FL = -1>
+__global__ void __launch_bounds__(512, 1)
+conv3x3_x3_c16pp_kernel(const float* __restrict__ in, const bf16_bits* __restrict__ Bt,
+                        bf16_bits* __restrict__ out_split, EpiParams epi, int tilesX, int tilesY, int ntiles,
+                        X3Geom g, unsigned in_bytes, int ppprio) {
+  constexpr int TH = 16, TW = 26, WM = 4, TM = 7;
+  constexpr int NT = 64 * WM, PB = 96, PW2 = TW + 2, PR = (TH + 2) * PW2, T = TH * TW, NS = 5;
+  constexpr int ITEMS = PR * 4, PPT = (ITEMS + NT - 1) / NT;  // item = (patch pixel, channel quad), per team
+  constexpr int BB = 2 * NS * 3 * 1024, BPT = (BB / 16 + 2 * NT - 1) / (2 * NT);
+  constexpr int NO = T / 4, PATCH = PR * PB, STGW = TM * 4 * X3_STG_ROW;  // stage floats per wave
+  static_assert(WM * TM * 16 >= T && (WM * TM - 3) * 16 < T && PPT == 8, "shape");
+  static_assert(BB + 2 * PATCH + WM * STGW * 4 + 32 * 16 <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[BB + 2 * PATCH + WM * STGW * 4];
+  __shared__ f32x4 epl[32];
+
+  const int lane = threadIdx.x & 63;
+  const int eflags = FL < 0 ? epi.flags : FL;
+  const int wid = wave_uniform(threadIdx.x >> 6);
+  const int team = wid >> 2, wm = wid & 3, tt = threadIdx.x & (NT - 1);
+  const int fr = lane & 15, fq = lane >> 4, th = fq >> 1;
+  unsigned char* const patch = smem + BB + team * PATCH;
+  float* const stgp = reinterpret_cast<float*>(smem + BB + 2 * PATCH) + wm * STGW;
+  // this workgroup's tiles [lo, hi) (balanced, XCD-local order); the team's k-th is lo + team + 2 k
+  const int wg = xcd_tile(blockIdx.x, gridDim.x);
+  const int lo = (int)((long long)ntiles * wg / gridDim.x), hi = (int)((long long)ntiles * (wg + 1) / gridDim.x);
+  const int nmine = (hi - lo - team + 1) / 2;
+
+  if (threadIdx.x < 32) {
+    const X3EpiCol c = x3_epi_col(epi, eflags, threadIdx.x);
+    epl[threadIdx.x] = f32x4{c.pb, c.pm, c.ps, c.pg};
+  }
+  {  // weights once (both teams): the packed [n/16][step][piece][lane][8] block of columns 0-31
+    u32x4 w[BPT];
+#pragma unroll
+    for (int u = 0; u < BPT; ++u) {
+      int e = threadIdx.x + u * 2 * NT;
+      e = e < BB / 16 ? e : BB / 16 - 1;
+      w[u] = *reinterpret_cast<const u32x4*>(reinterpret_cast<const unsigned char*>(Bt) + 16 * e);
+    }
+#pragma unroll
+    for (int u = 0; u < BPT; ++u) {
+      int e = threadIdx.x + u * 2 * NT;
+      e = e < BB / 16 ? e : BB / 16 - 1;
+      *reinterpret_cast<u32x4*>(smem + 16 * e) = w[u];
+    }
+  }
+
+  const auto rsA = __builtin_amdgcn_make_buffer_rsrc((void*)in, 0, (int)in_bytes, 0x00020000);
+  auto tile_of = [&](int k, int& b, int& y0, int& x0) {
+    const int t = lo + team + 2 * k;
+    const int tx = t % tilesX, t2 = t / tilesX, ty = t2 % tilesY;
+    b = t2 / tilesY;
+    y0 = ty * TH;
+    x0 = tx * TW;
+  };
+  f32x4 stg[PPT];
+  auto load_tile = [&](int k) {
+    int b, y0, x0;
+    tile_of(k, b, y0, x0);
+#pragma unroll
+    for (int d = 0; d < PPT; ++d) {
+      int e = tt + d * NT;
+      e = e < ITEMS ? e : ITEMS - 1;
+      const int pr = e >> 2, q = e & 3, py = pr / PW2, px = pr - py * PW2;
+      const int iy = y0 - 1 + py, ix = x0 - 1 + px;
+      const bool ok = (unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W;
+      const unsigned vo = ok ? (unsigned)((((b * g.H + iy) * g.W + ix) * 16 + 4 * q) * 4) : OOB_OFF;
+      stg[d] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsA, vo, 0, 0));
+    }
+  };
+  auto split_tile = [&]() {  // 16-B fp32 channel quad -> three 8-B bf16 quads (pieces at 32 p + 8 q)
+    bool ok = true;
+#pragma unroll
+    for (int d = 0; d < PPT; ++d)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) ok = ok && x3_split_ok(stg[d][c]);
+    const bool fast = __builtin_amdgcn_ballot_w64(!ok) == 0;
+#pragma unroll
+    for (int d = 0; d < PPT; ++d) {
+      int e = tt + d * NT;
+      e = e < ITEMS ? e : ITEMS - 1;
+      const int dst = (e >> 2) * PB + 8 * (e & 3);
+      uint2 w[3];
+      split3_pack2(fast, stg[d][0], stg[d][1], w[0].x, w[1].x, w[2].x);
+      split3_pack2(fast, stg[d][2], stg[d][3], w[0].y, w[1].y, w[2].y);
+#pragma unroll
+      for (int p = 0; p < 3; ++p) *reinterpret_cast<uint2*>(patch + dst + 32 * p) = w[p];
+    }
+  };
+
+  // fragment rows as conv3x3_x3_c16p_kernel (pool-window-major rows)
+  constexpr int NPP = (TM + 1) / 2;
+  static_assert(PR * PB < 65536, "16-bit patch offsets");
+  unsigned prow2[NPP];
+#pragma unroll
+  for (int k = 0; k < NPP; ++k) prow2[k] = 0;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    int r = (wm * TM + i) * 16 + fr;
+    r = r < T ? r : T - 1;
+    const int w = r >> 2, q = r & 3;
+    const int ly = 2 * (w / (TW / 2)) + (q >> 1), lx = 2 * (w % (TW / 2)) + (q & 1);
+    prow2[i / 2] |= (unsigned)(((ly + 1) * PW2 + lx + 1) * PB) << (16 * (i % 2));
+  }
+  auto prow = [&](int i) {
+    unsigned w = prow2[i / 2];
+    asm volatile("" : "+v"(w));
+    return (int)((w >> (16 * (i % 2))) & 0xffffu);
+  };
+  const int fqo = 16 * (fq & 1);
+  auto toff = [&](int s) {
+    const int ta = 2 * s, tb = 2 * s + 1 < 9 ? 2 * s + 1 : 8;
+    const int oa = ((ta / 3 - 1) * PW2 + (ta % 3 - 1)) * PB, ob = ((tb / 3 - 1) * PW2 + (tb % 3 - 1)) * PB;
+    return th ? ob : oa;
+  };
+  auto frag = [&](int i, int off, bf16x8 (&a)[3]) {
+    const unsigned char* q = patch + prow(i) + fqo + off;
+#pragma unroll
+    for (int p = 0; p < 3; ++p) a[p] = *reinterpret_cast<const bf16x8*>(q + 32 * p);
+  };
+  auto bfrag = [&](int s, bf16x8 (&bb)[3][2]) {
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        bb[p][j] = *reinterpret_cast<const bf16x8*>(smem + (j * NS * 3 + s * 3 + p) * 1024 + lane * 16);
+  };
+  typedef short s16x4 __attribute__((ext_vector_type(4)));
+  const int hoff = (PW2 + 1) * PB + 8 * fq;
+  const int hb = (fr + 16 * (fq >> 1)) * 16 + 8 * (fq & 1);
+
+  // prologue: each team's first patch split into its area, its second tile's loads in flight
+  if (nmine > 0) {
+    load_tile(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    split_tile();
+    if (nmine > 1) load_tile(1);
+  }
+  __syncthreads();  // weights, epl, both teams' first patches
+
+  const int nA = (hi - lo + 1) / 2, nB = (hi - lo) / 2;
+  const int nsteps = 2 * nA > 2 * nB + 1 ? 2 * nA : 2 * nB + 1;
+#if (X3DIAG & 32768) != 0
+  unsigned long long dg[4] = {0, 0, 0, 0}, t_in = __builtin_amdgcn_s_memtime(), t_start = t_in;
+#define C16PP_MARK(slot)                                           \
+  {                                                                \
+    const unsigned long long t_now = __builtin_amdgcn_s_memtime(); \
+    dg[slot] += t_now - t_in;                                      \
+    t_in = t_now;                                                  \
+  }
+#else
+#define C16PP_MARK(slot)
+#endif
+  if (team == 1) {
+    C16PP_MARK(2)
+    __syncthreads();
+    C16PP_MARK(3)
+  }
+  for (int k = 0; k < nmine; ++k) {
+    f32x4 acc[TM][2], accc[TM][2];
+    {  // MFMA step of tile k (conv3x3_x3_c16p_kernel's loop)
+      if (ppprio) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = accc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      constexpr int NSF = NS - 1;  // full 16x16x32 steps; tap 8 alone on 16x16x16 below
+      bf16x8 af[2][3], bq[3][2];
+      frag(0, toff(0), af[0]);
+#pragma unroll
+      for (int s = 0; s < NSF; ++s) {
+        const int off = toff(s), off_next = toff(s + 1 < NSF ? s + 1 : s);
+        bfrag(s, bq);
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const int cur = (s * TM + i) & 1, nxt = cur ^ 1;
+          if (i + 1 < TM)
+            frag(i + 1, off, af[nxt]);
+          else if (s + 1 < NSF)
+            frag(0, off_next, af[nxt]);
+#pragma unroll
+          for (int jb = 0; jb < 2; ++jb) x3_step<true>(acc[i][jb], accc[i][jb], af[cur], bq, jb);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+      s16x4 hbq[3][2];
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) hbq[p][j] = *reinterpret_cast<const s16x4*>(smem + (j * NS * 3 + 4 * 3 + p) * 1024 + hb);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int pr = prow(i);
+        s16x4 a[3];
+#pragma unroll
+        for (int p = 0; p < 3; ++p) a[p] = *reinterpret_cast<const s16x4*>(patch + pr + hoff + 32 * p);
+#pragma unroll
+        for (int jb = 0; jb < 2; ++jb) {
+          f32x4 c = accc[i][jb];
+          c = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a[2], hbq[0][jb], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a[1], hbq[1][jb], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a[0], hbq[2][jb], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a[1], hbq[0][jb], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a[0], hbq[1][jb], c, 0, 0, 0);
+          accc[i][jb] = c;
+          acc[i][jb] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a[0], hbq[0][jb], acc[i][jb], 0, 0, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      wait_lgkm0();
+      if (ppprio) __builtin_amdgcn_s_setprio(0);
+    }
+    C16PP_MARK(0)
+    __syncthreads();  // the team's patch is read by all its waves (and the other team's store step is done)
+    C16PP_MARK(3)
+    {  // store step: tile k + 1's patch in, tile k + 2's loads out, tile k's pooled split planes out
+      if (k + 1 < nmine) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile k + 1's fp32 patch (and tile k - 1's stores)
+        split_tile();
+        if (k + 2 < nmine) load_tile(k + 2);
+      }
+      C16PP_MARK(1)
+      x3_fold(acc, accc);
+      int b, y0, x0;
+      tile_of(k, b, y0, x0);
+      float epb[2], epm[2], eps[2], epg[2];
+#pragma unroll
+      for (int jb = 0; jb < 2; ++jb) {
+        const f32x4 e = epl[16 * jb + fr];
+        epb[jb] = e[0], epm[jb] = e[1], eps[jb] = e[2], epg[jb] = e[3];
+      }
+      pool_epilogue_batch<FL>(acc, epb, epm, eps, epg, epi.flags,
+                              [&](int i, int jb, float v) { stgp[(4 * i + fq) * X3_STG_ROW + 16 * jb + fr] = v; });
+      auto orow_of = [&](int w) {
+        const int py = (y0 >> 1) + w / (TW / 2), px = (x0 >> 1) + w % (TW / 2);
+        return (py >= g.PH || px >= g.PW) ? -1 : (b * (g.PH + 2) + py + 1) * (g.PW + 2) + px + 1;
+      };
+      x3_pool_split_store_f<TM>(stgp, orow_of, NO, 4 * wm * TM, out_split, 96, 0, lane);
+      wait_lgkm0();  // the split patch written, the stage read
+      C16PP_MARK(2)
+    }
+    __syncthreads();
+    C16PP_MARK(3)
+  }
+  for (int st = team + 2 * nmine; st < nsteps; ++st) __syncthreads();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#if (X3DIAG & 32768) != 0
+  if ((threadIdx.x & 255) == 0 && blockIdx.x < C16PP_DIAG_WGS) {  // (vector stores from lane 0)
+    unsigned long long* d = c16pp_diag_stamps + 16 * blockIdx.x + 4 * team;
+    d[0] = dg[0], d[1] = dg[1], d[2] = dg[2], d[3] = dg[3];
+    if (team == 0) {
+      c16pp_diag_stamps[16 * blockIdx.x + 8] = __builtin_amdgcn_s_memtime() - t_start;
+      c16pp_diag_stamps[16 * blockIdx.x + 9] = (unsigned long long)nmine;
+    }
+  }
+#endif
+#undef C16PP_MARK
 }
 
 

@@ -459,6 +459,19 @@ int launch_conv_x3(const bf16_bits* in_split, const bf16_bits* Bt, float* out, b
       const int ty4 = (H + 3) / 4;
       hipLaunchKernelGGL((conv3x3_x3_c16_kernel<4, 26, 4, 2, true>), dim3((unsigned)(nimg * tilesX * ty4)), dim3(256), 0,
                          stream, in32p, Bt, out, out_split, N, epi, tilesX, ty4, xg, (unsigned)in32);
+    } else if (pool && out_split && blocks >= 4LL * device_cu_count() && !getenv_flag_off("DNN_HIP_X3_C16PP") &&
+               !getenv_flag_off("DNN_HIP_X3_C16P")) {
+      // batch grids (>= 4 tiles per CU): the ping-pong form, one 512-thread workgroup per CU, the
+      // persistent kernel's bits (conv3x3_x3_c16pp_kernel).  DNN_HIP_X3_C16PP=0 (read per launch,
+      // A/B) keeps the two-workgroup persistent kernel; DNN_HIP_X3_PP_PRIO=0 the default priority
+      const int G = device_cu_count();
+      const int prio = !getenv_flag_off("DNN_HIP_X3_PP_PRIO");
+      if (epi.flags == X3_YOLO_FL)
+        hipLaunchKernelGGL((conv3x3_x3_c16pp_kernel<X3_YOLO_FL>), dim3((unsigned)G), dim3(512), 0, stream, in32p, Bt,
+                           out_split, epi, tilesX, tilesY, (int)blocks, xg, (unsigned)in32, prio);
+      else
+        hipLaunchKernelGGL((conv3x3_x3_c16pp_kernel<-1>), dim3((unsigned)G), dim3(512), 0, stream, in32p, Bt,
+                           out_split, epi, tilesX, tilesY, (int)blocks, xg, (unsigned)in32, prio);
     } else if (getenv_flag_off("DNN_HIP_X3_C16P") || !pool) {  // (the persistent kernel: the pooled form, conv1)
       if (pool)
         hipLaunchKernelGGL((conv3x3_x3_c16_kernel<16, 26, 4, 7, true>), dim3((unsigned)blocks), dim3(256), 0, stream,
@@ -946,6 +959,17 @@ extern "C" __attribute__((visibility("default"))) int dnn_acc2_diag_stamps(unsig
 }
 #endif
 
+#if (X3DIAG & 32768) != 0
+// diagnostic builds (X3DIAG bit 32768): conv3x3_x3_c16pp_kernel's per-workgroup step cycle sums of its
+// last launch (16 per workgroup, gemm_x3_patch.h) copied to host[0 .. 16 n)
+extern "C" __attribute__((visibility("default"))) int dnn_c16pp_diag_stamps(unsigned long long* host, int n) {
+  if (n < 0 || n > dnnhip::C16PP_DIAG_WGS) return -2;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(dnnhip::c16pp_diag_stamps), (size_t)n * 16 * sizeof(unsigned long long),
+                             0, hipMemcpyDeviceToHost) == hipSuccess
+             ? 0
+             : -1;
+}
+#endif
 #if (X3DIAG & 2048) != 0
 // diagnostic builds (X3DIAG bit 2048): conv3x3_x3_pp_kernel's per-workgroup step cycle sums of its
 // last launch (8 per workgroup, gemm_x3_patch.h) copied to host[0 .. 8 n)

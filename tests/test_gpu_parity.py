@@ -1990,6 +1990,62 @@ def test_x3_pingpong_equals_tile_kernel(monkeypatch, B):
     assert R.normwise_err(outs["1"], ref) < 3 * LAYER_TOL
 
 
+@pytest.mark.parametrize("case", [(11, 208, 208), (9, 200, 210)])
+def test_x3_c16_pingpong_equals_persistent(monkeypatch, case):
+    """conv1's ping-pong kernel (conv3x3_x3_c16pp_kernel: one 512-thread workgroup per CU, two
+    wave teams alternating MFMA and store steps; batch grids of >= 4 tiles per CU) equals the
+    two-workgroup persistent kernel (DNN_HIP_X3_C16PP=0) bit for bit -- YOLO's 208 x 208 frames
+    and ragged 200 x 210 ones (partial tiles on both edges), tile counts that leave the teams of a
+    workgroup unequal work; repeat runs equal; batch rows equal batch-1 runs; within the fp32
+    tolerance of the float64 oracle; negative-gamma channels."""
+    B, H, W = case
+    rng = np.random.default_rng(B * 31 + H + W)
+    x = rng.standard_normal((B, H, W, 16)).astype(np.float32)
+
+    def layer(c, od):
+        k = (rng.standard_normal((3, 3, c, od)) * np.sqrt(2.0 / (9 * c))).astype(np.float32)
+        b = rng.standard_normal(od).astype(np.float32) * 0.1
+        gam = rng.uniform(0.5, 1.5, od).astype(np.float32)
+        gam[::5] *= -1
+        return k, b, (rng.standard_normal(od).astype(np.float32) * 0.1, rng.uniform(0.5, 1.5, od).astype(np.float32),
+                      gam)
+
+    layers = [(layer(16, 32), True), (layer(32, 64), False)]
+
+    def graph(shape):
+        g = dnn_hip.DnnGraphBuilder()
+        y = g.create_input(list(shape))
+        y = g.create_max_pool2d(y, [1, 2, 2, 1], [1, 1, 1, 1], "SAME")  # (an fp32 producer before conv1)
+        for (k, b, n), pool in layers:
+            y = g.create_conv2d(y, k, [1, 1, 1, 1], "SAME")
+            y = g.create_bias_add(y, b)
+            y = g.create_batch_norm(y, *n, 1e-5)
+            y = g.create_leaky_relu(y)
+            if pool:
+                y = g.create_max_pool2d(y, [1, 2, 2, 1], [1, 2, 2, 1], "SAME")
+        g.set_out_node(y)
+        return g
+
+    outs = {}
+    for arm in ("1", "0"):
+        monkeypatch.setenv("DNN_HIP_X3_C16PP", arm)
+        eng = dnn_hip.DnnInferenceEngine(graph(x.shape), False)
+        conv = [ln for ln in eng.plan().describe().splitlines() if ln.startswith("conv")]
+        assert all("mode=patch_x3" in c for c in conv) and "+pool2x2s2" in conv[0], conv
+        outs[arm] = eng.run(x)
+        assert np.array_equal(eng.run(x), outs[arm]), arm
+    assert np.array_equal(outs["1"], outs["0"])
+    monkeypatch.delenv("DNN_HIP_X3_C16PP")
+    one = dnn_hip.DnnInferenceEngine(graph((1,) + x.shape[1:]), False)
+    assert np.array_equal(one.run(x[B - 1:B]), outs["1"][B - 1:B])
+    ref = R.max_pool2d(x[[0, B - 1]], [1, 2, 2, 1], [1, 1, 1, 1], "SAME")
+    for (k, b, n), pool in layers:
+        ref = R.leaky_relu(R.batch_norm(R.bias_add(R.conv2d(ref, k), b), *n, 1e-5))
+        if pool:
+            ref = R.max_pool2d(ref, [1, 2, 2, 1], [1, 2, 2, 1], "SAME")
+    assert R.normwise_err(outs["1"][[0, B - 1]], ref) < 3 * LAYER_TOL
+
+
 def test_x3_tile_small_tiles_same_bits():
     """The narrow x3 tile kernel's two tile shapes (kernels_x3.hip: 8 x 26 / 4 x 26 tiles when a
     launch has at least two workgroups per CU, else 2 x 26 tiles of 2 x 2 waves -- the single-frame

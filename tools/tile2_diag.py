@@ -116,6 +116,19 @@ def main():
                       ("team B MFMA steps", 3), ("team B store steps", 4), ("team B barrier waits", 5),
                       ("total (wave 0)", 6)):
             print("  %-22s %10.0f" % (nm, statistics.median(r[i] for r in rows)))
+    fc = getattr(plan.lib, "dnn_c16pp_diag_stamps", None)
+    if fc is not None:  # X3DIAG 32768: conv1's ping-pong kernel's step cycles
+        fc.restype = ctypes.c_int
+        fc.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        cb = (ctypes.c_ulonglong * (512 * 16))()
+        assert fc(cb, 512) == 0
+        rows = [list(cb[16 * w:16 * w + 16]) for w in range(512) if cb[16 * w + 8] > 0]
+        print("ping-pong conv1: %d workgroups, median cycles per workgroup (tiles of team A %d)" %
+              (len(rows), statistics.median(r[9] for r in rows) if rows else 0))
+        for nm, i in (("team A MFMA steps", 0), ("team A wait+split+loads", 1), ("team A epilogue+stores", 2),
+                      ("team A barrier waits", 3), ("team B MFMA steps", 4), ("team B wait+split+loads", 5),
+                      ("team B epilogue+stores", 6), ("team B barrier waits", 7), ("total (wave 0)", 8)):
+            print("  %-24s %10.0f" % (nm, statistics.median(r[i] for r in rows)))
     fi = getattr(plan.lib, "dnn_img_diag_stamps", None)
     if fi is not None:  # X3DIAG 16384: the whole-image kernel's phases (conv5 + pool5)
         fi.restype = ctypes.c_int
