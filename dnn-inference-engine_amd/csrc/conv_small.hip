@@ -214,14 +214,23 @@ constexpr int C0_ROWS_PER_WAVE = 5;  // 20 row DMAs per tile over 4 waves (rows 
 // FL: the epilogue flag set at compile time (-1: runtime `epi.flags`); EVEN: OH and OW even, so
 // no pool window is ragged (YOLO's 416 x 416: the per-window edge selects drop out).  (Round 3's
 // SPL form stored conv1's split planes here: conv1 -15 us, conv0 +23 us; removed, git history.)
-template <int CIN, int FL = -1, bool EVEN = false>
+// D16 (round 6; CIN = 3, W % 4 == 0): the patch rows by 16-B LDS-DMA, three rows per
+// instruction.  A patch row is the aligned run of 22 pixels from x0 - 4 (17 units of 16 B, 68
+// floats: the 18 patch pixels start at float 9); with W % 4 == 0 and x0 % 16 == 0 a 16-B unit never
+// straddles the frame edge, so out-of-frame units take the out-of-range offset as whole units.  Two
+// DMA instructions per wave and tile (rows 3 j .. 3 j + 2 for j = wid, wid + 4; waves 2 and 3's
+// second is a dummy of zeros into spare rows 18-20) instead of five 4-B row DMAs.
+template <int CIN, int FL = -1, bool EVEN = false, bool D16 = false>
 __global__ void __launch_bounds__(256, 7)  // 7 waves per SIMD (<= 72 registers): latency-bound, occupancy pays
 conv0_packed_pool_kernel(const float* __restrict__ in, const float* __restrict__ w, float* __restrict__ out,
                          DirectGeom g, int tilesX, int tilesY, int ntiles, const float* __restrict__ zero,
                          EpiParams epi, uint4 mags) {  // mags: magic numbers of tilesX, tilesY (div_magic)
-  constexpr int K = 9 * CIN, KS = (K + 3) / 4, RW = SC_P * CIN, RS = C0_RS;
-  static_assert(RW <= RS && RW <= 64, "patch row");
-  __shared__ __attribute__((aligned(16))) float patch[3][(4 * C0_ROWS_PER_WAVE) * RS];  // triple buffer
+  constexpr int K = 9 * CIN, KS = (K + 3) / 4, RW = SC_P * CIN, RS = D16 ? 68 : C0_RS;
+  constexpr int NDMA = D16 ? 2 : C0_ROWS_PER_WAVE;  // DMA instructions per wave and tile
+  constexpr int PROWS = D16 ? 21 : 4 * C0_ROWS_PER_WAVE;  // LDS rows per buffer (D16: 18 + the dummies' 3)
+  constexpr int X0F = D16 ? 3 * CIN : 0;  // float offset of patch pixel 0 in an LDS row
+  static_assert(RW <= RS && RW <= 64 && (!D16 || CIN == 3), "patch row");
+  __shared__ __attribute__((aligned(16))) float patch[3][PROWS * RS];  // triple buffer
   __shared__ __attribute__((aligned(16))) float stage[4][2][8][16];  // per wave: 2 window rows x 8 windows x 16 ch
 
   const int lane = threadIdx.x & 63;
@@ -245,7 +254,7 @@ conv0_packed_pool_kernel(const float* __restrict__ in, const float* __restrict__
 
   // the lane's pixel in M-tile 0 (rows pool-window-major: row = 4*window + 2*dy + dx); M-tile
   // i adds the constant 2*(i>>1) rows and 8*(i&1) pixels
-  const int pix0 = (4 * wid + ((fr & 3) >> 1)) * RS + (2 * (fr >> 2) + (fr & 1)) * CIN;
+  const int pix0 = (4 * wid + ((fr & 3) >> 1)) * RS + (2 * (fr >> 2) + (fr & 1)) * CIN + X0F;
 
   // tile coordinates: one set of divisions per tile, shared by its DMA issue and its stores
   struct Tile {
@@ -263,6 +272,25 @@ conv0_packed_pool_kernel(const float* __restrict__ in, const float* __restrict__
   const auto rsIn = __builtin_amdgcn_make_buffer_rsrc((void*)in, 0, (int)((size_t)g.B * g.H * g.W * CIN * 4), 0x00020000);
   (void)zero;
   auto issue = [&](const Tile& c, bool valid, int buf) {
+    if constexpr (D16) {
+      // lane l < 51 of instruction j: patch row 3 j + l / 17, unit l % 17 of the run from pixel
+      // xa = 16 tx - 4 (patch pixel 0 = xa + 3: pl == 1, launcher)
+      const int xa = c.tx * SC_T - 4, y0 = c.ty * SC_T - g.pt;
+      const int r3 = lane / 17, u = lane - 17 * r3;
+      const int xu = xa + (4 * u) / 3;  // first pixel the unit touches (units never straddle the edge)
+      const bool xok = valid && lane < 51 && xu >= 0 && xu < g.W;
+      const unsigned rstride = (unsigned)(g.W * CIN * 4);
+      const unsigned lo = (unsigned)(((c.b * g.H + y0) * g.W + xa) * CIN * 4 + 16 * u);
+#pragma unroll
+      for (int q = 0; q < NDMA; ++q) {
+        const int j = wid + 4 * q < 6 ? wid + 4 * q : 6, r = 3 * j + r3;  // (j = 6: waves 2, 3's dummy, rows 18-20)
+        const bool ok = xok && r < SC_P && (unsigned)(y0 + r) < (unsigned)g.H;
+        if (lane < 51)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rsIn, (__attribute__((address_space(3))) void*)&patch[buf][3 * j * RS],
+                                                   16, (int)(ok ? lo + (unsigned)r * rstride : OOB_OFF), 0, 0, 0);
+      }
+      return;
+    }
     const int x0 = c.tx * SC_T - g.pl, y0 = c.ty * SC_T - g.pt;
     const int px = x0 + lane / CIN;
     const bool xok = valid && (unsigned)px < (unsigned)g.W;
@@ -295,11 +323,11 @@ conv0_packed_pool_kernel(const float* __restrict__ in, const float* __restrict__
   int buf = 0;
   for (int it = 0; t < ntiles; t += G, ++it) {
     if (it == 0)
-      wait_vmcnt<C0_ROWS_PER_WAVE>();
+      wait_vmcnt<NDMA>();
     else if (it == 1)
-      wait_vmcnt<C0_ROWS_PER_WAVE + ST>();
+      wait_vmcnt<NDMA + ST>();
     else
-      wait_vmcnt<C0_ROWS_PER_WAVE + 2 * ST>();
+      wait_vmcnt<NDMA + 2 * ST>();
     raw_barrier();  // every wave's rows of `buf` landed; every wave finished reading tile t-1's buffer
     // tile t+2 into the buffer tile t-1 used (dummy past the end: the count stays fixed)
     const int t2 = t + 2 * G;
@@ -379,7 +407,10 @@ static int launch_conv0(const float* in, const float* w, OutT* out, const Direct
   // the next tile's patch prefetched into registers during the current tile's MFMAs)
   const int nt = (int)blocks;
   const char* eg = getenv("DNN_HIP_C0_GRID");  // (tuning experiments: workgroups of the launch)
-  const int gmax = eg && atoi(eg) > 0 ? atoi(eg) : 4096;  // (fp16 conv0 at batch 64: 2048 89.4 us, 4096 85.1, 8192 87.2)
+  // (fp16 conv0 at batch 64: 2048 89.4 us, 4096 85.1, 8192 87.2; the fp32 form of this kernel is only
+  // the fallback of launch_conv0_mfma -- YOLO's fp32 conv0 runs conv0_packed_pool_kernel -- and
+  // keeps its round-4 cap of 2048)
+  const int gmax = eg && atoi(eg) > 0 ? atoi(eg) : F16 ? 4096 : 2048;
   const dim3 grid((unsigned)(nt < gmax ? nt : gmax));
   switch (cin) {
     case 1: hipLaunchKernelGGL((conv0_mfma_pool_kernel<1, F16, OutT>), grid, dim3(256), 0, s, in, w, out, g, tilesX, tilesY, nt, epi); break;
@@ -432,20 +463,33 @@ int launch_conv0_mfma(const float* in, const float* w, float* out, const DirectG
     v = 4 * (v < 8 ? v : 8);
     return cache[dev] = (long long)v * device_cu_count();
   };
-#define C0P(FL_, EV_)                                                                                           \
+#define C0P(FL_, EV_, D16_)                                                                                     \
   do {                                                                                                           \
     static long long cache[64] = {};                                                                             \
-    const long long slots = slots_of(reinterpret_cast<const void*>(conv0_packed_pool_kernel<3, FL_, EV_>), cache); \
+    const long long slots =                                                                                      \
+        slots_of(reinterpret_cast<const void*>(conv0_packed_pool_kernel<3, FL_, EV_, D16_>), cache);             \
     const unsigned grid = (unsigned)(blocks < slots ? blocks : slots);                                           \
-    hipLaunchKernelGGL((conv0_packed_pool_kernel<3, FL_, EV_>), dim3(grid), dim3(256), 0, s, in, w, out, g, tilesX, \
-                       tilesY, (int)blocks, zero, epi, mags);                                                    \
+    hipLaunchKernelGGL((conv0_packed_pool_kernel<3, FL_, EV_, D16_>), dim3(grid), dim3(256), 0, s, in, w, out, g, \
+                       tilesX, tilesY, (int)blocks, zero, epi, mags);                                            \
   } while (0)
+  // 16-B patch-row DMAs (D16) where units cannot straddle the frame edge: W % 4 == 0, one pixel of
+  // left padding (SAME 3x3).  DNN_HIP_C0_D16=0 (read per launch, A/B): the 4-B row DMAs; same bits
+  const bool d16 = g.W % 4 == 0 && g.pl == 1 && !getenv_flag_off("DNN_HIP_C0_D16");
   if (epi.flags == YOLO && even) {
-    C0P(YOLO, true);
+    if (d16)
+      C0P(YOLO, true, true);
+    else
+      C0P(YOLO, true, false);
   } else if (even) {
-    C0P(-1, true);
+    if (d16)
+      C0P(-1, true, true);
+    else
+      C0P(-1, true, false);
   } else {
-    C0P(-1, false);
+    if (d16)
+      C0P(-1, false, true);
+    else
+      C0P(-1, false, false);
   }
 #undef C0P
   hipError_t e = hipGetLastError();

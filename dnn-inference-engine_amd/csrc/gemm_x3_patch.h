@@ -775,10 +775,11 @@ conv3x3_x3_c16p_kernel(const float* __restrict__ in, const bf16_bits* __restrict
 // pipes ~57 % busy).  Here ONE workgroup per CU runs two teams of 4 waves (one wave of each team
 // per SIMD) over a contiguous range of the CU's tiles (team A the even ones, team B the odd ones)
 // in lock step, as conv3x3_x3_pp_kernel: every step ends at a workgroup barrier; in each step one
-// team runs its MFMAs (at issue priority 1) while the other runs its store step -- wait for its
-// next tile's fp32 patch (loaded into registers one step earlier), split it into the team's patch
-// area, issue the loads of the tile after it, then fold, pool + epilogue through the stage and
-// store the pooled split planes of the tile it just computed.  LDS: the 30 KB of weights once (both
+// team runs its MFMAs (at issue priority 1) while the other runs its store step -- issue the loads
+// of its next tile's fp32 patch into registers, fold, pool + epilogue through the stage and store
+// the pooled split planes of the tile it just computed, then split the next patch into the team's
+// patch area (the loads' latency under the epilogue; no staging registers live in the MFMA step,
+// which reads the next K step's B fragments during the current one instead).  LDS: the 30 KB of weights once (both
 // teams), one split patch per team (48 KB each), one stage area (the store steps never overlap),
 // 150 KB in all.  Products, order and epilogue per output are conv3x3_x3_c16p_kernel<true, true>'s:
 // the same bits (tested).
@@ -913,12 +914,10 @@ conv3x3_x3_c16pp_kernel(const float* __restrict__ in, const bf16_bits* __restric
   const int hoff = (PW2 + 1) * PB + 8 * fq;
   const int hb = (fr + 16 * (fq >> 1)) * 16 + 8 * (fq & 1);
 
-  // prologue: each team's first patch split into its area, its second tile's loads in flight
+  // prologue: each team's first patch split into its area
   if (nmine > 0) {
     load_tile(0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     split_tile();
-    if (nmine > 1) load_tile(1);
   }
   __syncthreads();  // weights, epl, both teams' first patches
 
@@ -948,36 +947,48 @@ conv3x3_x3_c16pp_kernel(const float* __restrict__ in, const bf16_bits* __restric
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = accc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      // (unlike the two-workgroup kernel, no other MFMA wave shares the SIMD to cover a stall, so the
+      // next step's B fragments are read during this step -- two sets -- and the K = 16 step's A
+      // fragments one block ahead)
       constexpr int NSF = NS - 1;  // full 16x16x32 steps; tap 8 alone on 16x16x16 below
-      bf16x8 af[2][3], bq[3][2];
+      bf16x8 af[2][3], bq[2][3][2];
+      s16x4 hbq[3][2];
       frag(0, toff(0), af[0]);
+      bfrag(0, bq[0]);
 #pragma unroll
       for (int s = 0; s < NSF; ++s) {
         const int off = toff(s), off_next = toff(s + 1 < NSF ? s + 1 : s);
-        bfrag(s, bq);
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
           const int cur = (s * TM + i) & 1, nxt = cur ^ 1;
+          if (i == 0 && s + 1 < NSF) bfrag(s + 1, bq[(s + 1) & 1]);
+          if (i == 0 && s + 1 == NSF) {
+#pragma unroll
+            for (int p = 0; p < 3; ++p)
+#pragma unroll
+              for (int j = 0; j < 2; ++j)
+                hbq[p][j] = *reinterpret_cast<const s16x4*>(smem + (j * NS * 3 + 4 * 3 + p) * 1024 + hb);
+          }
           if (i + 1 < TM)
             frag(i + 1, off, af[nxt]);
           else if (s + 1 < NSF)
             frag(0, off_next, af[nxt]);
 #pragma unroll
-          for (int jb = 0; jb < 2; ++jb) x3_step<true>(acc[i][jb], accc[i][jb], af[cur], bq, jb);
+          for (int jb = 0; jb < 2; ++jb) x3_step<true>(acc[i][jb], accc[i][jb], af[cur], bq[s & 1], jb);
           __builtin_amdgcn_sched_barrier(0);
         }
       }
-      s16x4 hbq[3][2];
-#pragma unroll
-      for (int p = 0; p < 3; ++p)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) hbq[p][j] = *reinterpret_cast<const s16x4*>(smem + (j * NS * 3 + 4 * 3 + p) * 1024 + hb);
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
+      s16x4 ha[2][3];
+      auto hfrag = [&](int i, s16x4 (&a)[3]) {
         const int pr = prow(i);
-        s16x4 a[3];
 #pragma unroll
         for (int p = 0; p < 3; ++p) a[p] = *reinterpret_cast<const s16x4*>(patch + pr + hoff + 32 * p);
+      };
+      hfrag(0, ha[0]);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        if (i + 1 < TM) hfrag(i + 1, ha[(i + 1) & 1]);
+        const s16x4(&a)[3] = ha[i & 1];
 #pragma unroll
         for (int jb = 0; jb < 2; ++jb) {
           f32x4 c = accc[i][jb];
@@ -997,13 +1008,10 @@ conv3x3_x3_c16pp_kernel(const float* __restrict__ in, const bf16_bits* __restric
     C16PP_MARK(0)
     __syncthreads();  // the team's patch is read by all its waves (and the other team's store step is done)
     C16PP_MARK(3)
-    {  // store step: tile k + 1's patch in, tile k + 2's loads out, tile k's pooled split planes out
-      if (k + 1 < nmine) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile k + 1's fp32 patch (and tile k - 1's stores)
-        split_tile();
-        if (k + 2 < nmine) load_tile(k + 2);
-      }
-      C16PP_MARK(1)
+    {  // store step: tile k + 1's fp32 patch loaded, tile k's pooled split planes out, tile k + 1 split
+      // into the team's patch area (the loads in flight under the epilogue and stores; the
+      // compiler's wait before the split counts the stores issued after them)
+      if (k + 1 < nmine) load_tile(k + 1);
       x3_fold(acc, accc);
       int b, y0, x0;
       tile_of(k, b, y0, x0);
@@ -1020,8 +1028,10 @@ conv3x3_x3_c16pp_kernel(const float* __restrict__ in, const bf16_bits* __restric
         return (py >= g.PH || px >= g.PW) ? -1 : (b * (g.PH + 2) + py + 1) * (g.PW + 2) + px + 1;
       };
       x3_pool_split_store_f<TM>(stgp, orow_of, NO, 4 * wm * TM, out_split, 96, 0, lane);
-      wait_lgkm0();  // the split patch written, the stage read
       C16PP_MARK(2)
+      if (k + 1 < nmine) split_tile();
+      wait_lgkm0();  // the split patch written, the stage read
+      C16PP_MARK(1)
     }
     __syncthreads();
     C16PP_MARK(3)

@@ -354,9 +354,11 @@ def test_patch_conv_pool_bit_exact(monkeypatch, case):
     assert R.normwise_err(outs["patch"], _oracle_chain(x, k, **kw)) < LAYER_TOL
 
 
-@pytest.mark.parametrize("hw", [(40, 38), (13, 13), (17, 22)])
+@pytest.mark.parametrize("hw", [(40, 38), (13, 13), (17, 22), (40, 36), (18, 52), (33, 20)])
 def test_direct_conv0_pool_vs_oracle(monkeypatch, hw):
-    """conv0's direct kernel (3 input channels, pool fused) vs the oracle and vs the explicit path."""
+    """conv0's direct kernel (3 input channels, pool fused) vs the oracle and vs the explicit path;
+    where W % 4 == 0 (16-B patch-row DMAs, D16) also equal bit for bit to the 4-B row DMAs
+    (DNN_HIP_C0_D16=0): tiles past the right / bottom edge, frames narrower than two tiles."""
     H, W = hw
     rng = np.random.default_rng(H * W)
     x = rng.uniform(0, 1, (3, H, W, 3)).astype(np.float32)
@@ -371,6 +373,11 @@ def test_direct_conv0_pool_vs_oracle(monkeypatch, hw):
     ref = _oracle_chain(x, k, **kw)
     assert y.shape == ref.shape
     assert R.normwise_err(y, ref) < LAYER_TOL
+    assert np.array_equal(eng.run(x), y)
+    if W % 4 == 0:
+        monkeypatch.setenv("DNN_HIP_C0_D16", "0")
+        assert np.array_equal(eng.run(x), y)
+        monkeypatch.delenv("DNN_HIP_C0_D16")
     monkeypatch.setenv("DNN_HIP_FUSE", "0")
     y0 = dnn_hip.DnnInferenceEngine(_chain(x.shape, k, **kw), False).run(x)
     assert R.normwise_err(y, y0) < LAYER_TOL
