@@ -235,7 +235,17 @@ def latency_b1(dnn_hip, yolo_graph, ws, dev, iters=200, latency=True):
         e1.record(s)
     s.synchronize()
     out["graph_device_ms"] = round(e0.elapsed_time(e1) / 50, 4)
+    # the same for back-to-back eager forwards: on this runtime a graph replay's device time is a
+    # few us above eager issue (tools/lat_env.py), so both are reported
+    with torch.cuda.stream(s):
+        e0.record(s)
+        for _ in range(50):
+            p1.run_device(1, x.data_ptr(), y.data_ptr(), sp)
+        e1.record(s)
+    s.synchronize()
+    out["eager_device_ms"] = round(e0.elapsed_time(e1) / 50, 4)
     out["images_per_s_graph"] = round(1e3 / out["graph_ms"], 1)
+    out["images_per_s_eager"] = round(1e3 / out["eager_ms"], 1)
     p1.timing_begin(20)
     for _ in range(20):
         p1.run_device(1, x.data_ptr(), y.data_ptr(), sp)
