@@ -608,6 +608,7 @@ def main():
     # the step ~1 %); --kernels: around every kernel, for the per-kernel table.  Two clock-stamp
     # launches on the run stream bracket the timed forwards (the shader clock over the region)
     clk = torch.zeros((2, CLOCK_WGS, 4), dtype=torch.int64, device=dev)
+    dnn_hip.clock_stamp(clk[0].data_ptr(), CLOCK_WGS, stream)  # (first launch outside the timed region)
     plan.timing_begin(args.steps, only=None if args.kernels else DOMINANT)
     torch.cuda.synchronize()
     if distributed:

@@ -512,7 +512,7 @@ def lower_graph(g):
 
 def clock_stamp(dev_ptr, nwg, stream_ptr, lib=None):
     """Launch the clock-stamp kernel (dnn_clock_stamp): nwg workgroups, 4 uint64 each at dev_ptr."""
-    lib = lib or load_library()
+    lib = lib or mylib
     _check(lib.dnn_clock_stamp(ctypes.c_void_p(stream_ptr), ctypes.c_void_p(dev_ptr), int(nwg)), "clock_stamp", lib)
 
 
