@@ -219,18 +219,19 @@ constexpr int C0_ROWS_PER_WAVE = 5;  // 20 row DMAs per tile over 4 waves (rows 
 // floats: the 18 patch pixels start at float 9); with W % 4 == 0 and x0 % 16 == 0 a 16-B unit never
 // straddles the frame edge, so out-of-frame units take the out-of-range offset as whole units.  Two
 // DMA instructions per wave and tile (rows 3 j .. 3 j + 2 for j = wid, wid + 4; waves 2 and 3's
-// second is a dummy of zeros into spare rows 18-20) instead of five 4-B row DMAs.
-template <int CIN, int FL = -1, bool EVEN = false, bool D16 = false>
-__global__ void __launch_bounds__(256, 7)  // 7 waves per SIMD (<= 72 registers): latency-bound, occupancy pays
+// second repeats triplet 4 / 5) instead of five 4-B row DMAs.
+template <int CIN, int FL = -1, bool EVEN = false, bool D16 = false, int NB = 3>
+__global__ void __launch_bounds__(256, D16 ? 8 : 7)  // 7-8 waves per SIMD (<= 64-72 registers): latency-bound, occupancy pays
 conv0_packed_pool_kernel(const float* __restrict__ in, const float* __restrict__ w, float* __restrict__ out,
                          DirectGeom g, int tilesX, int tilesY, int ntiles, const float* __restrict__ zero,
                          EpiParams epi, uint4 mags) {  // mags: magic numbers of tilesX, tilesY (div_magic)
   constexpr int K = 9 * CIN, KS = (K + 3) / 4, RW = SC_P * CIN, RS = D16 ? 68 : C0_RS;
   constexpr int NDMA = D16 ? 2 : C0_ROWS_PER_WAVE;  // DMA instructions per wave and tile
-  constexpr int PROWS = D16 ? 21 : 4 * C0_ROWS_PER_WAVE;  // LDS rows per buffer (D16: 18 + the dummies' 3)
+  constexpr int PROWS = D16 ? 18 : 4 * C0_ROWS_PER_WAVE;  // LDS rows per buffer
   constexpr int X0F = D16 ? 3 * CIN : 0;  // float offset of patch pixel 0 in an LDS row
   static_assert(RW <= RS && RW <= 64 && (!D16 || CIN == 3), "patch row");
-  __shared__ __attribute__((aligned(16))) float patch[3][PROWS * RS];  // triple buffer
+  static_assert(NB >= 3 && NB <= 5, "patch ring");
+  __shared__ __attribute__((aligned(16))) float patch[NB][PROWS * RS];  // ring of NB buffers
   __shared__ __attribute__((aligned(16))) float stage[4][2][8][16];  // per wave: 2 window rows x 8 windows x 16 ch
 
   const int lane = threadIdx.x & 63;
@@ -283,7 +284,9 @@ conv0_packed_pool_kernel(const float* __restrict__ in, const float* __restrict__
       const unsigned lo = (unsigned)(((c.b * g.H + y0) * g.W + xa) * CIN * 4 + 16 * u);
 #pragma unroll
       for (int q = 0; q < NDMA; ++q) {
-        const int j = wid + 4 * q < 6 ? wid + 4 * q : 6, r = 3 * j + r3;  // (j = 6: waves 2, 3's dummy, rows 18-20)
+        // (waves 2 and 3's second instruction repeats triplet 4 / 5 of waves 0 and 1: the same bytes
+        // into the same LDS rows, so no spare rows; a fixed DMA count per wave)
+        const int j = wid + 4 * q < 6 ? wid + 4 * q : wid + 2, r = 3 * j + r3;
         const bool ok = xok && r < SC_P && (unsigned)(y0 + r) < (unsigned)g.H;
         if (lane < 51)
           __builtin_amdgcn_raw_ptr_buffer_load_lds(rsIn, (__attribute__((address_space(3))) void*)&patch[buf][3 * j * RS],
@@ -307,32 +310,39 @@ conv0_packed_pool_kernel(const float* __restrict__ in, const float* __restrict__
     }
   };
 
-  // Two tiles in flight: tile t's rows were issued two iterations ago.  Per wave and tile the
-  // VMEM stream is C0_ROWS_PER_WAVE DMAs then ST stores, so when tile t is consumed the ops
-  // issued after its DMAs are at most: stores(t-2), DMAs(t+1), stores(t-1).
+  // NB - 1 tiles in flight: tile t's rows were issued NB - 1 iterations ago.  Per wave and tile the
+  // VMEM stream is NDMA DMAs then ST stores, so when tile t is consumed the ops issued after its
+  // DMAs are: stores(t - NB + 1), then DMAs(t + i) and stores(t - NB + 1 + i) for i = 1 .. NB - 2
+  // -- (NB - 2) NDMA + (NB - 1) ST -- and in the first iterations j < NB - 1 the prologue's later
+  // DMAs and the j stores since: (NB - 2) NDMA + j ST.  (NB = 3: stores(t-2), DMAs(t+1), stores(t-1).)
   constexpr int ST = 1;
   const auto orsrc = out_rsrc(out, (unsigned)((size_t)g.B * g.PH * g.PW * 16 * sizeof(float)));
   const int G = gridDim.x;
   int t = blockIdx.x;
-  Tile cur = coords(t < ntiles ? t : 0);
-  Tile nxt = coords(t + G < ntiles ? t + G : 0);
+  Tile q[NB - 1];  // tiles t, t + G, ..., t + (NB - 2) G
+#pragma unroll
+  for (int j = 0; j < NB - 1; ++j) q[j] = coords(t + j * G < ntiles ? t + j * G : 0);
   if (t < ntiles) {
-    issue(cur, true, 0);
-    issue(nxt, t + G < ntiles, 1);
+#pragma unroll
+    for (int j = 0; j < NB - 1; ++j) issue(q[j], t + j * G < ntiles, j);
   }
   int buf = 0;
   for (int it = 0; t < ntiles; t += G, ++it) {
     if (it == 0)
-      wait_vmcnt<NDMA>();
+      wait_vmcnt<(NB - 2) * NDMA>();
     else if (it == 1)
-      wait_vmcnt<NDMA + ST>();
+      wait_vmcnt<(NB - 2) * NDMA + ST>();
+    else if (NB > 3 && it == 2)
+      wait_vmcnt<(NB - 2) * NDMA + 2 * ST>();
+    else if (NB > 4 && it == 3)
+      wait_vmcnt<(NB - 2) * NDMA + 3 * ST>();
     else
-      wait_vmcnt<NDMA + 2 * ST>();
+      wait_vmcnt<(NB - 2) * NDMA + (NB - 1) * ST>();
     raw_barrier();  // every wave's rows of `buf` landed; every wave finished reading tile t-1's buffer
-    // tile t+2 into the buffer tile t-1 used (dummy past the end: the count stays fixed)
-    const int t2 = t + 2 * G;
+    // tile t + (NB - 1) G into the buffer tile t - 1 used (dummy past the end: the count stays fixed)
+    const int t2 = t + (NB - 1) * G;
     const Tile nn = coords(t2 < ntiles ? t2 : 0);
-    if (!(C0DIAG & 1)) issue(nn, t2 < ntiles, buf == 0 ? 2 : buf - 1);
+    if (!(C0DIAG & 1)) issue(nn, t2 < ntiles, buf == 0 ? NB - 1 : buf - 1);
     const float* P = patch[buf];
 
     f32x4 acc[4];
@@ -350,9 +360,11 @@ conv0_packed_pool_kernel(const float* __restrict__ in, const float* __restrict__
       }
     }
 
+    const Tile cur = q[0];
     const int b = cur.b, y0 = cur.ty * SC_T, x0 = cur.tx * SC_T;
-    cur = nxt;
-    nxt = nn;
+#pragma unroll
+    for (int j = 0; j + 1 < NB - 1; ++j) q[j] = q[j + 1];
+    q[NB - 2] = nn;
     // pool + epilogue into the wave's LDS stage (the four windows' divisions behind one
     // wave-uniform check: pool_epilogue_batch), then 16-B coalesced stores
     f32x4 pv[4][1];
@@ -384,7 +396,7 @@ conv0_packed_pool_kernel(const float* __restrict__ in, const float* __restrict__
       store16(orsrc, off, *reinterpret_cast<const f32x4*>(&stage[wid][lr][0][0] + f));
     }
     wait_lgkm0();
-    buf = buf == 2 ? 0 : buf + 1;
+    buf = buf == NB - 1 ? 0 : buf + 1;
   }
   wait_vmcnt<0>();  // no LDS-DMA may land after the workgroup exits
 }
@@ -463,15 +475,19 @@ int launch_conv0_mfma(const float* in, const float* w, float* out, const DirectG
     v = 4 * (v < 8 ? v : 8);
     return cache[dev] = (long long)v * device_cu_count();
   };
-#define C0P(FL_, EV_, D16_)                                                                                     \
+#define C0PN(FL_, EV_, D16_, NB_)                                                                               \
   do {                                                                                                           \
     static long long cache[64] = {};                                                                             \
     const long long slots =                                                                                      \
-        slots_of(reinterpret_cast<const void*>(conv0_packed_pool_kernel<3, FL_, EV_, D16_>), cache);             \
+        slots_of(reinterpret_cast<const void*>(conv0_packed_pool_kernel<3, FL_, EV_, D16_, NB_>), cache);        \
     const unsigned grid = (unsigned)(blocks < slots ? blocks : slots);                                           \
-    hipLaunchKernelGGL((conv0_packed_pool_kernel<3, FL_, EV_, D16_>), dim3(grid), dim3(256), 0, s, in, w, out, g, \
-                       tilesX, tilesY, (int)blocks, zero, epi, mags);                                            \
+    hipLaunchKernelGGL((conv0_packed_pool_kernel<3, FL_, EV_, D16_, NB_>), dim3(grid), dim3(256), 0, s, in, w,    \
+                       out, g, tilesX, tilesY, (int)blocks, zero, epi, mags);                                    \
   } while (0)
+  // (patch ring depth: 4 and 5 buffers measured slower at batch 64 -- 0.1242 / 0.1353 / 0.1424 ms for
+  // 3 / 4 / 5, same process: the LDS they take costs a workgroup per CU each, and occupancy hides
+  // more of the DMA latency than the deeper ring)
+#define C0P(FL_, EV_, D16_) C0PN(FL_, EV_, D16_, 3)
   // 16-B patch-row DMAs (D16) where units cannot straddle the frame edge: W % 4 == 0, one pixel of
   // left padding (SAME 3x3).  DNN_HIP_C0_D16=0 (read per launch, A/B): the 4-B row DMAs; same bits
   const bool d16 = g.W % 4 == 0 && g.pl == 1 && !getenv_flag_off("DNN_HIP_C0_D16");
@@ -492,6 +508,7 @@ int launch_conv0_mfma(const float* in, const float* w, float* out, const DirectG
       C0P(-1, false, false);
   }
 #undef C0P
+#undef C0PN
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
     set_error("launch conv0_packed: %s", hipGetErrorString(e));
