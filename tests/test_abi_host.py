@@ -442,3 +442,25 @@ def test_fp16_patch_kernel_only_where_its_patch_fits(hw, want_patch):
         assert ("mode=patch16" in conv[0]) == want_patch, conv
     finally:
         lib.dnn_plan_destroy(h)
+
+
+def test_sclk_from_stamps_host_only():
+    """The bench's shader-clock arithmetic (dnn_hip.sclk_from_stamps): per XCD the medians of the
+    two counters over its workgroups, d(memtime) / d(memrealtime) x 100 MHz; XCDs present in only
+    one of the two stamp sets are left out."""
+    nwg = 64
+    start = np.zeros((nwg, 4), dtype=np.int64)
+    end = np.zeros((nwg, 4), dtype=np.int64)
+    for w in range(nwg):
+        x = w % 8
+        ghz = 1.8 + 0.05 * x
+        start[w] = [1_000_000 + 37 * w, 500_000 + w, x, 0]
+        end[w] = [start[w, 0] + int(round(ghz * 1e4)), start[w, 1] + 1000, x, 0]  # 10 us at 100 MHz
+    c = dnn_hip.sclk_from_stamps(start, end)
+    assert set(c["per_xcd"]) == set(range(8))
+    for x in range(8):
+        assert abs(c["per_xcd"][x] - (1.8 + 0.05 * x)) < 1e-9
+    assert abs(c["min"] - 1.8) < 1e-9 and abs(c["max"] - 2.15) < 1e-9
+    assert abs(c["window_us"] - 10.0) < 1e-9
+    end[:, 2] = 9  # no XCD in common
+    assert dnn_hip.sclk_from_stamps(start, end) is None

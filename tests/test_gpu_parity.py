@@ -458,6 +458,49 @@ def test_yolo_batch64_golden_indices_and_batch_invariance(yolo_weights, golden_f
     assert plan.run_host(x[:0]).shape == (0, 13, 13, 125)
 
 
+def test_clock_stamps_and_plan_clock_api(yolo_b1):
+    """dnn_clock_stamp (csrc/clock.hip) and the plan's clock stamps around one kernel
+    (dnn_plan_clock_begin / end): per-XCD shader clocks in a plausible range, stamps monotone,
+    every XCD sampled by one workgroup per CU, stamping stopped after the requested runs, the
+    forward's output unchanged by the stamp launches, and the API's error returns."""
+    import torch
+    plan = yolo_b1.plan()
+    x = synth.frame(1)
+    y0 = plan.run_host(x)
+    dev = torch.device("cuda", 0)
+    nwg = 256
+    s = torch.cuda.Stream(dev)
+    buf = torch.zeros((2, nwg, 4), dtype=torch.int64, device=dev)
+    dnn_hip.clock_stamp(buf[0].data_ptr(), nwg, s.cuda_stream)
+    t = torch.empty((1 << 24,), device=dev)
+    with torch.cuda.stream(s):
+        for _ in range(20):
+            t.mul_(1.0001)
+    dnn_hip.clock_stamp(buf[1].data_ptr(), nwg, s.cuda_stream)
+    s.synchronize()
+    a, b = buf[0].cpu().numpy(), buf[1].cpu().numpy()
+    assert np.all(b[:, 1] > a[:, 1]) and np.all(b[:, 0] > a[:, 0])
+    c = dnn_hip.sclk_from_stamps(a, b)
+    assert c is not None and 0.3 < c["min"] <= c["mean"] <= c["max"] < 3.0, c
+    assert len(c["per_xcd"]) >= 1 and all(0 <= int(k) < 16 for k in c["per_xcd"])
+    runs = 3
+    kb = torch.zeros((runs + 2, 2, nwg, 4), dtype=torch.int64, device=dev)
+    plan.clock_begin("conv7.gemm", kb.data_ptr(), runs, nwg)
+    for _ in range(runs + 2):  # more runs than slots: stamping stops at `runs`
+        y = plan.run_host(x)
+    assert plan.clock_end() == runs
+    assert np.array_equal(y, y0)
+    k = kb.cpu().numpy()
+    for i in range(runs):
+        ci = dnn_hip.sclk_from_stamps(k[i, 0], k[i, 1])
+        assert ci is not None and 0.3 < ci["mean"] < 3.0, ci
+    assert not k[runs:].any()
+    with pytest.raises(dnn_hip.DnnHipError):
+        plan.clock_end()  # not active
+    with pytest.raises(dnn_hip.DnnHipError):
+        dnn_hip.clock_stamp(kb.data_ptr(), 0, s.cuda_stream)
+
+
 def test_plan_timing_api(yolo_b1):
     plan = yolo_b1.plan()
     x = synth.frame(1)
