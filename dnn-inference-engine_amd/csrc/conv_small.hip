@@ -221,7 +221,10 @@ constexpr int C0_ROWS_PER_WAVE = 5;  // 20 row DMAs per tile over 4 waves (rows 
 // DMA instructions per wave and tile (rows 3 j .. 3 j + 2 for j = wid, wid + 4; waves 2 and 3's
 // second repeats triplet 4 / 5) instead of five 4-B row DMAs.
 template <int CIN, int FL = -1, bool EVEN = false, bool D16 = false, int NB = 3>
-__global__ void __launch_bounds__(256, D16 ? 8 : 7)  // 7-8 waves per SIMD (<= 64-72 registers): latency-bound, occupancy pays
+#ifndef C0_D16_OCC
+#define C0_D16_OCC 8
+#endif
+__global__ void __launch_bounds__(256, D16 ? C0_D16_OCC : 7)  // 7-8 waves per SIMD (<= 64-72 registers): latency-bound, occupancy pays
 conv0_packed_pool_kernel(const float* __restrict__ in, const float* __restrict__ w, float* __restrict__ out,
                          DirectGeom g, int tilesX, int tilesY, int ntiles, const float* __restrict__ zero,
                          EpiParams epi, uint4 mags) {  // mags: magic numbers of tilesX, tilesY (div_magic)
