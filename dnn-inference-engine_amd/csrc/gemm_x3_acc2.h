@@ -401,13 +401,13 @@ conv3x3_x3_acc2_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __rest
           q[1][e] = w1;
           q[2][e] = w2;
         }
-        bf16_bits* d = out_split + (size_t)o * (3 * N) + (n0 >> 5) * 96 + c8;
+        const size_t d = (size_t)o * (3 * N) + (n0 >> 5) * 96 + c8;  // (halves)
 #pragma unroll
-        for (int pc = 0; pc < 3; ++pc) *reinterpret_cast<u32x4*>(d + 32 * pc) = q[pc];
+        for (int pc = 0; pc < 3; ++pc) store16_at(out_split, 2 * (d + 32 * pc), q[pc]);
       } else {
-        float* d = out + ((size_t)(g.out_mode == 2 ? split * M : 0) + o) * N + n0 + c8;
-        *reinterpret_cast<f32x4*>(d) = lo;
-        *reinterpret_cast<f32x4*>(d + 4) = hi;
+        const size_t d = ((size_t)(g.out_mode == 2 ? split * M : 0) + o) * N + n0 + c8;  // (floats)
+        store16_at(out, 4 * d, __builtin_bit_cast(u32x4, lo));
+        store16_at(out, 4 * d + 16, __builtin_bit_cast(u32x4, hi));
       }
     }
   });

@@ -209,9 +209,9 @@ conv3x3_x3_img_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __restr
     pool_epilogue_batch<FL>(win, cb, cm, cs, cgm, epi.flags, [&](int, int c, float e) { o[c] = e; });
     const int n = nb * 128 + c8;
     if (out_split == nullptr) {  // fp32 [B][H][W][N] (the plan's last layer)
-      float* d = out + ((size_t)b * HW + pix) * N + n;
-      *reinterpret_cast<f32x4*>(d) = f32x4{o[0], o[1], o[2], o[3]};
-      *reinterpret_cast<f32x4*>(d + 4) = f32x4{o[4], o[5], o[6], o[7]};
+      const size_t d = ((size_t)b * HW + pix) * N + n;  // (floats)
+      store16_at(out, 4 * d, __builtin_bit_cast(u32x4, f32x4{o[0], o[1], o[2], o[3]}));
+      store16_at(out, 4 * d + 16, __builtin_bit_cast(u32x4, f32x4{o[4], o[5], o[6], o[7]}));
       continue;
     }
     bool ok = true;
@@ -227,9 +227,9 @@ conv3x3_x3_img_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __restr
       q[1][e] = w1;
       q[2][e] = w2;
     }
-    bf16_bits* d = out_split + ((size_t)b * PR + (y + 1) * WP + x + 1) * (3 * (size_t)N) + (n >> 5) * 96 + (n & 31);
+    const size_t d = ((size_t)b * PR + (y + 1) * WP + x + 1) * (3 * (size_t)N) + (n >> 5) * 96 + (n & 31);
 #pragma unroll
-    for (int pc = 0; pc < 3; ++pc) *reinterpret_cast<u32x4*>(d + 32 * pc) = q[pc];
+    for (int pc = 0; pc < 3; ++pc) store16_at(out_split, 2 * (d + 32 * pc), q[pc]);
   }
   IMG_STAMP(6, __builtin_amdgcn_s_memtime())
   IMG_STAMP(7, __builtin_amdgcn_s_memrealtime())

@@ -179,9 +179,9 @@ __device__ __forceinline__ void x3_pool_split_store_f(const float* stg, OF&& oro
       q[1][e] = w1;
       q[2][e] = w2;
     }
-    bf16_bits* d = out_split + (size_t)o * n3 + col0 + c8;
+    const size_t d = (size_t)o * n3 + col0 + c8;  // (halves)
 #pragma unroll
-    for (int pc = 0; pc < 3; ++pc) *reinterpret_cast<u32x4*>(d + 32 * pc) = q[pc];
+    for (int pc = 0; pc < 3; ++pc) store16_at(out_split, 2 * (d + 32 * pc), q[pc]);
   }
 }
 template <int TM>
