@@ -635,8 +635,8 @@ conv1_patch_f16_kernel(const half_t* __restrict__ in, const half_t* __restrict__
       const int wy = (y0 >> 1) + 2 * wid + (wl >> 3), wx = (x0 >> 1) + (wl & 7);
       const h8v v = *reinterpret_cast<const h8v*>(st + wl * SP + 8 * cg);
       if (wy < g.PH && wx < g.PW)
-        *reinterpret_cast<h8v*>(out + (((size_t)b * (g.PH + 2 * opad) + wy + opad) * (g.PW + 2 * opad) + wx + opad) * 32 +
-                                8 * cg) = v;
+        store16_at(out, 2 * ((((size_t)b * (g.PH + 2 * opad) + wy + opad) * (g.PW + 2 * opad) + wx + opad) * 32 + 8 * cg),
+                   __builtin_bit_cast(u32x4, v));
     }
 #else
 #pragma unroll

@@ -234,7 +234,7 @@ conv3x3_f16_acc_kernel(const half_t* __restrict__ in, const half_t* __restrict__
         v[e] = (half_t)lo[e];
         v[e + 4] = (half_t)hi[e];
       }
-      *reinterpret_cast<h8v*>(out + (size_t)o * N + n0 + c8) = v;
+      store16_at(out, 2 * ((size_t)o * N + n0 + c8), __builtin_bit_cast(u32x4, v));
     }
   });
 }

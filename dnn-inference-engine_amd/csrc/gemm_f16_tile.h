@@ -284,7 +284,7 @@ conv3x3_f16_tile_kernel(const half_t* __restrict__ in, const half_t* __restrict_
           if (x + 1 < TW) v = __builtin_elementwise_max(v, sp[(TW + 1) * (SW / 8)]);
         }
         const size_t o = g.out_padded ? (size_t)(b * (TH + 2) + y + 1) * (TW + 2) + x + 1 : (size_t)(b * TH + y) * TW + x;
-        *reinterpret_cast<h8v*>(out + o * N + ncol0 + 8 * gq) = v;
+        store16_at(out, 2 * (o * N + ncol0 + 8 * gq), __builtin_bit_cast(u32x4, v));
       }
       wait_lgkm0();
       __syncthreads();  // the stage read before pair q + 2's DMA reuses the buffer
@@ -316,7 +316,7 @@ conv3x3_f16_tile_kernel(const half_t* __restrict__ in, const half_t* __restrict_
           if (py < g.PH && px < g.PW) {
             const size_t o = g.out_padded ? (size_t)(b * (g.PH + 2) + py + 1) * (g.PW + 2) + px + 1
                                           : (size_t)(b * g.PH + py) * g.PW + px;
-            *reinterpret_cast<h8v*>(out + o * N + n0 + 8 * gq) = *reinterpret_cast<const h8v*>(st + wl * SROW + 8 * gq);
+            store16_at(out, 2 * (o * N + n0 + 8 * gq), *reinterpret_cast<const u32x4*>(st + wl * SROW + 8 * gq));
           }
         }
       }

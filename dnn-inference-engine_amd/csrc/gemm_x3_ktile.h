@@ -276,13 +276,13 @@ conv3x3_x3_ktile_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __res
             q[1][e] = w1;
             q[2][e] = w2;
           }
-          bf16_bits* d = out_split + op * (3 * (size_t)N) + (n0 >> 5) * 96 + c8;
+          const size_t d = op * (3 * (size_t)N) + (n0 >> 5) * 96 + c8;
 #pragma unroll
-          for (int pc = 0; pc < 3; ++pc) *reinterpret_cast<u32x4*>(d + 32 * pc) = q[pc];
+          for (int pc = 0; pc < 3; ++pc) store16_at(out_split, 2 * (d + 32 * pc), q[pc]);
         } else {
-          float* d = out + (((size_t)b * g.H + y) * g.W + xx) * N + n0 + c8;
-          *reinterpret_cast<f32x4*>(d) = f32x4{o[0], o[1], o[2], o[3]};
-          *reinterpret_cast<f32x4*>(d + 4) = f32x4{o[4], o[5], o[6], o[7]};
+          const size_t d = (((size_t)b * g.H + y) * g.W + xx) * N + n0 + c8;
+          store16_at(out, 4 * d, __builtin_bit_cast(u32x4, f32x4{o[0], o[1], o[2], o[3]}));
+          store16_at(out, 4 * d + 16, __builtin_bit_cast(u32x4, f32x4{o[4], o[5], o[6], o[7]}));
         }
       }
     }
