@@ -394,6 +394,15 @@ __device__ __forceinline__ void store16_at(const void* base, size_t off, u32x4 v
   const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
   __builtin_amdgcn_raw_buffer_store_b128(v, rs, (unsigned)off, 0, DNN_EPI_STORE_AUX);
 }
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void store8_at(const void* base, size_t off, u32x2 v) {
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b64(v, rs, (unsigned)off, 0, DNN_EPI_STORE_AUX);
+}
+__device__ __forceinline__ void store4_at(const void* base, size_t off, float v) {
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), rs, (unsigned)off, 0, DNN_EPI_STORE_AUX);
+}
 __device__ __forceinline__ void store4(__amdgpu_buffer_rsrc_t r, unsigned off, float v) {
   __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, off, 0, 0);
 }

@@ -192,7 +192,7 @@ conv3x3_x3_lat_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __restr
   // rest of the waves' loops + these stores 4.7 us -- two waves per SIMD make a SIMD's MFMA work
   // ~10 us, and a frame's x3 conv7 is ~9 us of MFMA on all 1,024 SIMDs at 2 GHz; staging these
   // stores through LDS as whole 16-B row pieces measured the same.)
-  float* dst = part + (size_t)split * M * N;
+  const size_t dst = (size_t)split * M * N;  // (floats)
 #pragma unroll
   for (int i = 0; i < TMW; ++i) {
     if (i == TMW - 1 && tail) continue;
@@ -202,7 +202,7 @@ conv3x3_x3_lat_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __restr
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int m = m0 + 16 * (rg * TMW + i) + 4 * fq + r;
-        if (m <= mlast) dst[(size_t)m * N + n] = accm[i][jb][r];
+        if (m <= mlast) store4_at(part, 4 * (dst + (size_t)m * N + n), accm[i][jb][r]);
       }
     }
   }

@@ -223,15 +223,21 @@ __global__ void x3_combine_kernel(const float* __restrict__ part, int splits, lo
       s0[e] = a, s1[e] = b2, s2[e] = c2;
     }
     const size_t row = ((size_t)b * (g.OH + 2) + oy + 1) * (g.OW + 2) + ox + 1;
-    bf16_bits* d = out_split + row * (3 * (size_t)g.C) + (c >> 5) * 96 + (c & 31);
-    *reinterpret_cast<u16v*>(d) = s0;
-    *reinterpret_cast<u16v*>(d + 32) = s1;
-    *reinterpret_cast<u16v*>(d + 64) = s2;
+    const size_t d = 2 * (row * (3 * (size_t)g.C) + (c >> 5) * 96 + (c & 31));  // (bytes)
+    if constexpr (CPT == 8) {
+      store16_at(out_split, d, __builtin_bit_cast(u32x4, s0));
+      store16_at(out_split, d + 64, __builtin_bit_cast(u32x4, s1));
+      store16_at(out_split, d + 128, __builtin_bit_cast(u32x4, s2));
+    } else {
+      store8_at(out_split, d, __builtin_bit_cast(u32x2, s0));
+      store8_at(out_split, d + 64, __builtin_bit_cast(u32x2, s1));
+      store8_at(out_split, d + 128, __builtin_bit_cast(u32x2, s2));
+    }
   } else {
-    float* d = out + (((size_t)b * g.OH + oy) * g.OW + ox) * g.C + c;
+    const size_t d = 4 * ((((size_t)b * g.OH + oy) * g.OW + ox) * g.C + c);  // (bytes)
 #pragma unroll
     for (int v = 0; v < NV; ++v)
-      *reinterpret_cast<float4*>(d + 4 * v) = make_float4(m[4 * v], m[4 * v + 1], m[4 * v + 2], m[4 * v + 3]);
+      store16_at(out, d + 16 * v, __builtin_bit_cast(u32x4, f32x4{m[4 * v], m[4 * v + 1], m[4 * v + 2], m[4 * v + 3]}));
   }
 }
 
@@ -246,7 +252,9 @@ int launch_x3_combine(const float* part, int splits, long long slab, const EpiPa
   // many slices (> 2: latency plans): 4 channels per thread (8 measured slower there)
   const int cpt = splits > 2 && win > 0 ? 4 : 8;
   const long long total = (long long)g.B * g.OH * g.OW * (g.C / cpt);
-  if ((total + 255) / 256 > 0x7fffffffLL) {
+  const long long out_bytes = out_split ? (long long)g.B * (g.OH + 2) * (g.OW + 2) * g.C * 6
+                                        : (long long)g.B * g.OH * g.OW * g.C * 4;
+  if ((total + 255) / 256 > 0x7fffffffLL || out_bytes >= 0x80000000LL) {  // (32-bit store offsets)
     set_error("x3_combine: %lld outputs", total);
     return -2;
   }
@@ -818,7 +826,8 @@ int launch_conv_x3_lat(const bf16_bits* in_split, const bf16_bits* Bt, float* pa
   const int cpw = splits >= 1 && (K / 288) % splits == 0 ? (K / 288) / splits : 0;  // the plan's x3_lat_splits
   const long long span = M <= 0x7fffffffLL ? x3_span(M, H, W) : 1LL << 40;
   if (M % per_img != 0 || K != 9 * C || C % 32 != 0 || N % 64 != 0 || Npad != N || (cpw != 1 && cpw != 2) ||
-      in_bytes >= 0x80000000LL || b_bytes >= 0x80000000LL || span > X3_NPR || part == nullptr) {
+      in_bytes >= 0x80000000LL || b_bytes >= 0x80000000LL || span > X3_NPR || part == nullptr ||
+      (long long)splits * M * N * 4 >= 0x80000000LL) {  // (32-bit partial store offsets)
     set_error("conv_x3_lat: unsupported shape M=%lld N=%d K=%d %dx%dx%d splits=%d", M, N, K, H, W, C, splits);
     return -2;
   }

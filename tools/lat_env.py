@@ -70,6 +70,11 @@ def child(iters):
         e1.record(s)
     s.synchronize()
     out["eager_device_ms"] = round(e0.elapsed_time(e1) / 100, 4)
+    p1.timing_begin(100)
+    for _ in range(100):
+        p1.run_device(1, x.data_ptr(), y.data_ptr(), sp)
+    ms, cnt = p1.timing_end()
+    out["kernels_us"] = {k["name"]: round(1e3 * m / max(c, 1), 2) for k, m, c in zip(p1.kernels(), ms, cnt)}
     print(json.dumps(out), flush=True)
     p1.close()
 
@@ -103,7 +108,9 @@ def main():
             res[arm].append(d)
             print("round", r, arm, d, flush=True)
     for arm, v in res.items():
-        print(json.dumps({"arm": arm, **{k: statistics.median(x[k] for x in v) for k in v[0]}}), flush=True)
+        med = {k: statistics.median(x[k] for x in v) for k in v[0] if k != "kernels_us"}
+        med["kernels_us"] = {k: statistics.median(x["kernels_us"][k] for x in v) for k in v[0]["kernels_us"]}
+        print(json.dumps({"arm": arm, **med}), flush=True)
 
 
 if __name__ == "__main__":
