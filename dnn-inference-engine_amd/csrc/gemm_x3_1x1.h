@@ -27,8 +27,8 @@ __global__ void __launch_bounds__(256, 2)
 conv1x1_x3_kernel(const bf16_bits* __restrict__ in, const bf16_bits* __restrict__ Bt, float* __restrict__ out, int M,
                   int N, int K, EpiParams epi, int tilesM, X3Geom g, unsigned in_bytes, unsigned b_bytes) {
   constexpr int BM = 16 * TMW, LP = X3_1X1_LP, NS = X3_1X1_NS, RB = 192;
-  constexpr int SLOT = BM * LP;               // 7168 B per 32 rows: 7 one-KiB DMA pieces
-  constexpr int NPC = (SLOT + 1023) / 1024;   // pieces per step
+  constexpr int NPC = (BM * LP + 1023) / 1024;  // one-KiB DMA pieces per step (7 for 32 rows)
+  constexpr int SLOT = NPC * 1024;              // a step's LDS slot: whole pieces (>= BM LP)
   constexpr int PPW = (NPC + 3) / 4;          // pieces per wave per step
   __shared__ __attribute__((aligned(1024))) unsigned char smem[NS * SLOT];
 
