@@ -747,6 +747,18 @@ int dnn_plan_finalize(dnn_plan* p, int device, void* weights, void* workspace) {
       DNN_REQUIRE(L.type != 1 || L.C % 8 == 0, "dnn_plan_finalize: fp16 pool needs C %% 8 == 0 (C=%d)", L.C);
     }
   layout(p);
+  // the fused kernels' output stores take 32-bit byte offsets from their region's base (the
+  // write-through buffer stores of gemm_f32.h store16_at): every region a kernel writes, the
+  // caller's output included (at most one activation), must stay below 2 GiB
+  {
+    const unsigned long long lim = 0x80000000ULL;
+    bool ok = (unsigned long long)p->act_floats * 4 < lim && (unsigned long long)p->slab_floats * 4 < lim;
+    for (auto& L : p->layers)
+      if (L.out_padded)
+        ok = ok && (unsigned long long)p->batch * (L.out_h() + 2) * (L.out_w() + 2) * L.OC * (p->fp16 ? 2 : 6) < lim;
+    DNN_REQUIRE(ok, "dnn_plan_finalize: batch %d makes an activation region >= 2 GiB; split the batch over plans",
+                p->batch);
+  }
   DNN_HIP_TRY(hipSetDevice(device));
   p->device = device;
   if (weights) {

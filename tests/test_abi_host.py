@@ -253,6 +253,14 @@ def test_plan_errors_are_reported():
     finally:
         lib.dnn_plan_destroy(h)
     assert lib.dnn_plan_create(-1, 4, 4, 3, ctypes.byref(h)) != 0
+    # a batch whose activation region reaches 2 GiB (the fused kernels' 32-bit store offsets) is
+    # refused at finalize, before any device call
+    assert lib.dnn_plan_create(2048, 416, 416, 3, ctypes.byref(h)) == 0
+    try:
+        assert lib.dnn_plan_add_conv(h, 3, 3, 16, 1, 1, 1, None, None, None, None, None, 0.0, 1) == 0
+        assert lib.dnn_plan_finalize(h, 0, None, None) != 0 and "2 GiB" in dnn_hip.last_error()
+    finally:
+        lib.dnn_plan_destroy(h)
 
 
 def test_postprocess_api_host_checks():
