@@ -530,9 +530,18 @@ def main():
     def compute(inp, out, n):
         plan.run_device(n, inp.data_ptr(), out.data_ptr(), stream)
 
+    # each step's postprocess runs beside the NEXT forward's conv7 (a plan mark right before it):
+    # conv7's 248 one-per-CU workgroups leave 8 CUs idle for 0.7 ms, where the postprocess's 64
+    # workgroups (137 KB of LDS each, one per CU) fit, instead of taking 64 CUs from conv0 / conv1.
+    # DNN_BENCH_POST_AT=end: right after its own forward; or another kernel name
+    post_at = os.environ.get("DNN_BENCH_POST_AT", "conv7.gemm")
+    post_after = None
+    if args.gather == "detections" and post_at != "end" and post_at in [k["name"] for k in plan.kernels()]:
+        plan.set_mark(post_at)
+        post_after = plan.wait_mark
     runner = D.ShardedRunner(compute, B * world, (416, 416, 3), (13, 13, 125), dev,
                              timing=os.environ.get("DNN_BENCH_STEP_EVENTS", "1") == "1",
-                             gather_mode=os.environ.get("DNN_BENCH_GATHER_MODE", "deferred"))
+                             gather_mode=os.environ.get("DNN_BENCH_GATHER_MODE", "deferred"), post_after=post_after)
     if args.gather == "detections":
         import yolo_post
         dbufs = [yolo_post.DetectionBuffers(runner.shard_cap, dev) for _ in range(runner.slots)]

@@ -163,6 +163,10 @@ struct dnn_plan {
   // shader-clock stamps around one kernel (dnn_plan_clock_begin): run r's stamps of the opening
   // launch at clk_buf + 2 r nwg 4, of the closing launch 4 nwg further (clock.hip)
   int clk_kernel = -1, clk_cap = 0, clk_used = 0, clk_nwg = 0;
+  // mark: an event recorded on the run stream right before kernel `mark_kernel` of every run
+  // (dnn_plan_set_mark / dnn_plan_wait_mark)
+  int mark_kernel = -1;
+  hipEvent_t mark_ev = nullptr;
   bool clk_open = false;
   unsigned long long* clk_buf = nullptr;
   // captured forward (dnn_plan_run_graph)
@@ -314,6 +318,7 @@ void dnn_plan_destroy(dnn_plan* p) {
   if (p->device >= 0) (void)hipSetDevice(p->device);
   drop_graph(p);
   for (auto e : p->ev) (void)hipEventDestroy(e);
+  if (p->mark_ev) (void)hipEventDestroy(p->mark_ev);
   if (p->own_weights && p->weights) (void)hipFree(p->weights);
   if (p->own_ws && p->ws) (void)hipFree(p->ws);
   if (p->h_in_dev) (void)hipFree(p->h_in_dev);
@@ -807,6 +812,7 @@ static int record_events(dnn_plan* p, int kernel, hipStream_t s);
 // stamp after the event that closes it, so an event-timed kernel never contains a stamp launch
 static int record(dnn_plan* p, int kernel, hipStream_t s) {
   int rc;
+  if (p->mark_kernel >= 0 && kernel == p->mark_kernel) DNN_HIP_TRY(hipEventRecord(p->mark_ev, s));
   const bool close_now = p->clk_open;
   if (!close_now && p->clk_kernel >= 0 && kernel == p->clk_kernel && p->clk_used < p->clk_cap) {
     if ((rc = launch_clock_stamp(s, p->clk_buf + (size_t)p->clk_used * 8 * p->clk_nwg, p->clk_nwg))) return rc;
@@ -1084,6 +1090,7 @@ int dnn_plan_run_graph(dnn_plan* p, int n, const float* d_in, float* d_out, void
   DNN_REQUIRE(stream != nullptr, "dnn_plan_run_graph: needs a created stream (NULL cannot be captured)");
   DNN_REQUIRE(!p->timing, "dnn_plan_run_graph: per-kernel timing is active");
   DNN_REQUIRE(p->clk_kernel < 0, "dnn_plan_run_graph: clock stamping is active");
+  DNN_REQUIRE(p->mark_kernel < 0, "dnn_plan_run_graph: a mark is set");
   DNN_REQUIRE(n >= 0 && n <= p->batch, "dnn_plan_run_graph: n=%d outside [0, %d]", n, p->batch);
   if (n == 0) return 0;
   hipStream_t s = static_cast<hipStream_t>(stream);
@@ -1188,6 +1195,24 @@ int dnn_plan_clock_begin(dnn_plan* p, int kernel_idx, unsigned long long* dev_bu
   p->clk_nwg = nwg;
   p->clk_used = 0;
   p->clk_open = false;
+  return 0;
+}
+
+int dnn_plan_set_mark(dnn_plan* p, int kernel_idx) {
+  DNN_REQUIRE(p && p->finalized, "dnn_plan_set_mark: plan not finalized");
+  DNN_REQUIRE(kernel_idx >= -1 && kernel_idx < (int)p->kernels.size(), "dnn_plan_set_mark: bad kernel index %d",
+              kernel_idx);
+  if (kernel_idx >= 0 && !p->mark_ev) {
+    DNN_HIP_TRY(hipSetDevice(p->device));
+    DNN_HIP_TRY(hipEventCreateWithFlags(&p->mark_ev, hipEventDisableTiming));
+  }
+  p->mark_kernel = kernel_idx;
+  return 0;
+}
+
+int dnn_plan_wait_mark(dnn_plan* p, void* stream) {
+  DNN_REQUIRE(p && p->mark_kernel >= 0 && p->mark_ev, "dnn_plan_wait_mark: no mark set");
+  DNN_HIP_TRY(hipStreamWaitEvent(static_cast<hipStream_t>(stream), p->mark_ev, 0));
   return 0;
 }
 

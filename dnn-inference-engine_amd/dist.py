@@ -330,8 +330,13 @@ class ShardedRunner(object):
     """
 
     def __init__(self, compute, global_batch, in_shape, out_shape, device, dtype=torch.float32, timing=True,
-                 slots=None, gather_mode="deferred"):
+                 slots=None, gather_mode="deferred", post_after=None):
         self.timing = bool(timing)  # per-step HIP timing events for stats()
+        # post_after(stream_ptr) (pipelined path, optional): a step's postprocess is enqueued right
+        # after the NEXT step's forward, on the post stream made to wait by post_after -- e.g. for a
+        # mark inside that forward (Plan.wait_mark) -- so it runs beside the next forward's late
+        # layers instead of its first ones.  The last step's is enqueued at its finish.
+        self.post_after = post_after
         if gather_mode not in DetectionGather.MODES:
             raise ValueError(f"gather_mode {gather_mode!r}")
         self.gather_mode = gather_mode  # DetectionGather mode of the pipelined path
@@ -388,26 +393,43 @@ class ShardedRunner(object):
             # streams and the null stream; tools/stream_queue_probe.py), so neither the
             # postprocess nor the gather can end up serialised behind later forwards
             self._side = _HostStream() if host else torch.cuda.Stream(dev, priority=-1)
-            self._post = _HostStream() if host else torch.cuda.Stream(dev, priority=-1)
+            self._post = _HostStream() if host else torch.cuda.Stream(
+                dev, priority=int(os.environ.get("DNN_POST_STREAM_PRIORITY", "-1")))  # (A/B)
             self._freed = [None] * self.slots
             self._gather = None
             self._deferred = None
+            self._post_wait = None  # post_after: the step whose postprocess awaits the next forward
             self.reset_stats()
         cur = _HostStream() if host else torch.cuda.current_stream(dev)
         if self._freed[slot] is not None:
             cur.wait_event(self._freed[slot])
         # ev: 0/1 forward, 2 pack done, 3 gather enqueued (deferred: the size exchange), 4 gather
-        # done, 5 payload gather start (deferred mode; the same point as 3 otherwise)
-        ev = [_HostEvent() if host else torch.cuda.Event(enable_timing=self.timing) for _ in range(6)]
+        # done, 5 payload gather start (deferred mode; the same point as 3 otherwise), 6 post start
+        ev = [_HostEvent() if host else torch.cuda.Event(enable_timing=self.timing) for _ in range(7)]
         out = self._outs[slot]
         ev[0].record(cur)
         self.compute(local_in, out, self.count)
         ev[1].record(cur)
+        h = [slot, None, None, None, ev, (out, post)]  # packed / total / counts once its post is enqueued
+        if self.post_after is None:
+            self._enqueue_post(h, None)
+        else:
+            if self._post_wait is not None:  # the previous step's, beside this forward's late layers
+                self._enqueue_post(self._post_wait, None if host else self.post_after)
+            self._post_wait = h
+        return h
+
+    def _enqueue_post(self, h, after):
+        slot, ev = h[0], h[4]
+        out, post = h[5]
         self._post.wait_event(ev[1])
         with self._on(self._post):
-            packed, total, counts = post(out, self.count, slot, self._post.cuda_stream)
+            if after is not None:
+                after(self._post.cuda_stream)
+            ev[6].record(self._post)
+            h[1], h[2], h[3] = post(out, self.count, slot, self._post.cuda_stream)
             ev[2].record(self._post)
-        return slot, packed, total, counts, ev
+        h[5] = None
 
     @staticmethod
     def _on(stream):
@@ -426,7 +448,11 @@ class ShardedRunner(object):
         "deferred" — this call enqueues this step's size exchange and completes the PREVIOUS
         step's gather (sizes read a step after their exchange), returning the previous
         step's detections; flush_detections() completes the last one."""
-        slot, packed, total, counts, ev = handle
+        if handle[5] is not None:  # post_after: the last step's postprocess, after its own forward
+            if self._post_wait is handle:
+                self._post_wait = None
+            self._enqueue_post(handle, None)
+        slot, packed, total, counts, ev = handle[:5]
         if self._gather is None:
             self._gather = DetectionGather(self.shard_cap, packed.shape[0], self.out.device,
                                            slots=self.slots, mode=self.gather_mode)
@@ -494,7 +520,7 @@ class ShardedRunner(object):
                 if force:
                     e[4].synchronize()
                 self._sums[0] += e[0].elapsed_time(e[1])
-                self._sums[1] += e[1].elapsed_time(e[2])
+                self._sums[1] += e[6].elapsed_time(e[2])
                 self._sums[2] += e[5].elapsed_time(e[4])
                 self._sums[3] += e[3].elapsed_time(e[4])
 

@@ -74,6 +74,8 @@ def _bind_plan_api(lib):
         "dnn_clock_stamp": (i, [vp, vp, i]),
         "dnn_plan_clock_begin": (i, [vp, i, vp, i, i]),
         "dnn_plan_clock_end": (i, [vp, P(i)]),
+        "dnn_plan_set_mark": (i, [vp, i]),
+        "dnn_plan_wait_mark": (i, [vp, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -693,6 +695,15 @@ class Plan(object):
         runs = ctypes.c_int()
         _check(self.lib.dnn_plan_clock_end(self.h, ctypes.byref(runs)), "clock_end", self.lib)
         return runs.value
+
+    def set_mark(self, kernel):
+        """Record an event right before `kernel` (a kernel name; None: off) in every later run
+        (dnn_plan_set_mark); wait_mark(stream) makes a stream wait for the latest run's mark."""
+        idx = -1 if kernel is None else [k["name"] for k in self.kernels()].index(kernel)
+        _check(self.lib.dnn_plan_set_mark(self.h, idx), "set_mark", self.lib)
+
+    def wait_mark(self, stream_ptr):
+        _check(self.lib.dnn_plan_wait_mark(self.h, ctypes.c_void_p(stream_ptr)), "wait_mark", self.lib)
 
     def close(self):
         if getattr(self, "h", None):

@@ -132,6 +132,14 @@ int dnn_clock_stamp(void* stream, unsigned long long* dev_out, int nwg);
 int dnn_plan_clock_begin(dnn_plan* plan, int kernel_idx, unsigned long long* dev_buf, int max_runs, int nwg);
 int dnn_plan_clock_end(dnn_plan* plan, int* runs);
 
+/* Mark inside a run (scheduling other streams' work beside a forward's later layers).
+ * dnn_plan_set_mark: from now on every run records an event on its stream right before kernel
+ * `kernel_idx` (-1: off; not with dnn_plan_run_graph).
+ * dnn_plan_wait_mark: makes `stream` wait for the mark of the most recent run enqueued (the
+ * usual stream-wait-event semantics: a later run's mark does not affect an earlier wait). */
+int dnn_plan_set_mark(dnn_plan* plan, int kernel_idx);
+int dnn_plan_wait_mark(dnn_plan* plan, void* stream);
+
 #pragma GCC visibility pop
 #ifdef __cplusplus
 }

@@ -151,7 +151,7 @@ def test_sharded_detection_gather_gloo(world, total, mode):
     assert len(others) == world - 1 and all(r[2] is True for r in others)
 
 
-def _pipe_worker(rank, world, port, total, steps, q):
+def _pipe_worker(rank, world, port, total, steps, q, defer_post=False):
     for p in (REPO, PKG, ORACLE):
         sys.path.insert(0, p)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
@@ -181,7 +181,8 @@ def _pipe_worker(rank, world, port, total, steps, q):
             return (torch.from_numpy(packed.view(np.uint8).reshape(-1, 40)), torch.tensor([p], dtype=torch.int32),
                     torch.from_numpy(counts))
 
-        runner = Dw.ShardedRunner(compute, total, (13, 13, 125), (13, 13, 125), device="cpu")
+        runner = Dw.ShardedRunner(compute, total, (13, 13, 125), (13, 13, 125), device="cpu",
+                                  post_after=(lambda stream: None) if defer_post else None)
         assert runner.gather_mode == "deferred" and runner.inflight == runner.slots - 1
         pending, got, firsts = [], [], []
         for k in range(steps):  # bench.py's loop: finish step k - inflight + 1 after launching step k
@@ -213,17 +214,20 @@ def _pipe_worker(rank, world, port, total, steps, q):
         torch.distributed.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,total,steps", [(2, 7, 6), (8, 11, 5)])
-def test_pipelined_runner_deferred_order_gloo(world, total, steps):
+@pytest.mark.parametrize("world,total,steps,defer_post", [(2, 7, 6, False), (8, 11, 5, False), (2, 7, 6, True),
+                                                         (8, 11, 5, True), (2, 5, 1, True)])
+def test_pipelined_runner_deferred_order_gloo(world, total, steps, defer_post):
     """ShardedRunner's pipelined path with its default gather ("deferred"): driven as
     bench.py drives it (launch step k into slot k % slots, finish the oldest once `inflight` steps
     are pending, then drain and flush), rank 0 receives every step's detections exactly once and
     in step order: the first finish returns nothing (its sizes are read one finish later) and
-    flush_detections() returns the last step; non-root ranks receive nothing."""
+    flush_detections() returns the last step; non-root ranks receive nothing.  defer_post: each
+    step's postprocess enqueued after the next step's forward (post_after, bench.py's default),
+    the last one at its finish -- the same detections in the same order."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_pipe_worker, args=(r, world, port, total, steps, q)) for r in range(world)]
+    procs = [ctx.Process(target=_pipe_worker, args=(r, world, port, total, steps, q, defer_post)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=240) for _ in range(world)]
