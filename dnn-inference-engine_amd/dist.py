@@ -393,8 +393,7 @@ class ShardedRunner(object):
             # streams and the null stream; tools/stream_queue_probe.py), so neither the
             # postprocess nor the gather can end up serialised behind later forwards
             self._side = _HostStream() if host else torch.cuda.Stream(dev, priority=-1)
-            self._post = _HostStream() if host else torch.cuda.Stream(
-                dev, priority=int(os.environ.get("DNN_POST_STREAM_PRIORITY", "-1")))  # (A/B)
+            self._post = _HostStream() if host else torch.cuda.Stream(dev, priority=-1)
             self._freed = [None] * self.slots
             self._gather = None
             self._deferred = None
