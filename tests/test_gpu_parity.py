@@ -2321,31 +2321,3 @@ def test_x3_split_total_over_finite_fp32(monkeypatch, kind):
         print("%s x3=%s normwise err %.3e" % (kind, x3, errs[x3]))
     assert errs["1"] < LAYER_TOL and errs["0"] < LAYER_TOL, errs
     assert errs["1"] <= max(1.25 * errs["0"], 2e-7), errs
-
-
-@pytest.mark.gpu
-def test_plan_starting_at_16_channels_equals_the_whole_plan(yolo_weights):
-    """YOLO split into two plans -- conv0 + pool0, then conv1..conv8 starting at the 16-channel
-    layer (on the x3 kernel, which reads the first plan's fp32 output) -- gives the whole plan's
-    output bit for bit: the same kernels in the same order."""
-    import torch
-    B = 2
-    g, _ = yolo_graph.build_graph(dnn_hip.DnnGraphBuilder, yolo_weights, in_shape=(B, 416, 416, 3))
-    entries = dnn_hip.lower_graph(g)
-    dev = torch.device("cuda", 0)
-    whole = dnn_hip.Plan(B, (416, 416, 3), entries, device=0)
-    head = dnn_hip.Plan(B, (416, 416, 3), entries[:2], device=0)
-    rest = dnn_hip.Plan(B, (208, 208, 16), entries[2:], device=0)
-    assert "mode=patch_x3" in rest.describe().splitlines()[0]
-    x = torch.from_numpy(synth.frame(0)).to(dev).expand(B, 416, 416, 3).contiguous()
-    mid = torch.empty((B, 208, 208, 16), device=dev)
-    y1 = torch.empty((B, 13, 13, 125), device=dev)
-    y2 = torch.empty_like(y1)
-    s = torch.cuda.current_stream().cuda_stream
-    whole.run_device(B, x.data_ptr(), y1.data_ptr(), s)
-    head.run_device(B, x.data_ptr(), mid.data_ptr(), s)
-    rest.run_device(B, mid.data_ptr(), y2.data_ptr(), s)
-    torch.cuda.synchronize()
-    assert torch.equal(y1, y2)
-    for p in (whole, head, rest):
-        p.close()
