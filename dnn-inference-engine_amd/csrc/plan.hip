@@ -456,8 +456,7 @@ int dnn_plan_add_conv(dnn_plan* p, int kh, int kw, int od, int stride_h, int str
   // columns x one or two chunks per workgroup, 8 waves splitting rows / columns / chunks;
   // conv6 / conv7 of a one-frame plan) when it makes at least two K slices
   bool x3_cand = false, x3_lat = false, x3_k = false;
-  // (a plan's first layer only as the 16-channel kernel, which reads fp32 input)
-  if (!p->fp16 && L.mode == MODE_IMPLICIT && (!p->layers.empty() || L.C == 16)) {
+  if (!p->fp16 && L.mode == MODE_IMPLICIT && !p->layers.empty()) {
     const bool batch_ok = conv_x3_supported(L.C, od, L.H, L.W, L.OH, L.OW, kh, kw, stride_h, stride_w, L.pt, L.pl);
     // (the narrow kernels take small tiles in latency plans: batch_ok is enough.  conv1 at one
     // frame: the 16-channel kernel's 4 x 26 tiles 10.6 us, its 16 x 26 ones 11.7, the fp32 patch
@@ -500,18 +499,16 @@ int dnn_plan_add_conv(dnn_plan* p, int kh, int kw, int od, int stride_h, int str
     // producers that can write the split planes: a separate pool, another x3 conv, a pool-fused
     // implicit GEMM without split-K (its epilogue splits, EPI_OUT_X3) or the pool-fused patch
     // conv (conv1)
+    PlanLayer& prev = p->layers.back();
     if (L.C == 16) {  // the 16-channel x3 kernel reads the producer's fp32 output (conv1)
       L.mode = MODE_X3;
-    } else {
-      PlanLayer& prev = p->layers.back();
-      if ((prev.type == 1 && prev.C % 32 == 0) || (prev.type == 0 && prev.mode == MODE_X3) ||
-          (prev.type == 0 && prev.mode == MODE_IMPLICIT && prev.pool && prev.splits == 1) ||
-          (prev.type == 0 && prev.mode == MODE_PATCH && prev.pool)) {
-        L.mode = MODE_X3;
-        L.x3lat = x3_lat;
-        L.x3k = x3_k;
-        prev.out_padded = true;
-      }
+    } else if ((prev.type == 1 && prev.C % 32 == 0) || (prev.type == 0 && prev.mode == MODE_X3) ||
+        (prev.type == 0 && prev.mode == MODE_IMPLICIT && prev.pool && prev.splits == 1) ||
+        (prev.type == 0 && prev.mode == MODE_PATCH && prev.pool)) {
+      L.mode = MODE_X3;
+      L.x3lat = x3_lat;
+      L.x3k = x3_k;
+      prev.out_padded = true;
     }
   }
   set_cfg(p, L);

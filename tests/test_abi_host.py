@@ -240,24 +240,6 @@ def test_plan_x3_structure_host_only(monkeypatch):
     assert [i for i, ln in enumerate(conv) if "patch_x3" in ln] == [2, 3, 4, 6, 7] and "mode=patch " in conv[1] + " "
 
 
-def test_first_layer_16_channels_takes_the_x3_kernel():
-    """A plan that starts at a 16-channel 3x3 conv (YOLO's conv1 as a plan's first layer) runs it on
-    the 16-channel x3 kernel, which reads the fp32 input itself, like conv1 after conv0."""
-    lib = dnn_hip.mylib
-    h = ctypes.c_void_p()
-    assert lib.dnn_plan_create(64, 208, 208, 16, ctypes.byref(h)) == 0
-    try:
-        assert lib.dnn_plan_add_conv(h, 3, 3, 32, 1, 1, 1, None, None, None, None, None, 0.0, 1) == 0
-        assert lib.dnn_plan_add_max_pool(h, 2, 2, 2, 2, 1) == 0
-        assert lib.dnn_plan_add_conv(h, 3, 3, 64, 1, 1, 1, None, None, None, None, None, 0.0, 1) == 0
-        buf = ctypes.create_string_buffer(4096)
-        assert lib.dnn_plan_describe(h, buf, 4096) == 0
-        lines = buf.value.decode().splitlines()
-        assert "mode=patch_x3" in lines[0] and "+pool2x2s2" in lines[0] and "mode=patch_x3" in lines[1], lines
-    finally:
-        lib.dnn_plan_destroy(h)
-
-
 def test_plan_errors_are_reported():
     lib = dnn_hip.mylib
     h = ctypes.c_void_p()
